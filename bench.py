@@ -1,0 +1,218 @@
+"""Throughput benchmark of the MI355X render loop (BASELINE.json metric).
+
+metric : Mray/s (primary + secondary) -- closest-hit queries + shadow queries
+         (calls equivalent to KDTree::intersectRay / intersectShadowRay) per second
+         of wall time around the render steps.
+step   : one progressive layer of the whole frame of the config at its spp
+         (default: sponza stand-in 1920x1080 x 128 spp, k = 6).  Scene load, kd
+         build and upload happen before the timed region; the scene is resident in
+         HBM when the clock starts.  For N > 1 the frame is tile-split over ranks
+         (tile t -> rank t mod N) and each step ends with a torch.distributed
+         gather of the per-rank tile buffers to rank 0 (RCCL over xGMI) and the
+         root-side unpermute + progressive blend, all inside the timed region.
+
+Prints ONE JSON line on rank 0 with the contract fields plus "roofline" (render
+kernel, algorithmic bytes per SURVEY §8d / HIP-event kernel time vs 8 TB/s HBM)
+and "cpu_baseline" (the oracle's OpenMP restatement on a bounded row sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "chiaroscuro-raytracer_amd"))
+os.environ.setdefault("CHIARO_QUIET", "1")
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(pair_tris, info, leaf, cam, xres, yres, spp, k, seed, budget_s):
+    """Oracle restatement (OpenMP over rows, dynamic schedule) on a row sample."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle as po
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    osc = po.OracleScene(pair_tris, leaf_size=leaf, build_threads=threads)
+    log("cpu_baseline: oracle kd build %.1fs" % (time.time() - t0))
+    # calibrate on every 8th row at 1 spp, then size (rows, spp) to ~budget_s
+    step = 8
+    t0 = time.time()
+    osc.render(cam, xres, yres, 1, k, seed, y0=0, y1=yres, ystep=step, threads=threads)
+    dt = max(time.time() - t0, 1e-3)
+    rows = (yres + step - 1) // step
+    per_row_spp = dt / rows
+    work = budget_s / per_row_spp                   # affordable row-samples
+    s_spp = int(max(1, min(spp, work // yres)))     # whole frame if it fits, more spp if time allows
+    nrows = int(max(1, min(yres, work // s_spp)))
+    ystep = max(1, yres // nrows)
+    t0 = time.time()
+    _, c = osc.render(cam, xres, yres, s_spp, k, seed, y0=0, y1=yres, ystep=ystep, threads=threads)
+    dt = time.time() - t0
+    nr = (yres + ystep - 1) // ystep
+    rays = c["closest"] + c["shadow"]
+    return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": "oracle/liboracle.so (OpenMP rows, dynamic), %d of %d rows (every %d-th) x %d px x %d spp "
+                      "of the same frame/seed, %d rays in %.1f s" % (nr, yres, ystep, xres, s_spp, rays, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="sponza", help="cornell | cornell_box | sponza | sponza_4k")
+    ap.add_argument("--spp", type=int, default=0, help="override samples per step (default: config's)")
+    ap.add_argument("--kernel", type=int, default=-1)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import chiaroscuro_amd as ca
+    from chiaroscuro_amd import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev_index = local
+    torch.cuda.set_device(dev_index)
+
+    rtc = scenes.config_rtc(args.config)
+    t0 = time.time()
+    scene = ca.Scene(rtc)
+    info = scene.info
+    model = ca.Model(scene)
+    kd = ca.KDTree(model, scene)
+    dev = ca.Device(dev_index)
+    dev.upload(kd.describe())
+    if args.kernel >= 0:
+        dev.set_option("kernel", args.kernel)
+    if rank == 0:
+        log("scene %s: %d tris, load+kd+upload %.1fs" % (args.config, model.num_triangles, time.time() - t0))
+    xres, yres, k, seed = info["xres"], info["yres"], info["k"], info["seed"]
+    spp = args.spp or info["samples"]
+    cam = ca.camera(info["VP"], info["LA"], info["UP"], info["yview"], xres, yres)
+    tile = 32
+    stream = torch.cuda.current_stream().cuda_stream
+    frame = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda")
+    p0 = ca.render_params(xres, yres, spp, k, seed, nranks=world, tile=tile)
+    max_tiles = ca.Device.tiles_for_rank(p0, 0)
+    tiles = torch.zeros((max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda") if world > 1 else None
+    gathered = (torch.zeros((world, max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda")
+                if world > 1 and rank == 0 else None)
+
+    totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0}
+
+    def step(layer, record):
+        p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
+        if world == 1:
+            dev.render_device(cam, p, frame.data_ptr(), stream)
+        else:
+            dev.render_tiles_device(cam, p, tiles.data_ptr(), stream)
+            dist.gather(tiles, [gathered[r] for r in range(world)] if rank == 0 else None, dst=0)
+            if rank == 0:
+                dev.blend_tiles_device(p, gathered.data_ptr(), frame.data_ptr(), stream)
+        if record:
+            c = dev.counters()
+            totals["rays"] += c["closest"] + c["shadow"]
+            totals["kernel_ms"] += dev.last_kernel_ms()
+            totals["bytes"] += ca.algorithmic_bytes(c, c["pixels"])
+            totals["tritest"] += c["tritest"]
+            totals["px"] += c["pixels"]
+            totals["launches"] += 1
+
+    layer = 1
+    for w in range(args.warmup):
+        step(layer, False)
+        layer += 1
+        if rank == 0:
+            log("warmup %d done" % w)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(layer, True)
+        layer += 1
+        if rank == 0:
+            log("step %d: %.3fs elapsed" % (s, time.perf_counter() - t0))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([totals["rays"], totals["bytes"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(r)
+        rays_all = float(r[0].item())
+    else:
+        rays_all = float(totals["rays"])
+
+    if rank == 0:
+        value = rays_all / elapsed / 1e6
+        kms = totals["kernel_ms"] / max(totals["launches"], 1)
+        bytes_per_launch = totals["bytes"] / max(totals["launches"], 1)
+        achieved = bytes_per_launch / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+        traffic = None
+        pmc = ROOT / "profiles" / ("pmc_%s.json" % args.config)
+        if pmc.exists():
+            try:
+                traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(model.triangles(), info, info["leaf_size"], cam.as_array(), xres, yres, spp, k, seed,
+                               args.cpu_budget)
+        label = {"sponza": "sponza_standin (Sponza-Crytek stand-in, ~261k tris) 1920x1080",
+                 "sponza_4k": "sponza_standin (Sponza-Crytek stand-in) 3840x2160",
+                 "cornell": "cornell_unit 256x256", "cornell_box": "cornell_box_lit 1024x1024"}[args.config]
+        out = {
+            "metric": "Mray/s (primary+secondary) on sponza_crytek 1080p; 1/2/4/8-GPU scaling",
+            "value": round(value, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",  # one fixed frame, tile-split over the ranks
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic scene (deterministic generator), seeded counter RNG",
+            "config": {"workload": label, "spp_per_step": spp, "k": k, "tile": tile,
+                       "parallelism": "tile-split x%d" % world, "rays": int(rays_all),
+                       "mean_tritest_per_ray": round(totals["tritest"] / max(totals["rays"], 1), 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "render", "kernel_ms": round(kms, 3),
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,456 @@
+"""chiaroscuro_amd -- Python side of the MI355X path-tracing core.
+
+Thin ctypes bindings over the two in-tree shared libraries:
+
+* ``lib/libchiaro_hip.so``  -- the HIP kernels behind the C-ABI of
+  ``include/chiaro_hip.h`` (the drop-in boundary of the render loop);
+* ``lib/libchiaroscuro.so`` -- the host mirror of the reference's C++ classes
+  ``Scene`` / ``Model`` / ``KDTree`` / ``RayTracer`` (``include/chiaroscuro.h``).
+
+The Python names mirror the reference API (``RayTracer.rayTrace``,
+``getData``, ``maxVal``, ``normalizeImage``, ``exportImage``).  There is no CPU
+fallback: if the libraries are missing, or no GPU is present, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parent.parent
+LIB_DIR = PKG_ROOT / "lib"
+
+CR_OK = 0
+CR_ERRORS = {-1: "CR_E_INVALID", -2: "CR_E_HIP", -3: "CR_E_NOSCENE", -4: "CR_E_DEPTH", -5: "CR_E_OOM"}
+
+f3 = C.c_float * 3
+
+
+class CrCamera(C.Structure):
+    _fields_ = [("eye", f3), ("left_upper", f3), ("dx", f3), ("dy", f3)]
+
+    def as_array(self) -> np.ndarray:
+        return np.array(list(self.eye) + list(self.left_upper) + list(self.dx) + list(self.dy), dtype=np.float32)
+
+
+class CrRenderParams(C.Structure):
+    _fields_ = [("xres", C.c_uint32), ("yres", C.c_uint32), ("spp", C.c_uint32), ("k", C.c_int32),
+                ("background", f3), ("seed", C.c_uint32), ("layer", C.c_uint32), ("rank", C.c_uint32),
+                ("nranks", C.c_uint32), ("tile", C.c_uint32)]
+
+
+COUNTER_NAMES = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths", "pixels")
+
+
+class CrCounters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_NAMES]
+
+    def as_dict(self) -> dict:
+        return {n: int(getattr(self, n)) for n in COUNTER_NAMES}
+
+
+class CrKdNode(C.Structure):
+    _fields_ = [("split", C.c_float), ("axis", C.c_uint32), ("child_or_first", C.c_uint32), ("count", C.c_uint32)]
+
+
+class CrTexture(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("components", C.c_int32),
+                ("data", C.POINTER(C.c_uint8))]
+
+
+class CrSceneDesc(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("nodes", C.POINTER(CrKdNode)), ("n_refs", C.c_uint32),
+                ("refs", C.POINTER(C.c_uint32)), ("max_depth", C.c_uint32), ("box_min", f3), ("box_max", f3),
+                ("n_tris", C.c_uint32), ("tri_pos", C.POINTER(C.c_float)), ("tri_normal", C.POINTER(C.c_float)),
+                ("tri_kd", C.POINTER(C.c_float)), ("tri_ke", C.POINTER(C.c_float)),
+                ("tri_uv", C.POINTER(C.c_float)), ("tri_tex", C.POINTER(C.c_int32)),
+                ("tri_emissive", C.POINTER(C.c_uint8)), ("n_lights", C.c_uint32),
+                ("light_id", C.POINTER(C.c_uint32)), ("light_surface", C.POINTER(C.c_float)),
+                ("n_textures", C.c_uint32), ("textures", C.POINTER(CrTexture))]
+
+
+class ChiaroSceneInfo(C.Structure):
+    _fields_ = [("xres", C.c_uint32), ("yres", C.c_uint32), ("samples", C.c_uint32),
+                ("preview_height", C.c_uint32), ("leaf_size", C.c_uint32), ("seed", C.c_uint32),
+                ("k", C.c_int32), ("using_preview", C.c_int32), ("VP", f3), ("LA", f3), ("UP", f3),
+                ("background", f3), ("yview", C.c_float), ("exposure", C.c_float), ("n_invalid", C.c_uint32),
+                ("obj_path", C.c_char * 1024), ("render_path", C.c_char * 1024)]
+
+
+# --------------------------------------------------------------- loading --
+_hip = None
+_host = None
+
+# Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
+HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
+               "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_intersect",
+               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_set_option", "cr_synchronize")
+HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
+                "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
+                "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
+                "chiaro_model_destroy", "chiaro_kdtree_create", "chiaro_kdtree_num_nodes", "chiaro_kdtree_num_refs",
+                "chiaro_kdtree_export", "chiaro_kdtree_describe", "chiaro_kdtree_destroy",
+                "chiaro_raytracer_create", "chiaro_raytracer_raytrace", "chiaro_raytracer_pixels",
+                "chiaro_raytracer_data", "chiaro_raytracer_maxval", "chiaro_raytracer_layers",
+                "chiaro_raytracer_counters", "chiaro_raytracer_normalize", "chiaro_raytracer_export",
+                "chiaro_raytracer_ctx", "chiaro_raytracer_destroy", "chiaro_camera")
+
+P = C.c_void_p
+FP = C.POINTER(C.c_float)
+UP = C.POINTER(C.c_uint32)
+
+
+def _sig(lib, name, res, args):
+    fn = getattr(lib, name)
+    fn.restype = res
+    fn.argtypes = args
+
+
+def libs():
+    """Load (once) and return (libchiaro_hip, libchiaroscuro).  Raises if not built."""
+    global _hip, _host
+    if _hip is not None:
+        return _hip, _host
+    hip_path, host_path = LIB_DIR / "libchiaro_hip.so", LIB_DIR / "libchiaroscuro.so"
+    if not hip_path.exists() or not host_path.exists():
+        raise RuntimeError("chiaroscuro_amd: native libraries not built (%s); run "
+                           "`make -C chiaroscuro-raytracer_amd` or __graft_entry__.build()" % LIB_DIR)
+    hip = C.CDLL(str(hip_path), mode=C.RTLD_GLOBAL)
+    host = C.CDLL(str(host_path))
+    _sig(hip, "cr_create", P, [C.c_int])
+    _sig(hip, "cr_destroy", None, [P])
+    _sig(hip, "cr_last_error", C.c_char_p, [P])
+    _sig(hip, "cr_upload_scene", C.c_int, [P, C.POINTER(CrSceneDesc)])
+    _sig(hip, "cr_render", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), FP])
+    _sig(hip, "cr_render_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
+    _sig(hip, "cr_render_tiles_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
+    _sig(hip, "cr_blend_tiles_device", C.c_int, [P, C.POINTER(CrRenderParams), P, P, P])
+    _sig(hip, "cr_tiles_for_rank", C.c_uint32, [C.POINTER(CrRenderParams), C.c_uint32])
+    _sig(hip, "cr_intersect", C.c_int, [P, C.c_uint32, FP, FP, UP, UP, FP, FP])
+    _sig(hip, "cr_intersect_shadow", C.c_int, [P, C.c_uint32, FP, FP, FP, UP, UP])
+    _sig(hip, "cr_get_counters", C.c_int, [P, C.POINTER(CrCounters)])
+    _sig(hip, "cr_last_kernel_ms", C.c_float, [P])
+    _sig(hip, "cr_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
+    _sig(hip, "cr_synchronize", C.c_int, [P])
+
+    _sig(host, "chiaro_last_error", C.c_char_p, [])
+    _sig(host, "chiaro_scene_create", P, [C.c_int, C.POINTER(C.c_char_p)])
+    _sig(host, "chiaro_scene_info_get", C.c_int, [P, C.POINTER(ChiaroSceneInfo)])
+    _sig(host, "chiaro_scene_destroy", None, [P])
+    _sig(host, "chiaro_model_create", P, [P])
+    _sig(host, "chiaro_model_load", P, [C.c_char_p])
+    for n in ("chiaro_model_num_meshes", "chiaro_model_num_triangles", "chiaro_model_num_textures"):
+        _sig(host, n, C.c_uint32, [P])
+    _sig(host, "chiaro_model_triangles", C.c_int, [P, FP, FP, FP, FP, FP, C.POINTER(C.c_int32)])
+    _sig(host, "chiaro_model_texture", C.c_int,
+         [P, C.c_uint32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+          C.POINTER(C.POINTER(C.c_uint8))])
+    _sig(host, "chiaro_model_destroy", None, [P])
+    _sig(host, "chiaro_kdtree_create", P, [P, P, C.c_int])
+    _sig(host, "chiaro_kdtree_num_nodes", C.c_uint32, [P])
+    _sig(host, "chiaro_kdtree_num_refs", C.c_uint32, [P])
+    _sig(host, "chiaro_kdtree_export", C.c_int, [P, UP, UP, FP, UP, UP, UP, UP, FP])
+    _sig(host, "chiaro_kdtree_describe", C.c_int, [P, P, C.POINTER(CrSceneDesc)])
+    _sig(host, "chiaro_kdtree_destroy", None, [P])
+    _sig(host, "chiaro_raytracer_create", P, [P, P, C.c_int])
+    _sig(host, "chiaro_raytracer_raytrace", C.c_int, [P, FP, FP, FP, C.c_float])
+    _sig(host, "chiaro_raytracer_pixels", FP, [P])
+    _sig(host, "chiaro_raytracer_data", C.POINTER(C.c_uint8), [P])
+    _sig(host, "chiaro_raytracer_maxval", C.c_float, [P])
+    _sig(host, "chiaro_raytracer_layers", C.c_uint32, [P])
+    _sig(host, "chiaro_raytracer_counters", C.c_int, [P, C.POINTER(CrCounters)])
+    _sig(host, "chiaro_raytracer_normalize", C.c_int, [P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float])
+    _sig(host, "chiaro_raytracer_export", C.c_int, [P, C.c_char_p])
+    _sig(host, "chiaro_raytracer_ctx", P, [P])
+    _sig(host, "chiaro_raytracer_destroy", None, [P])
+    _sig(host, "chiaro_camera", C.c_int, [FP, FP, FP, C.c_float, C.c_uint32, C.c_uint32, C.POINTER(CrCamera)])
+    _hip, _host = hip, host
+    return hip, host
+
+
+def _fa(v) -> C.Array:
+    return (C.c_float * 3)(*[float(x) for x in v])
+
+
+def _ptr(a: np.ndarray, t=C.c_float):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def _host_err() -> str:
+    return libs()[1].chiaro_last_error().decode()
+
+
+# ------------------------------------------------------------------ camera --
+def camera(eye, center, up, yview, xres, yres) -> CrCamera:
+    """Camera basis exactly as src/rayTracer.cpp:41-49 (host side)."""
+    _, host = libs()
+    cam = CrCamera()
+    rc = host.chiaro_camera(_fa(eye), _fa(center), _fa(up), float(yview), int(xres), int(yres), C.byref(cam))
+    if rc:
+        raise ValueError("chiaro_camera failed")
+    return cam
+
+
+def render_params(xres, yres, spp, k, seed, layer=1, background=(0.0, 0.0, 0.0), rank=0, nranks=1,
+                  tile=32) -> CrRenderParams:
+    return CrRenderParams(int(xres), int(yres), int(spp), int(k), _fa(background), int(seed) & 0xFFFFFFFF,
+                          int(layer), int(rank), int(nranks), int(tile))
+
+
+# ------------------------------------------------------------------- host --
+class Scene:
+    """Scene(argc, argv): ``Scene(rtc_path, *overrides)``, src/scene.cpp:13-72."""
+
+    def __init__(self, rtc_path, *overrides):
+        _, host = libs()
+        argv = [b"chiaroscuro", str(rtc_path).encode()] + [str(o).encode() for o in overrides]
+        arr = (C.c_char_p * len(argv))(*argv)
+        self._h = host.chiaro_scene_create(len(argv), arr)
+        if not self._h:
+            raise ValueError("Scene: " + _host_err())
+
+    @property
+    def info(self) -> dict:
+        _, host = libs()
+        i = ChiaroSceneInfo()
+        host.chiaro_scene_info_get(self._h, C.byref(i))
+        return {"xres": i.xres, "yres": i.yres, "samples": i.samples, "k": i.k, "seed": i.seed,
+                "leaf_size": i.leaf_size, "VP": list(i.VP), "LA": list(i.LA), "UP": list(i.UP),
+                "yview": i.yview, "exposure": i.exposure, "background": list(i.background),
+                "preview_height": i.preview_height, "using_preview": bool(i.using_preview),
+                "n_invalid": i.n_invalid, "obj_path": i.obj_path.decode(), "render_path": i.render_path.decode()}
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _host is not None:
+            _host.chiaro_scene_destroy(self._h)
+            self._h = None
+
+
+class Model:
+    """Model(Scene&), src/model.cpp:17-36 (own OBJ/MTL loader)."""
+
+    def __init__(self, scene: Scene | None = None, path: str | None = None):
+        _, host = libs()
+        self._h = host.chiaro_model_create(scene._h) if scene is not None else host.chiaro_model_load(
+            str(path).encode())
+        if not self._h:
+            raise ValueError("Model: " + _host_err())
+
+    @property
+    def num_meshes(self) -> int:
+        return libs()[1].chiaro_model_num_meshes(self._h)
+
+    @property
+    def num_triangles(self) -> int:
+        return libs()[1].chiaro_model_num_triangles(self._h)
+
+    def triangles(self) -> dict:
+        """Triangle soup in KDTree order (src/kdtree.cpp:44-66)."""
+        _, host = libs()
+        n = self.num_triangles
+        out = {"pos": np.zeros((n, 9), np.float32), "vnrm": np.zeros((n, 9), np.float32),
+               "uv": np.zeros((n, 6), np.float32), "kd": np.zeros((n, 3), np.float32),
+               "ke": np.zeros((n, 3), np.float32), "tex": np.zeros(n, np.int32)}
+        host.chiaro_model_triangles(self._h, _ptr(out["pos"]), _ptr(out["vnrm"]), _ptr(out["uv"]),
+                                    _ptr(out["kd"]), _ptr(out["ke"]), _ptr(out["tex"], C.c_int32))
+        return out
+
+    def textures(self) -> list:
+        _, host = libs()
+        res = []
+        for i in range(host.chiaro_model_num_textures(self._h)):
+            w, h, nc = C.c_int32(), C.c_int32(), C.c_int32()
+            d = C.POINTER(C.c_uint8)()
+            host.chiaro_model_texture(self._h, i, C.byref(w), C.byref(h), C.byref(nc), C.byref(d))
+            arr = np.ctypeslib.as_array(d, shape=(w.value * h.value * nc.value,)).copy()
+            res.append((w.value, h.value, nc.value, arr))
+        return res
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _host is not None:
+            _host.chiaro_model_destroy(self._h)
+            self._h = None
+
+
+class KDTree:
+    """Host KDTree(Model&, Scene&) build, src/kdtree.cpp:34-194 (no device needed)."""
+
+    def __init__(self, model: Model, scene: Scene, threads: int = 0):
+        _, host = libs()
+        self._model, self._scene = model, scene
+        self._h = host.chiaro_kdtree_create(model._h, scene._h, int(threads))
+        if not self._h:
+            raise ValueError("KDTree: " + _host_err())
+
+    def export(self) -> dict:
+        _, host = libs()
+        n, r = host.chiaro_kdtree_num_nodes(self._h), host.chiaro_kdtree_num_refs(self._h)
+        o = {k: np.zeros(n, np.uint32) for k in ("is_leaf", "axis", "child", "leaf_first", "leaf_count")}
+        o["split"] = np.zeros(n, np.float32)
+        o["refs"] = np.zeros(max(r, 1), np.uint32)
+        o["box"] = np.zeros(6, np.float32)
+        host.chiaro_kdtree_export(self._h, _ptr(o["is_leaf"], C.c_uint32), _ptr(o["axis"], C.c_uint32),
+                                  _ptr(o["split"]), _ptr(o["child"], C.c_uint32), _ptr(o["leaf_first"], C.c_uint32),
+                                  _ptr(o["leaf_count"], C.c_uint32), _ptr(o["refs"], C.c_uint32), _ptr(o["box"]))
+        o["refs"] = o["refs"][:r]
+        return o
+
+    def describe(self) -> CrSceneDesc:
+        d = CrSceneDesc()
+        rc = libs()[1].chiaro_kdtree_describe(self._h, self._scene._h, C.byref(d))
+        if rc:
+            raise RuntimeError("describe: " + _host_err())
+        return d
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _host is not None:
+            _host.chiaro_kdtree_destroy(self._h)
+            self._h = None
+
+
+class Device:
+    """One cr_ctx (include/chiaro_hip.h) -- the raw C-ABI boundary."""
+
+    def __init__(self, device: int = 0):
+        hip, _ = libs()
+        self._c = hip.cr_create(int(device))
+        if not self._c:
+            raise RuntimeError("cr_create returned NULL")
+        self.device = device
+
+    def _chk(self, rc, what):
+        if rc != CR_OK:
+            raise RuntimeError("%s failed (%s): %s" % (what, CR_ERRORS.get(rc, rc),
+                                                       libs()[0].cr_last_error(self._c).decode()))
+
+    def upload(self, desc: CrSceneDesc):
+        self._chk(libs()[0].cr_upload_scene(self._c, C.byref(desc)), "cr_upload_scene")
+
+    def render(self, cam: CrCamera, p: CrRenderParams, accum: np.ndarray | None = None) -> np.ndarray:
+        out = accum if accum is not None else np.zeros((p.yres, p.xres, 3), np.float32)
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == p.yres * p.xres * 3
+        self._chk(libs()[0].cr_render(self._c, C.byref(cam), C.byref(p), _ptr(out)), "cr_render")
+        return out
+
+    def render_device(self, cam, p, d_frame_ptr: int, stream: int = 0):
+        self._chk(libs()[0].cr_render_device(self._c, C.byref(cam), C.byref(p), C.c_void_p(d_frame_ptr),
+                                             C.c_void_p(stream)), "cr_render_device")
+
+    def render_tiles_device(self, cam, p, d_tiles_ptr: int, stream: int = 0):
+        self._chk(libs()[0].cr_render_tiles_device(self._c, C.byref(cam), C.byref(p), C.c_void_p(d_tiles_ptr),
+                                                   C.c_void_p(stream)), "cr_render_tiles_device")
+
+    def blend_tiles_device(self, p, d_gathered_ptr: int, d_frame_ptr: int, stream: int = 0):
+        self._chk(libs()[0].cr_blend_tiles_device(self._c, C.byref(p), C.c_void_p(d_gathered_ptr),
+                                                  C.c_void_p(d_frame_ptr), C.c_void_p(stream)),
+                  "cr_blend_tiles_device")
+
+    @staticmethod
+    def tiles_for_rank(p: CrRenderParams, rank: int) -> int:
+        return int(libs()[0].cr_tiles_for_rank(C.byref(p), int(rank)))
+
+    def intersect(self, orig: np.ndarray, dirs: np.ndarray) -> dict:
+        orig = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+        dirs = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        n = len(orig)
+        hit, tri = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+        bary, dist = np.zeros((n, 2), np.float32), np.zeros(n, np.float32)
+        self._chk(libs()[0].cr_intersect(self._c, n, _ptr(orig), _ptr(dirs), _ptr(hit, C.c_uint32),
+                                         _ptr(tri, C.c_uint32), _ptr(bary), _ptr(dist)), "cr_intersect")
+        return {"hit": hit, "tri": tri, "bary": bary, "dist": dist}
+
+    def intersect_shadow(self, orig, dirs, dist, light) -> np.ndarray:
+        orig = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+        dirs = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        dist = np.ascontiguousarray(dist, np.float32)
+        light = np.ascontiguousarray(light, np.uint32)
+        occ = np.zeros(len(orig), np.uint32)
+        self._chk(libs()[0].cr_intersect_shadow(self._c, len(orig), _ptr(orig), _ptr(dirs), _ptr(dist),
+                                                _ptr(light, C.c_uint32), _ptr(occ, C.c_uint32)),
+                  "cr_intersect_shadow")
+        return occ
+
+    def counters(self) -> dict:
+        c = CrCounters()
+        libs()[0].cr_get_counters(self._c, C.byref(c))
+        return c.as_dict()
+
+    def last_kernel_ms(self) -> float:
+        return float(libs()[0].cr_last_kernel_ms(self._c))
+
+    def set_option(self, key: str, value: int):
+        self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")
+
+    def synchronize(self):
+        self._chk(libs()[0].cr_synchronize(self._c), "cr_synchronize")
+
+    def close(self):
+        if getattr(self, "_c", None):
+            libs()[0].cr_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        if _hip is not None:
+            self.close()
+
+
+class RayTracer:
+    """RayTracer(Model&, Scene&) -- include/rayTracer.hpp:10-41, GPU render loop."""
+
+    def __init__(self, model: Model, scene: Scene, device: int = 0):
+        _, host = libs()
+        self._model, self._scene = model, scene
+        self._h = host.chiaro_raytracer_create(model._h, scene._h, int(device))
+        if not self._h:
+            raise RuntimeError("RayTracer: " + _host_err())
+        info = scene.info
+        self.xres, self.yres = info["xres"], info["yres"]
+
+    def rayTrace(self, eye, center, up=(0.0, 1.0, 0.0), yview=1.0):
+        rc = libs()[1].chiaro_raytracer_raytrace(self._h, _fa(eye), _fa(center), _fa(up), float(yview))
+        if rc:
+            raise RuntimeError("rayTrace: " + _host_err())
+
+    ray_trace = rayTrace
+
+    @property
+    def pixels(self) -> np.ndarray:
+        p = libs()[1].chiaro_raytracer_pixels(self._h)
+        return np.ctypeslib.as_array(p, shape=(self.yres, self.xres, 3)).copy()
+
+    @property
+    def maxVal(self) -> float:
+        return float(libs()[1].chiaro_raytracer_maxval(self._h))
+
+    @property
+    def layers(self) -> int:
+        return int(libs()[1].chiaro_raytracer_layers(self._h))
+
+    def getData(self) -> np.ndarray:
+        d = libs()[1].chiaro_raytracer_data(self._h)
+        return np.ctypeslib.as_array(d, shape=(self.yres, self.xres, 3)).copy()
+
+    def normalizeImage(self, exposure=3.4028234663852886e38, defog=0.0, kneeLow=0.0, kneeHigh=5.0, gamma=2.2):
+        libs()[1].chiaro_raytracer_normalize(self._h, exposure, defog, kneeLow, kneeHigh, gamma)
+
+    def exportImage(self, filename: str):
+        if libs()[1].chiaro_raytracer_export(self._h, str(filename).encode()):
+            raise RuntimeError("exportImage: " + _host_err())
+
+    def counters(self) -> dict:
+        c = CrCounters()
+        libs()[1].chiaro_raytracer_counters(self._h, C.byref(c))
+        return c.as_dict()
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _host is not None:
+            _host.chiaro_raytracer_destroy(self._h)
+            self._h = None
+
+
+def algorithmic_bytes(c: dict, pixels_written: int, texel_bytes: int = 3) -> int:
+    """B = 8 N_inner + 8 N_leaf + 40 N_tritest + 80 N_hit + texel N_texhit + 24 px."""
+    return (8 * c["inner"] + 8 * c["leaf"] + 40 * c["tritest"] + 80 * c["hit"] + texel_bytes * c["texhit"]
+            + 24 * pixels_written)

@@ -1,0 +1,431 @@
+// cabi.cpp -- libchiaro_hip.so: the C-ABI boundary (include/chiaro_hip.h).
+//
+// Owns the device copies of the scene (re-laid out for the kernels, see
+// kernels.hip header), the progressive accumulator, the counters and the
+// per-launch HIP events.  No C++ exception or hipError_t crosses the ABI.
+#include "chiaro_hip.h"
+#include "kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+struct cr_ctx {
+    int device = -1;
+    int num_cus = 0;
+    std::string err;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.f;
+    // scene
+    bool has_scene = false;
+    cr::DevScene S{};
+    uint32_t stack_depth = 1;
+    std::vector<void *> scene_bufs;
+    // work buffers
+    unsigned long long *d_counters = nullptr;
+    uint32_t *d_work = nullptr;
+    float *d_accum = nullptr;
+    size_t accum_elems = 0;
+    cr_counters last{};
+    // options
+    int kernel = 0;
+    uint32_t block = 0;
+    uint32_t waves_per_cu = 0;
+};
+
+namespace {
+
+int fail(cr_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+int hip_fail(cr_ctx *c, hipError_t e, const char *what) {
+    return fail(c, CR_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIPCHK(call)                                                                                                 \
+    do {                                                                                                             \
+        hipError_t e_ = (call);                                                                                      \
+        if (e_ != hipSuccess) return hip_fail(c, e_, #call);                                                         \
+    } while (0)
+
+void free_scene(cr_ctx *c) {
+    for (void *p : c->scene_bufs) hipFree(p);
+    c->scene_bufs.clear();
+    c->has_scene = false;
+    c->S = cr::DevScene{};
+}
+
+template <class T> int upload(cr_ctx *c, const std::vector<T> &h, const T **out) {
+    void *d = nullptr;
+    size_t bytes = h.size() * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e != hipSuccess) return fail(c, CR_E_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    c->scene_bufs.push_back(d);
+    if (!h.empty()) {
+        e = hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(c, e, "hipMemcpy(scene)");
+    }
+    *out = (const T *)d;
+    return CR_OK;
+}
+
+int check_params(cr_ctx *c, const cr_render_params *p) {
+    if (!p) return fail(c, CR_E_INVALID, "null params");
+    if (!c->has_scene) return fail(c, CR_E_NOSCENE, "no scene uploaded");
+    if (p->xres == 0 || p->yres == 0 || p->spp == 0) return fail(c, CR_E_INVALID, "xres/yres/spp must be > 0");
+    if (p->k < 1 || p->k > 64) return fail(c, CR_E_INVALID, "k must be in [1, 64]");
+    if (p->layer < 1) return fail(c, CR_E_INVALID, "layer must be >= 1");
+    if (p->nranks < 1 || p->rank >= p->nranks) return fail(c, CR_E_INVALID, "bad rank/nranks");
+    uint64_t px = (uint64_t)p->xres * p->yres;
+    if (px > (1ull << 31)) return fail(c, CR_E_INVALID, "image too large");
+    return CR_OK;
+}
+
+uint32_t tile_of(const cr_render_params *p) { return p->tile ? p->tile : 32u; }
+
+void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_render_params *p, float *out, int mode) {
+    A.S = c->S;
+    std::memcpy(A.cam, cam->eye, 3 * sizeof(float));
+    std::memcpy(A.cam + 3, cam->left_upper, 3 * sizeof(float));
+    std::memcpy(A.cam + 6, cam->dx, 3 * sizeof(float));
+    std::memcpy(A.cam + 9, cam->dy, 3 * sizeof(float));
+    A.xres = p->xres;
+    A.yres = p->yres;
+    A.spp = p->spp;
+    A.K = p->k;
+    A.bg[0] = p->background[0];
+    A.bg[1] = p->background[1];
+    A.bg[2] = p->background[2];
+    A.seed = p->seed;
+    A.layer = p->layer;
+    A.rank = p->rank;
+    A.nranks = p->nranks;
+    A.tile = tile_of(p);
+    A.tiles_x = (p->xres + A.tile - 1) / A.tile;
+    A.n_items = cr_tiles_for_rank(p, p->rank) * A.tile * A.tile;
+    A.stack_depth = c->stack_depth;
+    A.mode = mode;
+    A.out = out;
+    A.counters = c->d_counters;
+    A.work = c->d_work;
+}
+
+int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
+    if (!cam || !out) return fail(c, CR_E_INVALID, "null camera/output");
+    int rc = check_params(c, p);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    cr::RenderArgs A{};
+    fill_args(c, A, cam, p, out, mode);
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
+    HIPCHK(hipEventRecord(c->ev0, st));
+    int e = cr::launch_render(A, c->kernel, c->block, c->waves_per_cu, c->num_cus, st);
+    if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
+    HIPCHK(hipEventRecord(c->ev1, st));
+    unsigned long long h[16];
+    HIPCHK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]};
+    return CR_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+cr_ctx *cr_create(int device) {
+    cr_ctx *c = new cr_ctx();
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        c->err = "no HIP device";
+        return c; // error surfaced on first use; cr_last_error explains
+    }
+    if (device < 0 || device >= n) {
+        c->err = "bad device index";
+        return c;
+    }
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) {
+        c->err = "hipSetDevice failed";
+        c->device = -1;
+        return c;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_work, 16 * sizeof(uint32_t)) != hipSuccess) {
+        c->err = "device init failed";
+        c->device = -1;
+    }
+    return c;
+}
+
+void cr_destroy(cr_ctx *c) {
+    if (!c) return;
+    if (c->device >= 0) {
+        hipSetDevice(c->device);
+        free_scene(c);
+        if (c->d_accum) hipFree(c->d_accum);
+        if (c->d_counters) hipFree(c->d_counters);
+        if (c->d_work) hipFree(c->d_work);
+        if (c->ev0) hipEventDestroy(c->ev0);
+        if (c->ev1) hipEventDestroy(c->ev1);
+        if (c->stream) hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+const char *cr_last_error(cr_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!d || !d->nodes || d->n_nodes == 0) return fail(c, CR_E_INVALID, "empty kd tree");
+    if (d->n_tris && (!d->tri_pos || !d->tri_normal || !d->tri_kd || !d->tri_ke || !d->tri_uv))
+        return fail(c, CR_E_INVALID, "missing triangle arrays");
+    if (d->max_depth > 256) return fail(c, CR_E_DEPTH, "kd tree deeper than 256");
+    HIPCHK(hipSetDevice(c->device));
+    free_scene(c);
+    const uint32_t nt = d->n_tris;
+    // nodes -> {split bits | first, axis | child<<2}
+    std::vector<uint2> nodes(d->n_nodes);
+    for (uint32_t i = 0; i < d->n_nodes; i++) {
+        const cr_kdnode &n = d->nodes[i];
+        if (n.axis == 3) {
+            if (n.count >= (1u << 30) || (uint64_t)n.child_or_first + n.count > d->n_refs)
+                return fail(c, CR_E_INVALID, "bad leaf range");
+            nodes[i] = make_uint2(n.child_or_first, 3u | (n.count << 2));
+        } else {
+            if (n.axis > 2 || n.child_or_first + 1 >= d->n_nodes || n.child_or_first >= (1u << 30))
+                return fail(c, CR_E_INVALID, "bad inner node");
+            uint32_t sb;
+            std::memcpy(&sb, &n.split, 4);
+            nodes[i] = make_uint2(sb, n.axis | (n.child_or_first << 2));
+        }
+    }
+    // leaf-ordered triangle records {A,id},{B-A},{C-A}: e1/e2 computed exactly as
+    // intersectRayTriangle does each time (kdtree.cpp:222-223), so bit-identical.
+    std::vector<float4> recs((size_t)3 * d->n_refs);
+    for (uint32_t r = 0; r < d->n_refs; r++) {
+        const uint32_t t = d->refs[r];
+        if (t >= nt) return fail(c, CR_E_INVALID, "leaf ref out of range");
+        const float *p = d->tri_pos + 9 * (size_t)t;
+        float idf;
+        std::memcpy(&idf, &t, 4);
+        recs[3 * (size_t)r] = make_float4(p[0], p[1], p[2], idf);
+        recs[3 * (size_t)r + 1] = make_float4(p[3] - p[0], p[4] - p[1], p[5] - p[2], 0.f);
+        recs[3 * (size_t)r + 2] = make_float4(p[6] - p[0], p[7] - p[1], p[8] - p[2], 0.f);
+    }
+    std::vector<float4> tri((size_t)3 * nt), mn(nt), mkd(nt), mke(nt);
+    std::vector<float2> muv((size_t)3 * nt);
+    for (uint32_t t = 0; t < nt; t++) {
+        const float *p = d->tri_pos + 9 * (size_t)t;
+        for (int v = 0; v < 3; v++) tri[3 * (size_t)t + v] = make_float4(p[3 * v], p[3 * v + 1], p[3 * v + 2], 0.f);
+        const uint32_t em = d->tri_emissive ? (d->tri_emissive[t] ? 1u : 0u)
+                                            : ((d->tri_ke[3 * t] > 0.f || d->tri_ke[3 * t + 1] > 0.f ||
+                                                d->tri_ke[3 * t + 2] > 0.f) ? 1u : 0u);
+        float emf;
+        std::memcpy(&emf, &em, 4);
+        mn[t] = make_float4(d->tri_normal[3 * t], d->tri_normal[3 * t + 1], d->tri_normal[3 * t + 2], emf);
+        int32_t ti = d->tri_tex ? d->tri_tex[t] : -1;
+        if (ti >= (int32_t)d->n_textures) return fail(c, CR_E_INVALID, "texture index out of range");
+        float tif;
+        std::memcpy(&tif, &ti, 4);
+        mkd[t] = make_float4(d->tri_kd[3 * t], d->tri_kd[3 * t + 1], d->tri_kd[3 * t + 2], tif);
+        mke[t] = make_float4(d->tri_ke[3 * t], d->tri_ke[3 * t + 1], d->tri_ke[3 * t + 2], 0.f);
+        for (int v = 0; v < 3; v++)
+            muv[3 * (size_t)t + v] = make_float2(d->tri_uv[6 * t + 2 * v], d->tri_uv[6 * t + 2 * v + 1]);
+    }
+    std::vector<uint2> lights(d->n_lights);
+    for (uint32_t i = 0; i < d->n_lights; i++) {
+        if (d->light_id[i] >= nt) return fail(c, CR_E_INVALID, "light id out of range");
+        uint32_t sb;
+        std::memcpy(&sb, &d->light_surface[i], 4);
+        lights[i] = make_uint2(d->light_id[i], sb);
+    }
+    std::vector<uint4> texs(d->n_textures);
+    std::vector<uint8_t> texels;
+    for (uint32_t i = 0; i < d->n_textures; i++) {
+        const cr_texture &t = d->textures[i];
+        if (t.width <= 0 || t.height <= 0 || t.components <= 0 || !t.data)
+            return fail(c, CR_E_INVALID, "bad texture");
+        size_t off = (texels.size() + 15) & ~(size_t)15;
+        size_t bytes = (size_t)t.width * t.height * t.components;
+        texels.resize(off + bytes + cr::tex_pad(t.width, t.components), 0);
+        std::memcpy(texels.data() + off, t.data, bytes);
+        if (off > 0xffffffffull) return fail(c, CR_E_INVALID, "texture atlas > 4 GiB");
+        texs[i] = make_uint4((uint32_t)t.width, (uint32_t)t.height, (uint32_t)t.components, (uint32_t)off);
+    }
+    int rc;
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, tri, &c->S.tri)) ||
+        (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
+        (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
+        (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels))) {
+        free_scene(c);
+        return rc;
+    }
+    c->S.nlights = d->n_lights;
+    c->S.bmin = make_float3(d->box_min[0], d->box_min[1], d->box_min[2]);
+    c->S.bmax = make_float3(d->box_max[0], d->box_max[1], d->box_max[2]);
+    c->stack_depth = d->max_depth > 0 ? d->max_depth : 1;
+    c->has_scene = true;
+    return CR_OK;
+}
+
+uint32_t cr_tiles_for_rank(const cr_render_params *p, uint32_t rank) {
+    if (!p || p->nranks == 0 || rank >= p->nranks || p->xres == 0 || p->yres == 0) return 0;
+    const uint32_t T = tile_of(p);
+    const uint32_t nt = ((p->xres + T - 1) / T) * ((p->yres + T - 1) / T);
+    return nt > rank ? (nt - rank + p->nranks - 1) / p->nranks : 0;
+}
+
+int cr_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!accum_rgb_out || !p) return fail(c, CR_E_INVALID, "null output/params");
+    cr_render_params q = *p;
+    if (q.nranks == 0) q.nranks = 1;
+    int rc = check_params(c, &q);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t elems = (size_t)q.xres * q.yres * 3;
+    if (elems != c->accum_elems) {
+        if (c->d_accum) hipFree(c->d_accum);
+        c->d_accum = nullptr;
+        c->accum_elems = 0;
+        if (hipMalloc(&c->d_accum, elems * sizeof(float)) != hipSuccess) return fail(c, CR_E_OOM, "accumulator");
+        c->accum_elems = elems;
+        HIPCHK(hipMemset(c->d_accum, 0, elems * sizeof(float)));
+    }
+    rc = run_render(c, cam, &q, c->d_accum, cr::MODE_BLEND, c->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(accum_rgb_out, c->d_accum, elems * sizeof(float), hipMemcpyDeviceToHost));
+    return CR_OK;
+}
+
+int cr_render_device(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *d_frame, void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    return run_render(c, cam, p, d_frame, cr::MODE_BLEND, (hipStream_t)stream);
+}
+
+int cr_render_tiles_device(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *d_tiles,
+                           void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    return run_render(c, cam, p, d_tiles, cr::MODE_TILES, (hipStream_t)stream);
+}
+
+int cr_blend_tiles_device(cr_ctx *c, const cr_render_params *p, const float *d_gathered, float *d_frame,
+                          void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!p || !d_gathered || !d_frame || p->nranks < 1 || p->layer < 1) return fail(c, CR_E_INVALID, "bad blend args");
+    HIPCHK(hipSetDevice(c->device));
+    cr::BlendArgs B{};
+    B.gathered = d_gathered;
+    B.frame = d_frame;
+    B.xres = p->xres;
+    B.yres = p->yres;
+    B.tile = tile_of(p);
+    B.tiles_x = (p->xres + B.tile - 1) / B.tile;
+    B.nranks = p->nranks;
+    B.max_tiles = cr_tiles_for_rank(p, 0);
+    B.layer = p->layer;
+    int e = cr::launch_blend(B, (hipStream_t)stream);
+    if (e) return hip_fail(c, (hipError_t)e, "blend kernel launch");
+    return CR_OK;
+}
+
+static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, const float *dir, const float *dist,
+                     const uint32_t *light, uint32_t *hit, uint32_t *tri, float *bary, float *dist_out) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!c->has_scene) return fail(c, CR_E_NOSCENE, "no scene uploaded");
+    if (n == 0) return CR_OK;
+    if (!orig || !dir || !hit) return fail(c, CR_E_INVALID, "null query arrays");
+    HIPCHK(hipSetDevice(c->device));
+    char *buf = nullptr;
+    const size_t fbytes = (size_t)n * 3 * sizeof(float);
+    const size_t total = 2 * fbytes + 4 * (size_t)n * sizeof(uint32_t) + 3 * (size_t)n * sizeof(float) + 256;
+    if (hipMalloc(&buf, total) != hipSuccess) return fail(c, CR_E_OOM, "query buffers");
+    char *p = buf;
+    auto take = [&](size_t b) { char *r = p; p += (b + 15) & ~(size_t)15; return r; };
+    cr::QueryArgs Q{};
+    Q.S = c->S;
+    Q.n = n;
+    Q.shadow = shadow ? 1u : 0u;
+    Q.stack_depth = c->stack_depth;
+    float *d_orig = (float *)take(fbytes), *d_dir = (float *)take(fbytes);
+    float *d_dist = (float *)take(n * sizeof(float));
+    uint32_t *d_light = (uint32_t *)take(n * sizeof(uint32_t));
+    uint32_t *d_hit = (uint32_t *)take(n * sizeof(uint32_t)), *d_tri = (uint32_t *)take(n * sizeof(uint32_t));
+    float *d_bary = (float *)take(2 * n * sizeof(float)), *d_do = (float *)take(n * sizeof(float));
+    hipError_t e = hipMemcpy(d_orig, orig, fbytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_dir, dir, fbytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && shadow) e = hipMemcpy(d_dist, dist, n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess && shadow) e = hipMemcpy(d_light, light, n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long));
+    Q.orig = d_orig; Q.dir = d_dir; Q.dist = d_dist; Q.light = d_light;
+    Q.hit = d_hit; Q.tri = d_tri; Q.bary = d_bary; Q.dist_out = d_do;
+    Q.counters = c->d_counters;
+    if (e == hipSuccess) e = (hipError_t)cr::launch_intersect(Q, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(hit, d_hit, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && !shadow && tri) e = hipMemcpy(tri, d_tri, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && !shadow && bary) e = hipMemcpy(bary, d_bary, 2 * n * sizeof(float), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && !shadow && dist_out) e = hipMemcpy(dist_out, d_do, n * sizeof(float), hipMemcpyDeviceToHost);
+    unsigned long long h[16] = {};
+    if (e == hipSuccess) e = hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost);
+    hipFree(buf);
+    if (e != hipSuccess) return hip_fail(c, e, "intersect");
+    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]};
+    return CR_OK;
+}
+
+int cr_intersect(cr_ctx *c, uint32_t n, const float *orig, const float *dir, uint32_t *hit, uint32_t *tri,
+                 float *bary, float *dist) {
+    return run_query(c, n, false, orig, dir, nullptr, nullptr, hit, tri, bary, dist);
+}
+
+int cr_intersect_shadow(cr_ctx *c, uint32_t n, const float *orig, const float *dir, const float *dist,
+                        const uint32_t *light_tri, uint32_t *occluded) {
+    if (c && n && (!dist || !light_tri)) return fail(c, CR_E_INVALID, "null dist/light");
+    return run_query(c, n, true, orig, dir, dist, light_tri, occluded, nullptr, nullptr, nullptr);
+}
+
+int cr_get_counters(cr_ctx *c, cr_counters *out) {
+    if (!c || !out) return CR_E_INVALID;
+    *out = c->last;
+    return CR_OK;
+}
+
+float cr_last_kernel_ms(cr_ctx *c) { return c ? c->last_ms : 0.f; }
+
+int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
+    if (!c || !key) return CR_E_INVALID;
+    if (!std::strcmp(key, "kernel") && (v == 0 || v == 1)) c->kernel = (int)v;
+    else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
+    else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
+    else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
+    return CR_OK;
+}
+
+int cr_synchronize(cr_ctx *c) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, "no device");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    return CR_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,67 @@
+// kernels.hpp -- device-side data layout shared by kernels.hip and cabi.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cr {
+
+enum { MODE_BLEND = 0, MODE_TILES = 1 };
+
+// Zero bytes appended after every texture: the reference's getColorAt reads one
+// texel past the row/image end for coords == 1.0 (src/mesh.cpp:23-30) and three
+// bytes for 1-channel images; the pad makes that read defined (zeros).
+__host__ __device__ inline uint64_t tex_pad(int w, int nc) { return (uint64_t)(w + 1) * nc + 4; }
+
+struct DevScene {
+    const uint2 *nodes;   // {split bits | first ref, axis | child<<2 ; leaf: 3 | count<<2}
+    const float4 *recs;   // 3 per leaf ref: {A, id bits}, {B-A, 0}, {C-A, 0}
+    const float4 *tri;    // 3 per triangle: A, B, C
+    const float4 *mat_n;  // normal, w = emissive flag bits
+    const float4 *mat_kd; // Kd, w = texture index (int bits, -1 none)
+    const float4 *mat_ke; // Ke
+    const float2 *mat_uv; // 3 per triangle
+    const uint2 *lights;  // {triangle id, surface bits}
+    const uint4 *texs;    // {w, h, nc, byte offset}
+    const uint8_t *texels;
+    uint32_t nlights;
+    float3 bmin, bmax;    // padded root box
+};
+
+struct RenderArgs {
+    DevScene S;
+    float cam[12];        // eye, leftUpper, dx, dy
+    uint32_t xres, yres, spp;
+    int K;
+    float bg[3];
+    uint32_t seed, layer;
+    uint32_t rank, nranks, tile, tiles_x;
+    uint32_t n_items;     // my_tiles * tile * tile
+    uint32_t stack_depth;
+    int mode;
+    float *out;
+    unsigned long long *counters; // 9 x u64
+    uint32_t *work;               // persistent-kernel work counter (zeroed per launch)
+};
+
+struct QueryArgs {
+    DevScene S;
+    uint32_t n, shadow, stack_depth;
+    const float *orig, *dir, *dist;
+    const uint32_t *light;
+    uint32_t *hit, *tri;
+    float *bary, *dist_out;
+    unsigned long long *counters;
+};
+
+struct BlendArgs {
+    const float *gathered;
+    float *frame;
+    uint32_t xres, yres, tile, tiles_x, nranks, max_tiles, layer;
+};
+
+int launch_render(const RenderArgs &A, int kernel, uint32_t block, uint32_t waves_per_cu, int num_cus,
+                  hipStream_t st);
+int launch_intersect(const QueryArgs &Q, hipStream_t st);
+int launch_blend(const BlendArgs &B, hipStream_t st);
+
+} // namespace cr

@@ -1,0 +1,295 @@
+// capi.cpp -- extern "C" wrappers of the host classes (include/chiaroscuro.h).
+#include "chiaroscuro.h"
+
+#include "kdtree.hpp"
+#include "model.hpp"
+#include "raytracer.hpp"
+#include "scene.hpp"
+
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+using namespace chiaro;
+
+struct chiaro_scene {
+    std::unique_ptr<Scene> s;
+};
+struct chiaro_model {
+    std::unique_ptr<Model> m;
+};
+struct chiaro_kdtree {
+    std::unique_ptr<KDTree> k;
+};
+struct chiaro_raytracer {
+    std::unique_ptr<RayTracer> r;
+};
+
+namespace {
+thread_local std::string g_err;
+template <class F> auto guard(F f, decltype(f()) bad) -> decltype(f()) {
+    try {
+        g_err.clear();
+        return f();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+    } catch (...) {
+        g_err = "unknown C++ exception";
+    }
+    return bad;
+}
+void cpy(char *dst, const std::string &s, size_t n) {
+    std::strncpy(dst, s.c_str(), n - 1);
+    dst[n - 1] = 0;
+}
+} // namespace
+
+extern "C" {
+
+const char *chiaro_last_error(void) { return g_err.c_str(); }
+
+chiaro_scene *chiaro_scene_create(int argc, const char *const *argv) {
+    return guard(
+        [&]() -> chiaro_scene * {
+            std::vector<char *> a;
+            for (int i = 0; i < argc; i++) a.push_back(const_cast<char *>(argv[i]));
+            a.push_back(nullptr);
+            auto *s = new chiaro_scene();
+            s->s.reset(new Scene(argc, a.data()));
+            return s;
+        },
+        (chiaro_scene *)nullptr);
+}
+
+int chiaro_scene_info_get(const chiaro_scene *s, chiaro_scene_info *o) {
+    if (!s || !o) return CR_E_INVALID;
+    const Scene &S = *s->s;
+    std::memset(o, 0, sizeof *o);
+    o->xres = S.xres;
+    o->yres = S.yres;
+    o->samples = S.samples;
+    o->preview_height = S.previewHeight;
+    o->leaf_size = (uint32_t)S.kdtreeLeafSize;
+    o->seed = S.seed;
+    o->k = S.k;
+    o->using_preview = S.usingOpenGLPreview ? 1 : 0;
+    for (int i = 0; i < 3; i++) {
+        o->VP[i] = S.VP[i];
+        o->LA[i] = S.LA[i];
+        o->UP[i] = S.UP[i];
+        o->background[i] = S.background[i];
+    }
+    o->yview = S.yview;
+    o->exposure = S.exposure;
+    o->n_invalid = (uint32_t)S.errors.size();
+    cpy(o->obj_path, S.objPath, sizeof o->obj_path);
+    cpy(o->render_path, S.renderPath, sizeof o->render_path);
+    return CR_OK;
+}
+
+void chiaro_scene_destroy(chiaro_scene *s) { delete s; }
+
+chiaro_model *chiaro_model_create(chiaro_scene *s) {
+    if (!s) return nullptr;
+    return guard(
+        [&]() -> chiaro_model * {
+            auto *m = new chiaro_model();
+            m->m.reset(new Model(*s->s));
+            if (!m->m->error.empty()) {
+                g_err = m->m->error;
+                delete m;
+                return nullptr;
+            }
+            return m;
+        },
+        (chiaro_model *)nullptr);
+}
+
+chiaro_model *chiaro_model_load(const char *path) {
+    if (!path) return nullptr;
+    return guard(
+        [&]() -> chiaro_model * {
+            auto *m = new chiaro_model();
+            m->m.reset(new Model(std::string(path)));
+            if (!m->m->error.empty()) {
+                g_err = m->m->error;
+                delete m;
+                return nullptr;
+            }
+            return m;
+        },
+        (chiaro_model *)nullptr);
+}
+
+uint32_t chiaro_model_num_meshes(const chiaro_model *m) { return m ? (uint32_t)m->m->meshes.size() : 0; }
+
+uint32_t chiaro_model_num_triangles(const chiaro_model *m) {
+    if (!m) return 0;
+    size_t n = 0;
+    for (auto &mesh : m->m->meshes) n += mesh.indices.size() / 3;
+    return (uint32_t)n;
+}
+
+uint32_t chiaro_model_num_textures(const chiaro_model *m) {
+    if (!m) return 0;
+    uint32_t n = 0;
+    for (auto &t : m->m->textures_loaded) n += t.image ? 1 : 0;
+    return n;
+}
+
+int chiaro_model_triangles(const chiaro_model *m, float *pos, float *vnrm, float *uv, float *kd, float *ke,
+                           int32_t *tex) {
+    if (!m) return CR_E_INVALID;
+    size_t t = 0;
+    for (auto &mesh : m->m->meshes) {
+        const int ti = (mesh.textureDiffuse && mesh.textureDiffuse->image) ? mesh.textureDiffuse->index : -1;
+        for (size_t i = 0; i + 2 < mesh.indices.size(); i += 3, t++) {
+            for (int v = 0; v < 3; v++) {
+                const Vertex &V = mesh.vertices[mesh.indices[i + v]];
+                for (int j = 0; j < 3; j++) {
+                    if (pos) pos[9 * t + 3 * v + j] = V.Position[j];
+                    if (vnrm) vnrm[9 * t + 3 * v + j] = V.Normal[j];
+                }
+                if (uv) {
+                    uv[6 * t + 2 * v] = V.TexCoords.x;
+                    uv[6 * t + 2 * v + 1] = V.TexCoords.y;
+                }
+            }
+            for (int j = 0; j < 3; j++) {
+                if (kd) kd[3 * t + j] = mesh.materialColor.diffuse[j];
+                if (ke) ke[3 * t + j] = mesh.materialColor.emissive[j];
+            }
+            if (tex) tex[t] = ti;
+        }
+    }
+    return CR_OK;
+}
+
+int chiaro_model_texture(const chiaro_model *m, uint32_t i, int32_t *w, int32_t *h, int32_t *nc,
+                         const uint8_t **data) {
+    if (!m) return CR_E_INVALID;
+    uint32_t k = 0;
+    for (auto &t : m->m->textures_loaded) {
+        if (!t.image) continue;
+        if (k++ == i) {
+            *w = t.width;
+            *h = t.height;
+            *nc = t.nrComponents;
+            *data = t.image;
+            return CR_OK;
+        }
+    }
+    return CR_E_INVALID;
+}
+
+void chiaro_model_destroy(chiaro_model *m) { delete m; }
+
+chiaro_kdtree *chiaro_kdtree_create(chiaro_model *m, chiaro_scene *s, int threads) {
+    if (!m || !s) return nullptr;
+    return guard(
+        [&]() -> chiaro_kdtree * {
+            auto *k = new chiaro_kdtree();
+            k->k.reset(new KDTree(*m->m, *s->s, threads));
+            return k;
+        },
+        (chiaro_kdtree *)nullptr);
+}
+
+uint32_t chiaro_kdtree_num_nodes(const chiaro_kdtree *k) { return k ? (uint32_t)k->k->nodes.size() : 0; }
+uint32_t chiaro_kdtree_num_refs(const chiaro_kdtree *k) { return k ? (uint32_t)k->k->refs.size() : 0; }
+
+int chiaro_kdtree_export(const chiaro_kdtree *k, uint32_t *is_leaf, uint32_t *axis, float *split, uint32_t *child,
+                         uint32_t *leaf_first, uint32_t *leaf_count, uint32_t *refs, float *box) {
+    if (!k) return CR_E_INVALID;
+    const KDTree &K = *k->k;
+    for (size_t i = 0; i < K.nodes.size(); i++) {
+        const auto &n = K.nodes[i];
+        is_leaf[i] = n.isLeaf;
+        axis[i] = n.isLeaf ? 3u : n.split.axis;
+        split[i] = n.isLeaf ? 0.f : n.split.position;
+        child[i] = n.isLeaf ? 0u : n.child;
+        leaf_first[i] = n.isLeaf ? n.first : 0u;
+        leaf_count[i] = n.isLeaf ? n.count : 0u;
+    }
+    std::memcpy(refs, K.refs.data(), K.refs.size() * sizeof(uint32_t));
+    box[0] = K.minCoords.x; box[1] = K.minCoords.y; box[2] = K.minCoords.z;
+    box[3] = K.maxCoords.x; box[4] = K.maxCoords.y; box[5] = K.maxCoords.z;
+    return CR_OK;
+}
+
+int chiaro_kdtree_describe(chiaro_kdtree *k, const chiaro_scene *s, cr_scene_desc *out) {
+    if (!k || !s || !out) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            k->k->describe(*s->s, *out);
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+
+void chiaro_kdtree_destroy(chiaro_kdtree *k) { delete k; }
+
+chiaro_raytracer *chiaro_raytracer_create(chiaro_model *m, chiaro_scene *s, int device) {
+    if (!m || !s) return nullptr;
+    return guard(
+        [&]() -> chiaro_raytracer * {
+            auto *r = new chiaro_raytracer();
+            try {
+                r->r.reset(new RayTracer(*m->m, *s->s, device));
+            } catch (...) {
+                delete r;
+                throw;
+            }
+            return r;
+        },
+        (chiaro_raytracer *)nullptr);
+}
+
+int chiaro_raytracer_raytrace(chiaro_raytracer *r, const float eye[3], const float center[3], const float up[3],
+                              float yview) {
+    if (!r) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            r->r->rayTrace(vec3(eye[0], eye[1], eye[2]), vec3(center[0], center[1], center[2]),
+                           vec3(up[0], up[1], up[2]), yview);
+            return CR_OK;
+        },
+        CR_E_HIP);
+}
+
+const float *chiaro_raytracer_pixels(const chiaro_raytracer *r) { return r ? r->r->pixelData() : nullptr; }
+const uint8_t *chiaro_raytracer_data(chiaro_raytracer *r) { return r ? r->r->getData() : nullptr; }
+float chiaro_raytracer_maxval(const chiaro_raytracer *r) { return r ? r->r->maxVal : 0.f; }
+uint32_t chiaro_raytracer_layers(const chiaro_raytracer *r) { return r ? r->r->layers() : 0; }
+int chiaro_raytracer_counters(const chiaro_raytracer *r, cr_counters *out) {
+    if (!r || !out) return CR_E_INVALID;
+    *out = r->r->lastCounters();
+    return CR_OK;
+}
+int chiaro_raytracer_normalize(chiaro_raytracer *r, float exposure, float defog, float kl, float kh, float gamma) {
+    if (!r) return CR_E_INVALID;
+    r->r->normalizeImage(exposure, defog, kl, kh, gamma);
+    return CR_OK;
+}
+int chiaro_raytracer_export(chiaro_raytracer *r, const char *filename) {
+    if (!r || !filename) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            r->r->exportImage(filename);
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+cr_ctx *chiaro_raytracer_ctx(chiaro_raytracer *r) { return r ? r->r->context() : nullptr; }
+void chiaro_raytracer_destroy(chiaro_raytracer *r) { delete r; }
+
+int chiaro_camera(const float eye[3], const float center[3], const float up[3], float yview, uint32_t xres,
+                  uint32_t yres, cr_camera *out) {
+    if (!eye || !center || !up || !out || !xres || !yres) return CR_E_INVALID;
+    *out = make_camera(vec3(eye[0], eye[1], eye[2]), vec3(center[0], center[1], center[2]), vec3(up[0], up[1], up[2]),
+                       yview, xres, yres);
+    return CR_OK;
+}
+
+} // extern "C"

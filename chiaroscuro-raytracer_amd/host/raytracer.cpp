@@ -1,0 +1,290 @@
+// raytracer.cpp -- host side of RayTracer (src/rayTracer.cpp), GPU render loop.
+#include "raytracer.hpp"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+
+#include <zlib.h>
+
+namespace chiaro {
+
+cr_camera make_camera(vec3 eye, vec3 center, vec3 up, float yview, unsigned xres, unsigned yres) {
+    // rayTracer.cpp:41-43
+    float z = 1.f;
+    float y = z * 0.5f * yview;
+    float x = y * ((float)xres / (float)yres);
+    // gtc/matrix_transform.inl:521-546 lookAtRH, upper 3x3 as m[col][row]
+    const vec3 f = normalize(center - eye);
+    const vec3 s = normalize(cross(f, up));
+    const vec3 u = cross(s, f);
+    const float m[3][3] = {{s.x, u.x, -f.x}, {s.y, u.y, -f.y}, {s.z, u.z, -f.z}};
+    // func_matrix.inl:272-294
+    const float ood = 1.f / (+m[0][0] * (m[1][1] * m[2][2] - m[2][1] * m[1][2])
+                             - m[1][0] * (m[0][1] * m[2][2] - m[2][1] * m[0][2])
+                             + m[2][0] * (m[0][1] * m[1][2] - m[1][1] * m[0][2]));
+    float r[3][3];
+    r[0][0] = +(m[1][1] * m[2][2] - m[2][1] * m[1][2]) * ood;
+    r[1][0] = -(m[1][0] * m[2][2] - m[2][0] * m[1][2]) * ood;
+    r[2][0] = +(m[1][0] * m[2][1] - m[2][0] * m[1][1]) * ood;
+    r[0][1] = -(m[0][1] * m[2][2] - m[2][1] * m[0][2]) * ood;
+    r[1][1] = +(m[0][0] * m[2][2] - m[2][0] * m[0][2]) * ood;
+    r[2][1] = -(m[0][0] * m[2][1] - m[2][0] * m[0][1]) * ood;
+    r[0][2] = +(m[0][1] * m[1][2] - m[1][1] * m[0][2]) * ood;
+    r[1][2] = -(m[0][0] * m[1][2] - m[1][0] * m[0][2]) * ood;
+    r[2][2] = +(m[0][0] * m[1][1] - m[1][0] * m[0][1]) * ood;
+    // rayTracer.cpp:47-49: (scalar * mat3) * vec3 (type_mat3x3.inl:419-433)
+    auto mulv = [](const float a[3][3], vec3 v) {
+        return vec3(a[0][0] * v.x + a[1][0] * v.y + a[2][0] * v.z, a[0][1] * v.x + a[1][1] * v.y + a[2][1] * v.z,
+                    a[0][2] * v.x + a[1][2] * v.y + a[2][2] * v.z);
+    };
+    const float sy = 1.f / (float)yres, sx = 1.f / (float)xres;
+    float a[3][3], b[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            a[i][j] = r[i][j] * sy;
+            b[i][j] = r[i][j] * sx;
+        }
+    const vec3 dy = mulv(a, vec3(0.f, -2.f * y, 0.f));
+    const vec3 dx = mulv(b, vec3(2.f * x, 0.f, 0.f));
+    const vec3 lu = mulv(r, vec3(-x, y, -z));
+    cr_camera c;
+    c.eye[0] = eye.x; c.eye[1] = eye.y; c.eye[2] = eye.z;
+    c.left_upper[0] = lu.x; c.left_upper[1] = lu.y; c.left_upper[2] = lu.z;
+    c.dx[0] = dx.x; c.dx[1] = dx.y; c.dx[2] = dx.z;
+    c.dy[0] = dy.x; c.dy[1] = dy.y; c.dy[2] = dy.z;
+    return c;
+}
+
+RayTracer::RayTracer(Model &_model, Scene &_scene, int device)
+    : scene(_scene), pixels((size_t)_scene.yres * _scene.xres * 3, 0.f), data((size_t)_scene.yres * _scene.xres * 3),
+      kdtree(_model, _scene) {
+    ctx_ = cr_create(device);
+    cr_scene_desc d;
+    kdtree.describe(scene, d);
+    const int rc = cr_upload_scene(ctx_, &d);
+    if (rc != CR_OK) {
+        std::string msg = std::string("chiaro: scene upload failed: ") + cr_last_error(ctx_);
+        cr_destroy(ctx_);
+        ctx_ = nullptr;
+        throw std::runtime_error(msg);
+    }
+    kdtree.attach(ctx_);
+}
+
+RayTracer::~RayTracer() { cr_destroy(ctx_); }
+
+void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) {
+    // rayTracer.cpp:24 -- including the reference's `(lastUp == lastUp)`: a
+    // change of `up` alone does not reset the accumulation.
+    const bool newLayer = (eye == lastEye) && (center == lastCenter) && (lastUp == lastUp) && (yview == lastYview);
+    if (newLayer)
+        layers_++;
+    else {
+        layers_ = 1;
+        lastEye = eye;
+        lastCenter = center;
+        lastUp = up;
+        lastYview = yview;
+    }
+    if (!std::getenv("CHIARO_QUIET"))
+        std::cerr << "Camera at (" << eye.x << ", " << eye.y << ", " << eye.z << ") facing: (" << center.x << ", "
+                  << center.y << ", " << center.z << ")\nRendering image of size " << scene.xres << "x" << scene.yres
+                  << " with " << layers_ * scene.samples << " samples on the GPU...\t";
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    const cr_camera cam = make_camera(eye, center, up, yview, scene.xres, scene.yres);
+    cr_render_params p{};
+    p.xres = scene.xres;
+    p.yres = scene.yres;
+    p.spp = scene.samples;
+    p.k = scene.k;
+    p.background[0] = scene.background.x;
+    p.background[1] = scene.background.y;
+    p.background[2] = scene.background.z;
+    p.seed = scene.seed;
+    p.layer = layers_;
+    p.rank = 0;
+    p.nranks = 1;
+    p.tile = 32;
+    const int rc = cr_render(ctx_, &cam, &p, pixels.data());
+    if (rc != CR_OK) throw std::runtime_error(std::string("chiaro: render failed: ") + cr_last_error(ctx_));
+    cr_get_counters(ctx_, &counters_);
+    // rayTracer.cpp:51,66-68 (computed after the render instead of racily inside it)
+    maxVal = 0.f;
+    for (float v : pixels) maxVal = maxVal > v ? maxVal : v;
+    const auto t1 = std::chrono::high_resolution_clock::now();
+    lastSeconds_ = std::chrono::duration<double>(t1 - t0).count();
+    if (!std::getenv("CHIARO_QUIET")) std::cerr << "took " << lastSeconds_ << " seconds.\n";
+}
+
+uint8_t *RayTracer::getData() { return data.data(); }
+
+// rayTracer.cpp:173-195
+static inline float knee(double x, double f) { return logf(x * f + 1) / f; }
+static float findKneeF(float x, float y) {
+    float f0 = 0;
+    float f1 = 1;
+    while (knee(x, f1) > y) {
+        f0 = f1;
+        f1 = f1 * 2;
+    }
+    for (int i = 0; i < 30; ++i) {
+        float f2 = (f0 + f1) / 2;
+        float y2 = knee(x, f2);
+        if (y2 < y)
+            f1 = f2;
+        else
+            f0 = f2;
+    }
+    return (f0 + f1) / 2;
+}
+
+// rayTracer.cpp:198-223 (exrdisplay-style), host post-process
+void RayTracer::normalizeImage(float exposure, float defog, float kneeLow, float kneeHigh, float gamma) {
+    if (exposure == FLT_MAX) exposure = scene.exposure;
+    const float m = powf(2.f, exposure + 2.47393f);
+    const float s = 255.f * powf(2.f, -3.5f * gamma);
+    const float kl = powf(2.f, kneeLow);
+    const float f = findKneeF(powf(2.f, kneeHigh), powf(2.f, 3.5) - kl);
+    auto transform = [=](float x) {
+        x = std_max(0.f, x - defog);
+        x *= m;
+        if (x > kl) x = kl + knee(x - kl, f);
+        const float v = powf(x, gamma) * s;
+        return (v > 0.f ? v : 0.f) < 255.f ? (v > 0.f ? v : 0.f) : 255.f; // glm::clamp
+    };
+    for (unsigned y = 0; y < scene.yres; y++)
+        for (unsigned x = 0; x < scene.xres; x++) {
+            size_t i = 3 * ((size_t)(scene.yres - y - 1) * scene.xres + x);
+            const float *p = &pixels[3 * ((size_t)y * scene.xres + x)];
+            data[i++] = (uint8_t)transform(p[0]);
+            data[i++] = (uint8_t)transform(p[1]);
+            data[i++] = (uint8_t)transform(p[2]);
+        }
+}
+
+namespace {
+bool ends_with(const std::string &s, const char *suf) {
+    const size_t n = std::strlen(suf);
+    if (s.size() < n) return false;
+    for (size_t i = 0; i < n; i++)
+        if (std::tolower((unsigned char)s[s.size() - n + i]) != suf[i]) return false;
+    return true;
+}
+void put_be32(std::vector<unsigned char> &v, uint32_t x) {
+    for (int i = 3; i >= 0; i--) v.push_back((unsigned char)(x >> (8 * i)));
+}
+void png_chunk(std::ofstream &o, const char *type, const std::vector<unsigned char> &data) {
+    std::vector<unsigned char> buf;
+    put_be32(buf, (uint32_t)data.size());
+    buf.insert(buf.end(), type, type + 4);
+    buf.insert(buf.end(), data.begin(), data.end());
+    uLong crc = crc32(0L, Z_NULL, 0);
+    crc = crc32(crc, buf.data() + 4, (uInt)(buf.size() - 4));
+    put_be32(buf, (uint32_t)crc);
+    o.write((const char *)buf.data(), (std::streamsize)buf.size());
+}
+} // namespace
+
+// rayTracer.cpp:225-279 with this build's own writers (FreeImage is not available):
+// float formats keep pixels[0] as the top row, 8-bit formats go through normalizeImage.
+void RayTracer::exportImage(const char *filename) {
+    const std::string fn(filename);
+    const unsigned W = scene.xres, H = scene.yres;
+    std::ofstream o(fn, std::ios::binary);
+    if (!o) {
+        std::cerr << "Couldn't save the image.\nExport failed.\n";
+        return;
+    }
+    if (ends_with(fn, ".pfm")) {
+        o << "PF\n" << W << " " << H << "\n-1.0\n";
+        for (unsigned y = H; y-- > 0;) o.write((const char *)&pixels[3 * (size_t)y * W], (std::streamsize)(12 * W));
+    } else if (ends_with(fn, ".hdr")) { // Radiance RGBE, flat scanlines
+        o << "#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y " << H << " +X " << W << "\n";
+        std::vector<unsigned char> row(4 * (size_t)W);
+        for (unsigned y = 0; y < H; y++) {
+            for (unsigned x = 0; x < W; x++) {
+                const float *p = &pixels[3 * ((size_t)y * W + x)];
+                float v = std::max(p[0], std::max(p[1], p[2]));
+                unsigned char *e = &row[4 * (size_t)x];
+                if (v < 1e-32f) {
+                    e[0] = e[1] = e[2] = e[3] = 0;
+                } else {
+                    int ex;
+                    const float sc = std::frexp(v, &ex) * 256.0f / v;
+                    e[0] = (unsigned char)(p[0] * sc); e[1] = (unsigned char)(p[1] * sc);
+                    e[2] = (unsigned char)(p[2] * sc); e[3] = (unsigned char)(ex + 128);
+                }
+            }
+            o.write((const char *)row.data(), (std::streamsize)row.size());
+        }
+    } else if (ends_with(fn, ".exr")) { // scanline, uncompressed, FLOAT B,G,R
+        std::vector<unsigned char> h;
+        auto u32 = [&](uint32_t v) { for (int i = 0; i < 4; i++) h.push_back((unsigned char)(v >> (8 * i))); };
+        auto str = [&](const char *s) { h.insert(h.end(), s, s + std::strlen(s) + 1); };
+        u32(20000630u); u32(2u);
+        str("channels"); str("chlist"); u32(3 * 18 + 1);
+        for (const char *ch : {"B", "G", "R"}) { str(ch); u32(2u); u32(0u); u32(1u); u32(1u); }
+        h.push_back(0);
+        str("compression"); str("compression"); u32(1); h.push_back(0);
+        str("dataWindow"); str("box2i"); u32(16); u32(0); u32(0); u32(W - 1); u32(H - 1);
+        str("displayWindow"); str("box2i"); u32(16); u32(0); u32(0); u32(W - 1); u32(H - 1);
+        str("lineOrder"); str("lineOrder"); u32(1); h.push_back(0);
+        str("pixelAspectRatio"); str("float"); u32(4); { float one = 1.f; uint32_t b; std::memcpy(&b, &one, 4); u32(b); }
+        str("screenWindowCenter"); str("v2f"); u32(8); u32(0); u32(0);
+        str("screenWindowWidth"); str("float"); u32(4); { float one = 1.f; uint32_t b; std::memcpy(&b, &one, 4); u32(b); }
+        h.push_back(0);
+        const uint64_t line_bytes = 8 + 12ull * W;
+        const uint64_t table_end = h.size() + 8ull * H;
+        for (unsigned y = 0; y < H; y++) {
+            const uint64_t off = table_end + line_bytes * y;
+            for (int i = 0; i < 8; i++) h.push_back((unsigned char)(off >> (8 * i)));
+        }
+        o.write((const char *)h.data(), (std::streamsize)h.size());
+        std::vector<float> line(3 * (size_t)W);
+        for (unsigned y = 0; y < H; y++) {
+            const int32_t yy = (int32_t)y;
+            const uint32_t sz = 12 * W;
+            o.write((const char *)&yy, 4);
+            o.write((const char *)&sz, 4);
+            for (int c = 2, k = 0; c >= 0; c--, k++)
+                for (unsigned x = 0; x < W; x++) line[(size_t)k * W + x] = pixels[3 * ((size_t)y * W + x) + c];
+            o.write((const char *)line.data(), (std::streamsize)(line.size() * 4));
+        }
+    } else { // 8-bit: rows of `data` are bottom-up (rayTracer.cpp:217), write top-down
+        normalizeImage();
+        if (ends_with(fn, ".png")) {
+            static const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+            o.write((const char *)sig, 8);
+            std::vector<unsigned char> ihdr;
+            put_be32(ihdr, W);
+            put_be32(ihdr, H);
+            ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});
+            png_chunk(o, "IHDR", ihdr);
+            std::vector<unsigned char> raw;
+            raw.reserve((3 * (size_t)W + 1) * H);
+            for (unsigned y = 0; y < H; y++) {
+                raw.push_back(0);
+                const unsigned char *r = &data[3 * (size_t)(H - 1 - y) * W];
+                raw.insert(raw.end(), r, r + 3 * (size_t)W);
+            }
+            uLongf cl = compressBound((uLong)raw.size());
+            std::vector<unsigned char> comp(cl);
+            compress2(comp.data(), &cl, raw.data(), (uLong)raw.size(), 6);
+            comp.resize(cl);
+            png_chunk(o, "IDAT", comp);
+            png_chunk(o, "IEND", {});
+        } else { // PPM
+            o << "P6\n" << W << " " << H << "\n255\n";
+            for (unsigned y = 0; y < H; y++) o.write((const char *)&data[3 * (size_t)(H - 1 - y) * W], 3 * (std::streamsize)W);
+        }
+    }
+    if (o) std::cerr << "Render succesfully saved to file " << filename << "\n";
+    else std::cerr << "Couldn't save the image.\nExport failed.\n";
+}
+
+} // namespace chiaro

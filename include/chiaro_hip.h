@@ -1,0 +1,170 @@
+/*
+ * chiaro_hip.h -- the drop-in C-ABI boundary of the MI355X path-tracing core.
+ *
+ * Exported by libchiaro_hip.so.  Plain pointers and sizes only: no C++, no
+ * glm, no torch, no hipError_t crosses this boundary.  Every call returns 0
+ * (CR_OK) or a negative CR_E_* code; cr_last_error() gives the text.
+ *
+ * What each entry point replaces in the reference (Domingo1337/Chiaroscuro-RayTracer):
+ *
+ *   cr_upload_scene      KDTree::KDTree's products consumed by the render loop:
+ *                        KDTree::triangles / materials / nodes / minCoords / maxCoords
+ *                        (include/kdtree.hpp:43-76) and Scene::lightTriangles
+ *                        (include/scene.hpp:47) -- built on the host by the caller
+ *                        (src/kdtree.cpp:34-194), copied into device buffers here.
+ *   cr_render            the body of RayTracer::rayTrace after the camera set-up:
+ *                        the pixel x sample loop and the progressive blend
+ *                        (src/rayTracer.cpp:52-70) with RayTracer::sendRay
+ *                        (src/rayTracer.cpp:76-135), intersectRayKDTree (137-169),
+ *                        KDTree traversal (src/kdtree.cpp:196-344), Diffuse /
+ *                        Emissive BRDFs (src/brdf.cpp:10-85), Texture::getColorAt
+ *                        (src/mesh.cpp:21-35) and Scene::randomLight (src/scene.cpp:79-82).
+ *   cr_render_device     the same, into a caller-owned device framebuffer on a
+ *                        caller-supplied HIP stream (no host copy).
+ *   cr_render_tiles_device / cr_blend_tiles_device
+ *                        the same loop split over ranks by 32x32 tiles (no
+ *                        reference counterpart: the reference's only split is the
+ *                        OpenMP row loop, src/rayTracer.cpp:55).
+ *   cr_intersect         KDTree::intersectRay       (src/kdtree.cpp:210-216)
+ *   cr_intersect_shadow  KDTree::intersectShadowRay (src/kdtree.cpp:283-290)
+ *
+ * Threading: one cr_ctx per GPU, not thread-safe; calls on one ctx are serialised.
+ */
+#ifndef CHIARO_HIP_H
+#define CHIARO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CR_OK 0
+#define CR_E_INVALID (-1)  /* bad argument                         */
+#define CR_E_HIP (-2)      /* HIP runtime error (no device, fault) */
+#define CR_E_NOSCENE (-3)  /* render before cr_upload_scene        */
+#define CR_E_DEPTH (-4)    /* kd-tree deeper than the kernels support */
+#define CR_E_OOM (-5)      /* device allocation failed             */
+
+typedef struct cr_ctx cr_ctx;
+
+/* One kd node as KDTree::KDNode (include/kdtree.hpp:47-60):
+ *   inner: axis in {0,1,2}, split = Split::position, child = KDNode::child
+ *          (children at child and child+1, left = inLeft side)
+ *   leaf:  axis == 3, first/count index the leaf reference list
+ *          (KDNode::trianglesids, in order). */
+typedef struct {
+    float split;
+    uint32_t axis;
+    uint32_t child_or_first;
+    uint32_t count;
+} cr_kdnode;
+
+typedef struct {
+    int32_t width, height, components; /* Texture::width/height/nrComponents (include/mesh.hpp:173-182) */
+    const uint8_t *data;               /* width*height*components bytes, stb layout */
+} cr_texture;
+
+typedef struct {
+    /* kd tree, node 0 = root, DFS order exactly as KDTree::build allocates it */
+    uint32_t n_nodes;
+    const cr_kdnode *nodes;
+    uint32_t n_refs;
+    const uint32_t *refs;       /* concatenated leaf triangle id lists */
+    uint32_t max_depth;         /* deepest leaf (root = 0) */
+    float box_min[3], box_max[3]; /* KDTree::minCoords/maxCoords, AFTER the +-1e-4 pad */
+    /* triangles + materials, id order (KDTree::triangles / materials) */
+    uint32_t n_tris;
+    const float *tri_pos;       /* [n][9]  posFst, posSnd, posTrd              */
+    const float *tri_normal;    /* [n][3]  Material::normal ((n0+n1+n2)/3)     */
+    const float *tri_kd;        /* [n][3]  Material::Kd                        */
+    const float *tri_ke;        /* [n][3]  Material::Ke                        */
+    const float *tri_uv;        /* [n][6]  texFst, texSnd, texTrd              */
+    const int32_t *tri_tex;     /* [n]     texture index, -1 = none / not loaded */
+    const uint8_t *tri_emissive;/* [n]     Material::BRDFtype == Emissive      */
+    /* Scene::lightTriangles (include/scene.hpp:18-22), in push order */
+    uint32_t n_lights;
+    const uint32_t *light_id;
+    const float *light_surface;
+    /* textures referenced by tri_tex */
+    uint32_t n_textures;
+    const cr_texture *textures;
+} cr_scene_desc;
+
+/* Camera basis exactly as src/rayTracer.cpp:41-49 computes it (host side). */
+typedef struct {
+    float eye[3];
+    float left_upper[3];
+    float dx[3];
+    float dy[3];
+} cr_camera;
+
+typedef struct {
+    uint32_t xres, yres;  /* Scene::xres/yres */
+    uint32_t spp;         /* Scene::samples (per layer) */
+    int32_t k;            /* Scene::k, max path depth, 1..64 */
+    float background[3];  /* Scene::background */
+    uint32_t seed;        /* RNG stream key (DESIGN.md "RNG") */
+    uint32_t layer;       /* progressive layer L >= 1 (src/rayTracer.cpp:18-33) */
+    uint32_t rank, nranks;/* tile partition: tile t belongs to rank t % nranks */
+    uint32_t tile;        /* tile edge in pixels, 0 -> 32 */
+} cr_render_params;
+
+/* Query counters of the last render / intersect call. */
+typedef struct {
+    uint64_t closest;     /* KDTree::intersectRay-equivalent queries      */
+    uint64_t shadow;      /* KDTree::intersectShadowRay-equivalent queries (box-culled included) */
+    uint64_t inner;       /* inner node visits  */
+    uint64_t leaf;        /* leaf visits        */
+    uint64_t tritest;     /* triangle tests     */
+    uint64_t hit;         /* closest hits       */
+    uint64_t texhit;      /* textured hits      */
+    uint64_t paths;       /* camera paths       */
+    uint64_t pixels;      /* pixels written     */
+} cr_counters;
+
+cr_ctx *cr_create(int device);
+void cr_destroy(cr_ctx *ctx);
+const char *cr_last_error(cr_ctx *ctx);
+
+int cr_upload_scene(cr_ctx *ctx, const cr_scene_desc *desc);
+
+/* Full-frame render of one progressive layer; blend on device into the ctx's
+ * accumulator ((old*(L-1) + mean)/L), then copy [yres][xres][3] fp32 to
+ * accum_rgb_out (host).  Layer 1 ignores the previous accumulator. */
+int cr_render(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out);
+
+/* Same, blending into the caller-owned device buffer d_frame [yres][xres][3]
+ * (only this rank's tiles are touched) on `stream` (hipStream_t, NULL = null stream). */
+int cr_render_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *d_frame, void *stream);
+
+/* Batch means (no blend) of this rank's tiles into compact d_tiles
+ * [cr_tiles_for_rank][tile][tile][3]. */
+int cr_render_tiles_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *d_tiles,
+                           void *stream);
+/* Root side: d_gathered = [nranks][max_tiles][tile][tile][3] (rank r's compact
+ * buffer at slot r, max_tiles = cr_tiles_for_rank(p, 0)); unpermute and blend
+ * layer p->layer into d_frame [yres][xres][3]. */
+int cr_blend_tiles_device(cr_ctx *ctx, const cr_render_params *p, const float *d_gathered, float *d_frame,
+                          void *stream);
+uint32_t cr_tiles_for_rank(const cr_render_params *p, uint32_t rank);
+
+/* Ray queries (host arrays). dir need not be normalised (the reference does not). */
+int cr_intersect(cr_ctx *ctx, uint32_t n, const float *orig, const float *dir, uint32_t *hit, uint32_t *tri,
+                 float *bary, float *dist);
+int cr_intersect_shadow(cr_ctx *ctx, uint32_t n, const float *orig, const float *dir, const float *dist,
+                        const uint32_t *light_tri, uint32_t *occluded);
+
+int cr_get_counters(cr_ctx *ctx, cr_counters *out);
+/* Device time (ms) of the last render kernel, HIP events on its own stream. */
+float cr_last_kernel_ms(cr_ctx *ctx);
+/* Kernel variant / tuning knobs: "kernel" (0 = persistent wave-regeneration,
+ * 1 = one-thread-per-pixel), "block", "waves_per_cu". Returns CR_OK or CR_E_INVALID. */
+int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
+int cr_synchronize(cr_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

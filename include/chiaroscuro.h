@@ -1,0 +1,92 @@
+/*
+ * chiaroscuro.h -- C entry points of libchiaroscuro.so, the host mirror of the
+ * reference's C++ classes (Scene, Model, KDTree, RayTracer), for FFI callers
+ * (ctypes in this repo's tests and bench).  C++ callers use the host headers directly.
+ *
+ *   chiaro_scene_create      Scene::Scene(argc, argv)              src/scene.cpp:13-72
+ *   chiaro_model_create      Model::Model(Scene&)                  src/model.cpp:17-36
+ *   chiaro_raytracer_create  RayTracer::RayTracer(Model&, Scene&)  src/rayTracer.cpp:13-15
+ *                            (builds KDTree, src/kdtree.cpp:34-108, uploads via cr_upload_scene)
+ *   chiaro_raytracer_raytrace RayTracer::rayTrace                  src/rayTracer.cpp:17-74
+ *   chiaro_raytracer_data / _maxval / _normalize / _export
+ *                            getData / maxVal / normalizeImage / exportImage (rayTracer.cpp:171-279)
+ *   chiaro_camera            the camera basis of rayTrace          src/rayTracer.cpp:41-49
+ *
+ * Errors: functions return NULL / a negative code; chiaro_last_error() (per thread)
+ * gives the message.  C++ exceptions never cross this boundary.
+ */
+#ifndef CHIAROSCURO_H
+#define CHIAROSCURO_H
+
+#include "chiaro_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct chiaro_scene chiaro_scene;
+typedef struct chiaro_model chiaro_model;
+typedef struct chiaro_kdtree chiaro_kdtree;
+typedef struct chiaro_raytracer chiaro_raytracer;
+
+typedef struct {
+    uint32_t xres, yres, samples, preview_height, leaf_size, seed;
+    int32_t k;
+    int32_t using_preview;
+    float VP[3], LA[3], UP[3], background[3];
+    float yview, exposure;
+    uint32_t n_invalid; /* tokens reported as "Invalid argument" */
+    char obj_path[1024];
+    char render_path[1024];
+} chiaro_scene_info;
+
+const char *chiaro_last_error(void);
+
+chiaro_scene *chiaro_scene_create(int argc, const char *const *argv);
+int chiaro_scene_info_get(const chiaro_scene *s, chiaro_scene_info *out);
+void chiaro_scene_destroy(chiaro_scene *s);
+
+chiaro_model *chiaro_model_create(chiaro_scene *s);
+chiaro_model *chiaro_model_load(const char *obj_path);
+uint32_t chiaro_model_num_meshes(const chiaro_model *m);
+uint32_t chiaro_model_num_triangles(const chiaro_model *m);
+uint32_t chiaro_model_num_textures(const chiaro_model *m); /* loaded images */
+/* Triangle soup in KDTree order: pos[9n], vnrm[9n] (vertex normals), uv[6n], kd[3n], ke[3n], tex[n]. */
+int chiaro_model_triangles(const chiaro_model *m, float *pos, float *vnrm, float *uv, float *kd, float *ke,
+                           int32_t *tex);
+int chiaro_model_texture(const chiaro_model *m, uint32_t i, int32_t *w, int32_t *h, int32_t *nc,
+                         const uint8_t **data);
+void chiaro_model_destroy(chiaro_model *m);
+
+/* KDTree without a device (host build only): for kd dumps and for callers that
+ * drive libchiaro_hip.so themselves.  Appends to the scene's lightTriangles. */
+chiaro_kdtree *chiaro_kdtree_create(chiaro_model *m, chiaro_scene *s, int threads);
+uint32_t chiaro_kdtree_num_nodes(const chiaro_kdtree *k);
+uint32_t chiaro_kdtree_num_refs(const chiaro_kdtree *k);
+int chiaro_kdtree_export(const chiaro_kdtree *k, uint32_t *is_leaf, uint32_t *axis, float *split, uint32_t *child,
+                         uint32_t *leaf_first, uint32_t *leaf_count, uint32_t *refs, float *box);
+/* Fill the C-ABI scene description (pointers valid while k and s live). */
+int chiaro_kdtree_describe(chiaro_kdtree *k, const chiaro_scene *s, cr_scene_desc *out);
+void chiaro_kdtree_destroy(chiaro_kdtree *k);
+
+chiaro_raytracer *chiaro_raytracer_create(chiaro_model *m, chiaro_scene *s, int device);
+int chiaro_raytracer_raytrace(chiaro_raytracer *r, const float eye[3], const float center[3], const float up[3],
+                              float yview);
+const float *chiaro_raytracer_pixels(const chiaro_raytracer *r);
+const uint8_t *chiaro_raytracer_data(chiaro_raytracer *r);
+float chiaro_raytracer_maxval(const chiaro_raytracer *r);
+uint32_t chiaro_raytracer_layers(const chiaro_raytracer *r);
+int chiaro_raytracer_counters(const chiaro_raytracer *r, cr_counters *out);
+int chiaro_raytracer_normalize(chiaro_raytracer *r, float exposure, float defog, float knee_low, float knee_high,
+                               float gamma);
+int chiaro_raytracer_export(chiaro_raytracer *r, const char *filename);
+cr_ctx *chiaro_raytracer_ctx(chiaro_raytracer *r);
+void chiaro_raytracer_destroy(chiaro_raytracer *r);
+
+int chiaro_camera(const float eye[3], const float center[3], const float up[3], float yview, uint32_t xres,
+                  uint32_t yres, cr_camera *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

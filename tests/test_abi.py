@@ -1,0 +1,64 @@
+"""The C-ABI libraries load and export every symbol their headers declare
+(no compute calls here: this runs without a GPU)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared(header: Path) -> set:
+    src = re.sub(r"/\*.*?\*/", "", header.read_text(), flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    names = set()
+    for m in re.finditer(r"^[A-Za-z_][\w \t\*]*?\b([a-z_][a-z0-9_]*)\s*\(", src, flags=re.M):
+        if not m.group(0).lstrip().startswith(("typedef", "#")):
+            names.add(m.group(1))
+    return names
+
+
+def test_headers_parse():
+    hip = declared(ROOT / "include" / "chiaro_hip.h")
+    assert {"cr_create", "cr_upload_scene", "cr_render", "cr_intersect", "cr_destroy"} <= hip
+    host = declared(ROOT / "include" / "chiaroscuro.h")
+    assert {"chiaro_scene_create", "chiaro_raytracer_raytrace", "chiaro_camera"} <= host
+
+
+@pytest.mark.parametrize("lib,header", [("libchiaro_hip.so", "chiaro_hip.h"), ("libchiaroscuro.so", "chiaroscuro.h")])
+def test_library_exports_every_declared_symbol(ca, lib, header):
+    ca.libs()
+    L = ctypes.CDLL(str(ca.LIB_DIR / lib))
+    names = declared(ROOT / "include" / header)
+    missing = [n for n in sorted(names) if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_binding_lists_cover_headers(ca):
+    assert set(ca.HIP_SYMBOLS) == declared(ROOT / "include" / "chiaro_hip.h")
+    assert set(ca.HOST_SYMBOLS) == declared(ROOT / "include" / "chiaroscuro.h")
+
+
+def test_no_device_fails_loudly(ca):
+    """Without a GPU the product reports an error instead of falling back to the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    hip, _ = ca.libs()
+    c = hip.cr_create(0)
+    assert c
+    rc = hip.cr_upload_scene(c, None)
+    assert rc != 0
+    assert hip.cr_last_error(c)
+    hip.cr_destroy(c)
+    with pytest.raises(RuntimeError):
+        d = ca.Device(0)
+        d.render(ca.camera((0, 0, 2), (0, 0, 0), (0, 1, 0), 1.0, 4, 4), ca.render_params(4, 4, 1, 3, 0))
+
+
+def test_oracle_is_not_linked_by_product():
+    """The product libraries never reference the oracle."""
+    for lib in ("libchiaro_hip.so", "libchiaroscuro.so"):
+        data = (ROOT / "chiaroscuro-raytracer_amd" / "lib" / lib).read_bytes()
+        assert b"liboracle" not in data and b"or_render" not in data

@@ -1,0 +1,171 @@
+"""GPU parity: the HIP render loop (through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact.  The kernels evaluate every float in the reference's order with
+-ffp-contract=off and correctly rounded div/sqrt, and share the oracle's RNG and
+sincos, so pixels, ray-query results and the query counters must be identical.
+(The north-star tolerance, per-pixel relative RMSE < 1e-4, is asserted too where
+the oracle uses glibc sinf/cosf instead of the shared sincos.)
+"""
+import numpy as np
+import pytest
+
+from helpers import Pair, assert_bitwise, rel_rmse
+
+pytestmark = pytest.mark.gpu
+
+ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths")
+
+
+@pytest.fixture(scope="module")
+def cornell(ca, po, scenes):
+    return Pair(ca, po, scenes.config_rtc("cornell"))
+
+
+@pytest.fixture(scope="module")
+def cornell_mm(ca, po, scenes):
+    return Pair(ca, po, scenes.config_rtc("cornell_box"))
+
+
+@pytest.fixture(scope="module")
+def sponza(ca, po, scenes):
+    return Pair(ca, po, scenes.config_rtc("sponza"))
+
+
+def _render_both(ca, pair, xres, yres, spp, k=6, seed=0xC41A05C0, layer=1, kernel=None, accum=None):
+    cam = pair.camera(ca, xres, yres)
+    p = ca.render_params(xres, yres, spp, k, seed, layer=layer)
+    if kernel is not None:
+        pair.dev.set_option("kernel", kernel)
+    g = pair.dev.render(cam, p, None if accum is None else accum[0].copy())
+    gc = pair.dev.counters()
+    o, oc = pair.oracle.render(cam.as_array(), xres, yres, spp, k, seed, layer=layer,
+                               pixels=None if accum is None else accum[1].copy())
+    return g, gc, o, oc
+
+
+@pytest.mark.parametrize("kernel", [0, 1])
+def test_cornell_bitexact(ca, cornell, kernel):
+    g, gc, o, oc = _render_both(ca, cornell, 64, 64, 4, kernel=kernel)
+    assert_bitwise(g, o, "cornell 64x64x4")
+    assert {k: gc[k] for k in ORACLE_KEYS} == oc
+    assert gc["pixels"] == 64 * 64
+    assert o.mean() > 0.01  # lit
+
+
+def test_cornell_mm_bitexact_odd_size(ca, cornell_mm):
+    # non-multiple-of-tile image: edge tiles are partial
+    g, gc, o, oc = _render_both(ca, cornell_mm, 45, 37, 16)
+    assert_bitwise(g, o, "cornell_box 45x37x16")
+    assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
+def test_sponza_bitexact_small(ca, sponza):
+    g, gc, o, oc = _render_both(ca, sponza, 96, 54, 2)
+    assert_bitwise(g, o, "sponza 96x54x2")
+    assert {k: gc[k] for k in ORACLE_KEYS} == oc
+    assert oc["tritest"] > 100 * oc["closest"] / 10
+
+
+def test_progressive_layers(ca, cornell):
+    """Layer L blends (old*(L-1) + mean)/L on device (src/rayTracer.cpp:64)."""
+    cam = cornell.camera(ca, 32, 32)
+    g = o = None
+    for layer in (1, 2, 3):
+        p = ca.render_params(32, 32, 2, 6, 7, layer=layer)
+        g = cornell.dev.render(cam, p, None)  # accumulator kept on the device ctx
+        o, _ = cornell.oracle.render(cam.as_array(), 32, 32, 2, 6, 7, layer=layer, pixels=o)
+        assert_bitwise(g, o, "layer %d" % layer)
+
+
+def test_depth_limits_and_background(ca, cornell):
+    for k in (1, 2, 9):
+        g, gc, o, oc = _render_both(ca, cornell, 24, 24, 3, k=k)
+        assert_bitwise(g, o, "k=%d" % k)
+        assert {kk: gc[kk] for kk in ORACLE_KEYS} == oc
+    cam = cornell.camera(ca, 16, 16)
+    p = ca.render_params(16, 16, 2, 3, 1, background=(0.25, 0.5, 1.0))
+    g = cornell.dev.render(cam, p)
+    o, _ = cornell.oracle.render(cam.as_array(), 16, 16, 2, 3, 1, bg=(0.25, 0.5, 1.0))
+    assert_bitwise(g, o, "background")
+
+
+def test_tiles_partition_invariance(ca, cornell):
+    """Rendering the tiles of nranks ranks one after another and blending on the
+    root equals the 1-rank render bit for bit."""
+    import torch
+    xres, yres, spp, tile = 70, 50, 3, 16
+    cam = cornell.camera(ca, xres, yres)
+    full = cornell.dev.render(cam, ca.render_params(xres, yres, spp, 6, 11, tile=tile))
+    for nranks in (2, 3):
+        p0 = ca.render_params(xres, yres, spp, 6, 11, nranks=nranks, tile=tile)
+        maxt = ca.Device.tiles_for_rank(p0, 0)
+        gathered = torch.zeros((nranks, maxt, tile, tile, 3), dtype=torch.float32, device="cuda")
+        for r in range(nranks):
+            p = ca.render_params(xres, yres, spp, 6, 11, rank=r, nranks=nranks, tile=tile)
+            cornell.dev.render_tiles_device(cam, p, gathered[r].data_ptr())
+        frame = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda")
+        cornell.dev.blend_tiles_device(p0, gathered.data_ptr(), frame.data_ptr())
+        torch.cuda.synchronize()
+        assert_bitwise(frame.cpu().numpy(), full, "tiles nranks=%d" % nranks)
+
+
+def test_ray_queries_bitexact(ca, sponza, cornell):
+    """G2: KDTree::intersectRay / intersectShadowRay KAT incl. axis-parallel rays and
+    origins on split planes (src/kdtree.cpp:196-344)."""
+    rng = np.random.default_rng(5)
+    for pair in (cornell, sponza):
+        box = pair.oracle.kd_export()["box"]
+        lo, hi = box[:3], box[3:]
+        n = 4096
+        o = lo + (hi - lo) * rng.random((n, 3), dtype=np.float32)
+        d = rng.normal(size=(n, 3)).astype(np.float32)
+        d[: n // 8, 1:] = 0.0                 # axis-parallel (inf/NaN slabs)
+        d[n // 8: n // 4, 0] = 0.0
+        e = pair.oracle.kd_export()
+        inner = np.nonzero(e["is_leaf"] == 0)[0][: n // 8]
+        for j, ni in enumerate(inner):         # origins exactly on split planes
+            o[n // 4 + j, e["axis"][ni]] = e["split"][ni]
+        g = pair.dev.intersect(o, d)
+        want = pair.oracle.intersect(o, d)
+        assert np.array_equal(g["hit"], want["hit"])
+        h = want["hit"] == 1
+        assert h.sum() > n // 4
+        assert np.array_equal(g["tri"][h], want["tri"][h])
+        assert np.array_equal(g["bary"][h].view(np.uint32), want["bary"][h].view(np.uint32))
+        assert np.array_equal(g["dist"][h].view(np.uint32), want["dist"][h].view(np.uint32))
+        ids, _ = pair.oracle.lights()
+        light = ids[rng.integers(0, len(ids), n)]
+        dist = (rng.random(n) * np.linalg.norm(hi - lo)).astype(np.float32)
+        assert np.array_equal(pair.dev.intersect_shadow(o, d, dist, light),
+                              pair.oracle.intersect_shadow(o, d, dist, light))
+
+
+def test_north_star_tolerance_vs_glibc_trig(ca, po, cornell):
+    """With the oracle on glibc sinf/cosf (src/brdf.cpp:52-53 as compiled), the GPU
+    image stays within the north-star per-pixel tolerance (relative RMSE < 1e-4)."""
+    po.set_trig_mode(1)
+    try:
+        g, _, o, _ = _render_both(ca, cornell, 64, 64, 8)
+    finally:
+        po.set_trig_mode(0)
+    assert rel_rmse(g, o) < 1e-4
+
+
+def test_raytracer_api_layers(ca, scenes):
+    """RayTracer(Model&, Scene&).rayTrace twice with one camera -> layer 2 (src/rayTracer.cpp:24-33)."""
+    rtc = scenes.config_rtc("cornell")
+    sc = ca.Scene(rtc, "xres", "40", "yres", "30", "samples", "2")
+    m = ca.Model(sc)
+    rt = ca.RayTracer(m, sc)
+    i = sc.info
+    rt.rayTrace(i["VP"], i["LA"], i["UP"], i["yview"])
+    a = rt.pixels
+    rt.rayTrace(i["VP"], i["LA"], i["UP"], i["yview"])
+    assert rt.layers == 2
+    b = rt.pixels
+    assert not np.array_equal(a, b)
+    assert rt.maxVal == float(b.max())
+    rt.rayTrace(i["VP"], i["LA"], (0.2, 1.0, 0.0), i["yview"])  # up alone: no reset (reference quirk)
+    assert rt.layers == 3
+    rt.rayTrace((0.0, 1.1, 2.9), i["LA"], i["UP"], i["yview"])
+    assert rt.layers == 1

@@ -1,0 +1,95 @@
+"""Pin the oracle against golden vectors produced by the reference's own code.
+
+tests/golden/ref_*.json come from oracle/_ref (tests/golden/make_ref_golden.py):
+the reference's src/mesh.cpp (Texture::getColorAt) and its vendored glm 0.9.8.5
+compiled unmodified.  Everything is compared bit for bit.
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def f32(bits):
+    return np.asarray(bits, np.uint32).view(np.float32)
+
+
+def test_texture_lookup_matches_reference(po):
+    """G5: Texture::getColorAt (src/mesh.cpp:21-35): wrap loops, nearest texel, edge over-read."""
+    data = json.loads((GOLD / "ref_texture.json").read_text())
+    n = 0
+    for t in data["textures"]:
+        w, h, nc, salt = t["w"], t["h"], t["nc"], t["salt"]
+        i = np.arange(w * h * nc, dtype=np.uint64)
+        img = ((i * 2654435761 + salt) >> np.uint64(7)).astype(np.uint8)
+        tris = {"pos": np.zeros((1, 9), np.float32), "vnrm": np.zeros((1, 9), np.float32),
+                "uv": np.zeros((1, 6), np.float32), "kd": np.zeros((1, 3), np.float32),
+                "ke": np.zeros((1, 3), np.float32), "tex": np.zeros(1, np.int32)}
+        tris["pos"][0] = [0, 0, 0, 1, 0, 0, 0, 1, 0]
+        sc = po.OracleScene(tris, textures=[(w, h, nc, img)])
+        for c in t["cases"]:
+            u, v = f32([c["u"]])[0], f32([c["v"]])[0]
+            got = sc.tex_lookup(0, u, v)
+            assert np.array_equal(got.view(np.uint32), np.asarray(c["rgb"], np.uint32)), (w, h, nc, u, v)
+            n += 1
+    assert n == 4 * 144
+
+
+def test_camera_matches_reference_glm(po, ca):
+    """G6: camera basis of src/rayTracer.cpp:41-49 over the reference's glm; oracle AND host product."""
+    data = json.loads((GOLD / "ref_glm.json").read_text())
+    for c in data["camera"]:
+        args = (c["eye"], c["center"], c["up"], c["yview"], c["xres"], c["yres"])
+        want = np.asarray(c["out"], np.uint32)
+        assert np.array_equal(po.camera(*args).view(np.uint32), want), c
+        assert np.array_equal(ca.camera(*args).as_array().view(np.uint32), want), c
+
+
+def test_glm_primitives_match_reference(po):
+    """normalize / cross / dot / distance with glm 0.9.8.5's evaluation order."""
+    import ctypes as C
+    L = po.lib()
+    data = json.loads((GOLD / "ref_glm.json").read_text())
+    FP = C.POINTER(C.c_float)
+    for p in data["primitives"]:
+        a, b = f32(p["a"]).copy(), f32(p["b"]).copy()
+        out = np.zeros(3, np.float32)
+        L.or_glm_normalize(a.ctypes.data_as(FP), out.ctypes.data_as(FP))
+        assert np.array_equal(out.view(np.uint32), np.asarray(p["normalize"], np.uint32), equal_nan=False) or \
+            (np.isnan(out).all() and np.isnan(f32(p["normalize"])).all())
+        L.or_glm_cross(a.ctypes.data_as(FP), b.ctypes.data_as(FP), out.ctypes.data_as(FP))
+        assert np.array_equal(out.view(np.uint32), np.asarray(p["cross"], np.uint32))
+        d = np.float32(L.or_glm_dot(a.ctypes.data_as(FP), b.ctypes.data_as(FP)))
+        assert d.view(np.uint32) == p["dot"]
+        d = np.float32(L.or_glm_distance(a.ctypes.data_as(FP), b.ctypes.data_as(FP)))
+        assert d.view(np.uint32) == p["distance"]
+
+
+def test_kdtree_material_primitives_match_reference(po):
+    """Material normal (src/kdtree.cpp:58-60) and light surface (src/kdtree.cpp:72-77)."""
+    import ctypes as C
+    L = po.lib()
+    FP = C.POINTER(C.c_float)
+    data = json.loads((GOLD / "ref_glm.json").read_text())
+    assert data["triangles"]
+    for t in data["triangles"]:
+        p = f32(t["p"]).copy()
+        out = np.zeros(3, np.float32)
+        L.or_material_normal(p.ctypes.data_as(FP), out.ctypes.data_as(FP))
+        assert np.array_equal(out.view(np.uint32), np.asarray(t["material_normal"], np.uint32))
+        s = np.float32(L.or_light_surface(p.ctypes.data_as(FP)))
+        assert s.view(np.uint32) == t["surface"]
+
+
+@pytest.mark.skipif(not Path("/root/reference").exists(), reason="reference only present in the build container")
+def test_goldens_are_current():
+    """Re-running the generator reproduces the committed fixtures (build container only)."""
+    import subprocess
+    import sys
+    before = {p.name: p.read_bytes() for p in GOLD.glob("ref_*.json")}
+    subprocess.run([sys.executable, str(GOLD / "make_ref_golden.py")], check=True, capture_output=True)
+    after = {p.name: p.read_bytes() for p in GOLD.glob("ref_*.json")}
+    assert before == after
