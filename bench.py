@@ -134,12 +134,15 @@ def main():
             c = dev.counters()
             totals["rays"] += c["closest"] + c["shadow"]
             totals["kernel_ms"] += dev.last_kernel_ms()
-            totals["bytes"] += ca.algorithmic_bytes(c, c["pixels"])
-            totals["tritest"] += c["tritest"]
             totals["px"] += c["pixels"]
             totals["launches"] += 1
 
+    # Timed launches count only rays; the node/leaf/triangle counters of SURVEY §8d
+    # (algorithmic bytes) come from one extra, untimed launch of the counting
+    # variant on the first timed layer (results are deterministic per layer).
+    dev.set_option("counters", 0)
     layer = 1
+    first_timed = args.warmup + 1
     for w in range(args.warmup):
         step(layer, False)
         layer += 1
@@ -168,10 +171,23 @@ def main():
     else:
         rays_all = float(totals["rays"])
 
+    # counting pass (untimed): algorithmic bytes of one launch of this rank
+    dev.set_option("counters", 1)
+    pc = ca.render_params(xres, yres, spp, k, seed, layer=first_timed, rank=rank, nranks=world, tile=tile)
+    scratch = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda")
+    if world == 1:
+        dev.render_device(cam, pc, scratch.data_ptr(), stream)
+    else:
+        dev.render_tiles_device(cam, pc, tiles.data_ptr(), stream)
+    cc = dev.counters()
+    totals["bytes"] = ca.algorithmic_bytes(cc, cc["pixels"])
+    totals["tritest"] = cc["tritest"]
+    totals["count_rays"] = cc["closest"] + cc["shadow"]
+
     if rank == 0:
         value = rays_all / elapsed / 1e6
         kms = totals["kernel_ms"] / max(totals["launches"], 1)
-        bytes_per_launch = totals["bytes"] / max(totals["launches"], 1)
+        bytes_per_launch = totals["bytes"]  # counting pass: one launch, same size as a timed one
         achieved = bytes_per_launch / (kms / 1e3) / 1e9 if kms > 0 else 0.0
         traffic = None
         pmc = ROOT / "profiles" / ("pmc_%s.json" % args.config)
@@ -202,7 +218,7 @@ def main():
             "data": "synthetic scene (deterministic generator), seeded counter RNG",
             "config": {"workload": label, "spp_per_step": spp, "k": k, "tile": tile,
                        "parallelism": "tile-split x%d" % world, "rays": int(rays_all),
-                       "mean_tritest_per_ray": round(totals["tritest"] / max(totals["rays"], 1), 2)},
+                       "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "render", "kernel_ms": round(kms, 3),

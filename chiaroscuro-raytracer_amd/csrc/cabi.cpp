@@ -30,9 +30,12 @@ struct cr_ctx {
     uint32_t *d_work = nullptr;
     float *d_accum = nullptr;
     size_t accum_elems = 0;
+    void *d_gstack = nullptr, *d_pathbuf = nullptr;
+    size_t gstack_bytes = 0, pathbuf_bytes = 0;
     cr_counters last{};
     // options
     int kernel = 0;
+    int full_counters = 1;
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
 };
@@ -113,6 +116,7 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.out = out;
     A.counters = c->d_counters;
     A.work = c->d_work;
+    A.full_counters = c->full_counters;
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -122,6 +126,29 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     HIPCHK(hipSetDevice(c->device));
     cr::RenderArgs A{};
     fill_args(c, A, cam, p, out, mode);
+    if (c->kernel == 0) {
+        uint32_t blk, blocks;
+        cr::persistent_geometry(c->num_cus, c->waves_per_cu, blk, blocks);
+        A.gstride = blk * blocks;
+        const size_t gs = cr::persistent_gstack_bytes(c->stack_depth, A.gstride);
+        const size_t pb = cr::persistent_pathbuf_bytes(p->k, A.gstride);
+        if (gs > c->gstack_bytes) {
+            if (c->d_gstack) hipFree(c->d_gstack);
+            c->d_gstack = nullptr;
+            c->gstack_bytes = 0;
+            if (hipMalloc(&c->d_gstack, gs) != hipSuccess) return fail(c, CR_E_OOM, "stack overflow area");
+            c->gstack_bytes = gs;
+        }
+        if (pb > c->pathbuf_bytes) {
+            if (c->d_pathbuf) hipFree(c->d_pathbuf);
+            c->d_pathbuf = nullptr;
+            c->pathbuf_bytes = 0;
+            if (hipMalloc(&c->d_pathbuf, pb) != hipSuccess) return fail(c, CR_E_OOM, "path buffer");
+            c->pathbuf_bytes = pb;
+        }
+        A.gstack = (uint2 *)c->d_gstack;
+        A.pathbuf = (float4 *)c->d_pathbuf;
+    }
     HIPCHK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), st));
     HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
     HIPCHK(hipEventRecord(c->ev0, st));
@@ -175,6 +202,8 @@ void cr_destroy(cr_ctx *c) {
         hipSetDevice(c->device);
         free_scene(c);
         if (c->d_accum) hipFree(c->d_accum);
+        if (c->d_gstack) hipFree(c->d_gstack);
+        if (c->d_pathbuf) hipFree(c->d_pathbuf);
         if (c->d_counters) hipFree(c->d_counters);
         if (c->d_work) hipFree(c->d_work);
         if (c->ev0) hipEventDestroy(c->ev0);
@@ -414,6 +443,7 @@ float cr_last_kernel_ms(cr_ctx *c) { return c ? c->last_ms : 0.f; }
 int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!c || !key) return CR_E_INVALID;
     if (!std::strcmp(key, "kernel") && (v == 0 || v == 1)) c->kernel = (int)v;
+    else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);

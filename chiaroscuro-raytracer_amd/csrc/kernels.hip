@@ -21,9 +21,13 @@
 
 namespace cr {
 
+// Query counters (cr_counters order).  Per-lane by default; the persistent kernel
+// keeps the per-query ones as wave-uniform tallies taken with __ballot at
+// converged points (flag `uniform` bit i set -> field i is already a wave total).
 struct Ctr {
-    uint32_t closest, shadow, inner, leaf, tritest, hit, texhit, paths, pixels;
+    uint32_t closest = 0, shadow = 0, inner = 0, leaf = 0, tritest = 0, hit = 0, texhit = 0, paths = 0, pixels = 0;
 };
+__device__ __forceinline__ uint32_t wave_count(bool pred) { return (uint32_t)__popcll(__ballot(pred)); }
 
 struct Stack {
     uint32_t *node;
@@ -288,13 +292,17 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, uint32_t x, uin
     }
 }
 
-__device__ __forceinline__ void flush_counters(unsigned long long *ctrs, Ctr &c) {
-    uint32_t v[9] = {c.closest, c.shadow, c.inner, c.leaf, c.tritest, c.hit, c.texhit, c.paths, c.pixels};
+// Call with the whole wave converged.  Fields whose bit is set in `uniform` are
+// wave totals already; the others are summed over the 64 lanes.
+__device__ __forceinline__ void flush_counters(unsigned long long *ctrs, const Ctr &c, uint32_t uniform = 0u) {
+    const uint32_t v[9] = {c.closest, c.shadow, c.inner, c.leaf, c.tritest, c.hit, c.texhit, c.paths, c.pixels};
 #pragma unroll
     for (int i = 0; i < 9; i++) {
         unsigned long long s = v[i];
+        if (!(uniform & (1u << i))) {
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+            for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+        }
         if ((threadIdx.x & 63) == 0 && s) atomicAdd(&ctrs[i], s);
     }
 }
@@ -317,6 +325,285 @@ __global__ void __launch_bounds__(128) render_simple(RenderArgs A) {
         c.pixels++;
     }
     flush_counters(A.counters, c);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 0: persistent waves with per-lane path regeneration.
+//
+// Every lane owns one pixel at a time and runs its samples one after another
+// (so the per-pixel sum keeps the reference's sample order), but a lane never
+// waits for the rest of its wave between queries: each outer iteration every live
+// lane runs exactly one kd query -- a camera/bounce ray (closest hit) or a NEE
+// shadow ray (any hit) -- in ONE traversal loop, then advances its own path state
+// machine (shade / start shadow ray / bounce / finish sample / next pixel).
+// Pixels are handed out wave-wide: one atomicAdd per refill, lanes ranked by
+// __ballot + mbcnt.
+//
+// Traversal stack: 8-byte entries {far node, tmax}.  The far child's tmin is the
+// current tmax at pop time (it always equals the split distance stored implicitly
+// -- see DESIGN.md "stack invariant"), so the reference's (node, tmin, tmax)
+// recursion state fits in half the bytes.  The top R entries live in an LDS ring
+// laid out [slot][thread] (each lane on its own bank pair); deeper entries spill
+// to a per-lane global overflow area.
+// Per-bounce (direct, w) pairs for the back-to-front fold go to a per-lane global
+// buffer instead of registers, keeping the VGPR budget for occupancy.
+enum : uint32_t { ST_NEED_PIXEL = 0, ST_NEW_SAMPLE = 1, ST_CLOSEST = 2, ST_SHADOW = 3, ST_DONE = 4 };
+
+template <int R, bool FULL>
+__device__ __forceinline__ bool traverse_ring(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
+                                              uint32_t gid, f3 o, f3 d, bool shadow, float limit, uint32_t exclude,
+                                              uint32_t &tri, float &bx, float &by, Ctr &c) {
+    float tmin, tmax;
+    ray_box(S, o, d, tmin, tmax);
+    if (shadow) {
+        if (tmax < 0 || tmax < tmin || tmin > limit) return false;
+        tmax = std_min(tmax, limit);
+    } else {
+        if (tmax < 0 || tmax < tmin) return false;
+    }
+    const uint32_t bdim = blockDim.x, tid = threadIdx.x;
+    uint32_t sp = 0, nl = 0, node = 0;
+    for (;;) {
+        uint2 nd = S.nodes[node];
+        while ((nd.y & 3u) != 3u) {
+            if (FULL) c.inner++;
+            const uint32_t a = nd.y & 3u;
+            const float split = __uint_as_float(nd.x);
+            const float oa = comp(o, a), da = comp(d, a);
+            const float tsplit = (split - oa) / da;
+            const uint32_t below = (oa < split) || (oa == split && da <= 0);
+            const uint32_t child = nd.y >> 2;
+            if (tsplit >= tmax || tsplit < 0) {
+                node = child + (1u - below);
+            } else if (tsplit <= tmin) {
+                node = child + below;
+            } else {
+                const uint2 e = make_uint2(child + below, __float_as_uint(tmax));
+                const uint32_t slot = (sp & (R - 1)) * bdim + tid;
+                if (nl == R) gstk[(size_t)(sp - R) * gstride + gid] = ring[slot]; // spill the oldest
+                else nl++;
+                ring[slot] = e;
+                sp++;
+                node = child + (1u - below);
+                tmax = tsplit;
+            }
+            nd = S.nodes[node];
+        }
+        if (FULL) c.leaf++;
+        const uint32_t first = nd.x, count = nd.y >> 2;
+        bool found = false;
+        for (uint32_t j = 0; j < count; j++) {
+            const float4 r0 = S.recs[3 * (first + j)];
+            const float4 r1 = S.recs[3 * (first + j) + 1];
+            const float4 r2 = S.recs[3 * (first + j) + 2];
+            const uint32_t id = __float_as_uint(r0.w);
+            if (shadow && id == exclude) continue;
+            if (FULL) c.tritest++;
+            const f3 v0 = ld3(r0), e1 = ld3(r1), e2 = ld3(r2);
+            const f3 p = cross(d, e2);
+            const float aa = dot(e1, p);
+            if (aa < 1.19209290e-7F && aa > -1.19209290e-7F) continue;
+            const float f = 1.f / aa;
+            const f3 sv = sub(o, v0);
+            const float ux = f * dot(sv, p);
+            if (ux < 0.f || ux > 1.f) continue;
+            const f3 q = cross(sv, e1);
+            const float uy = f * dot(d, q);
+            if (uy < 0.f || uy + ux > 1.f) continue;
+            const float t = f * dot(e2, q);
+            if (t >= 0.f && t < tmax) {
+                if (shadow) return true;
+                bx = ux;
+                by = uy;
+                tmax = t;
+                tri = id;
+                found = true;
+            }
+        }
+        if (found) return true;
+        if (sp == 0) return false;
+        sp--;
+        uint2 e;
+        if (nl) {
+            e = ring[(sp & (R - 1)) * bdim + tid];
+            nl--;
+        } else {
+            e = gstk[(size_t)sp * gstride + gid];
+        }
+        node = e.x;
+        tmin = tmax; // == split distance of the popped entry (stack invariant)
+        tmax = __uint_as_float(e.y);
+    }
+}
+
+template <int R, bool FULL>
+__global__ void __launch_bounds__(256) render_persistent(RenderArgs A) {
+    extern __shared__ uint2 ring_lds[];
+    const DevScene &S = A.S;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const f3 eye = mk(A.cam[0], A.cam[1], A.cam[2]);
+    Ctr c = {};
+
+    uint32_t state = ST_NEED_PIXEL;
+    uint32_t px = 0, py = 0, slot = 0, s = 0;
+    f3 temp = mk(0.f, 0.f, 0.f);
+    Rng rng{0u, 0u};
+    int k = 1;
+    f3 o = eye, d = mk(0.f, 0.f, 1.f);
+    float limit = 0.f;
+    uint32_t exclude = 0xffffffffu;
+    f3 p = mk(0.f, 0.f, 0.f), normal = p, fcol = p, direct = p, contrib = p;
+
+    for (;;) {
+        // ---- wave-wide pixel refill (ballot + mbcnt ranks, one atomic per refill)
+        for (;;) {
+            const uint64_t need = __ballot(state == ST_NEED_PIXEL);
+            if (!need) break;
+            const uint32_t n = (uint32_t)__popcll(need);
+            const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(A.work, n);
+            base = __shfl(base, (int)leader, 64);
+            if (state == ST_NEED_PIXEL) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint32_t item = base + rank;
+                if (item >= A.n_items) {
+                    state = ST_DONE;
+                } else if (item_pixel(A, item, px, py, slot)) {
+                    state = ST_NEW_SAMPLE;
+                    s = 0;
+                    temp = mk(0.f, 0.f, 0.f);
+                } // else: partial-tile pixel outside the image, fetch again
+            }
+        }
+        c.paths += wave_count(state == ST_NEW_SAMPLE);
+        if (state == ST_NEW_SAMPLE) {
+            rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
+            o = eye;
+            d = camera_dir(A, px, py, rng);
+            k = 1;
+            state = ST_CLOSEST;
+        }
+        if (!__any(state != ST_DONE)) break;
+
+        // ---- one kd query per live lane
+        const bool shadow = state == ST_SHADOW;
+        c.shadow += wave_count(shadow);
+        c.closest += wave_count(state == ST_CLOSEST);
+        uint32_t t = 0;
+        float bx = 0.f, by = 0.f;
+        bool h = false;
+        if (state == ST_CLOSEST || state == ST_SHADOW)
+            h = traverse_ring<R, FULL>(S, ring_lds, A.gstack, A.gstride, gid, o, d, shadow, limit, exclude, t, bx, by, c);
+        c.hit += wave_count(state == ST_CLOSEST && h);
+
+        // ---- advance the path state machine (RayTracer::sendRay, rayTracer.cpp:76-135)
+        bool bounce = false, finish = false, textured = false, pixel_done = false;
+        f3 tail = mk(0.f, 0.f, 0.f);
+        if (state == ST_SHADOW) {
+            if (!h) direct = add(direct, contrib);
+            bounce = true;
+        } else if (state == ST_CLOSEST) {
+            if (!h) {
+                tail = mk(A.bg[0], A.bg[1], A.bg[2]);
+                finish = true;
+            } else {
+                const float4 nrm4 = S.mat_n[t];
+                normal = ld3(nrm4);
+                const float bz = (1.f - bx - by);
+                p = add(add(muls(ld3(S.tri[3 * t]), bz), muls(ld3(S.tri[3 * t + 1]), bx)),
+                        muls(ld3(S.tri[3 * t + 2]), by));
+                const float4 kd4 = S.mat_kd[t];
+                f3 Kd = ld3(kd4);
+                const int ti = __float_as_int(kd4.w);
+                if (ti >= 0) {
+                    const float2 ua = S.mat_uv[3 * t], ub = S.mat_uv[3 * t + 1], uc = S.mat_uv[3 * t + 2];
+                    Kd = tex_lookup(S, ti, (ua.x * bz + ub.x * bx) + uc.x * by, (ua.y * bz + ub.y * bx) + uc.y * by);
+                    textured = true;
+                }
+                fcol = muls(Kd, (float)0.31830988618379067154);
+                const f3 wo = normalize(sub(o, p));
+                if (k > 1) {
+                    direct = mk(0.f, 0.f, 0.f);
+                } else {
+                    const bool emissive = __float_as_uint(nrm4.w) != 0u;
+                    const f3 rad = emissive ? ld3(S.mat_ke[t]) : mk(0.f, 0.f, 0.f);
+                    direct = muls(rad, std_max(0.f, dot(wo, normal)));
+                }
+                if (S.nlights) {
+                    const uint32_t li = rng_index(rng, S.nlights);
+                    const uint2 L = S.lights[li];
+                    const uint32_t lid = L.x;
+                    const float v0 = rng_uniform(rng, 0.f, 1.f);
+                    const float v1 = rng_uniform(rng, 0.f, 1.f - v0);
+                    const f3 lp = add(add(muls(ld3(S.tri[3 * lid]), v0), muls(ld3(S.tri[3 * lid + 1]), v1)),
+                                      muls(ld3(S.tri[3 * lid + 2]), 1.f - v0 - v1));
+                    const float distance = distance3(p, lp);
+                    const f3 wl = normalize(sub(lp, p));
+                    // the NEE term does not depend on the shadow result: evaluate it now
+                    const float geometric = std_max(
+                        0.f, dot(normal, wl) * dot(neg(wl), ld3(S.mat_n[lid])) / (1.f + distance * distance));
+                    contrib = mul(muls(ld3(S.mat_ke[lid]), geometric * __uint_as_float(L.y) * (float)S.nlights), fcol);
+                    o = add(p, muls(normal, 0.001f));
+                    d = wl;
+                    limit = distance;
+                    exclude = lid;
+                    state = ST_SHADOW;
+                } else {
+                    bounce = true;
+                }
+            }
+        }
+        if (bounce) {
+            if (k == A.K) {
+                tail = direct;
+                finish = true;
+            } else {
+                const float sx = rng_uniform(rng, -1.f, 1.f);
+                const float sy = rng_uniform(rng, -1.f, 1.f);
+                f3 wi;
+                float pdf;
+                sample_wi(normal, sx, sy, wi, pdf);
+                const float Kmax = std_max(std_max(fcol.x, fcol.y), fcol.z);
+                if (pdf == 0.f || rng_uniform(rng, 0.f, 1.f) > Kmax) {
+                    tail = direct;
+                    finish = true;
+                } else {
+                    const float cosine = fabsf(dot(normal, wi));
+                    const f3 w = divs(muls(fcol, cosine), pdf * Kmax);
+                    A.pathbuf[(size_t)(2 * (k - 1)) * A.gstride + gid] = make_float4(direct.x, direct.y, direct.z, 0.f);
+                    A.pathbuf[(size_t)(2 * (k - 1) + 1) * A.gstride + gid] = make_float4(w.x, w.y, w.z, 0.f);
+                    o = add(p, muls(normal, 0.001f));
+                    d = wi;
+                    k++;
+                    state = ST_CLOSEST;
+                }
+            }
+        }
+        if (finish) {
+            f3 acc = tail; // back-to-front fold r_j = D_j + W_j * r_{j+1}
+            for (int j = k - 2; j >= 0; j--) {
+                const float4 Dj = A.pathbuf[(size_t)(2 * j) * A.gstride + gid];
+                const float4 Wj = A.pathbuf[(size_t)(2 * j + 1) * A.gstride + gid];
+                acc = add(ld3(Dj), mul(ld3(Wj), acc));
+            }
+            temp = add(temp, acc);
+            s++;
+            if (s == A.spp) {
+                write_pixel(A, px, py, slot, temp);
+                pixel_done = true;
+                state = ST_NEED_PIXEL;
+            } else {
+                state = ST_NEW_SAMPLE;
+            }
+        }
+        c.texhit += wave_count(textured);
+        c.pixels += wave_count(pixel_done);
+    }
+    // closest, shadow, hit, texhit, paths, pixels are wave tallies
+    flush_counters(A.counters, c, (1u << 0) | (1u << 1) | (1u << 5) | (1u << 6) | (1u << 7) | (1u << 8));
 }
 
 // ---------------------------------------------------------------------------
@@ -371,11 +658,27 @@ __global__ void __launch_bounds__(256) blend_tiles_kernel(BlendArgs B) {
 }
 
 // ---------------------------------------------------------------- launch --
+static const int RING = 8; // LDS ring entries per lane (8 B each)
+
+void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks) {
+    block = 256;
+    if (waves_per_cu == 0) waves_per_cu = 24;
+    blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * ((waves_per_cu * 64 + block - 1) / block);
+}
+
 int launch_render(const RenderArgs &A, int kernel, uint32_t block, uint32_t waves_per_cu, int num_cus,
                   hipStream_t st) {
-    (void)kernel;
-    (void)waves_per_cu;
-    (void)num_cus;
+    if (kernel == 0) {
+        uint32_t blk, blocks;
+        persistent_geometry(num_cus, waves_per_cu, blk, blocks);
+        if (A.gstride < blk * blocks) return (int)hipErrorInvalidValue;
+        const size_t lds = (size_t)RING * blk * sizeof(uint2);
+        if (A.full_counters)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(render_persistent<RING, true>), dim3(blocks), dim3(blk), lds, st, A);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(render_persistent<RING, false>), dim3(blocks), dim3(blk), lds, st, A);
+        return (int)hipGetLastError();
+    }
     block = 128;
     const size_t lds = (size_t)3 * A.stack_depth * block * sizeof(uint32_t);
     const uint32_t grid = (A.n_items + block - 1) / block;

@@ -41,7 +41,18 @@ struct RenderArgs {
     float *out;
     unsigned long long *counters; // 9 x u64
     uint32_t *work;               // persistent-kernel work counter (zeroed per launch)
+    // persistent kernel only
+    uint2 *gstack;                // traversal-stack overflow [stack_depth][gstride] {node, tmax bits}
+    float4 *pathbuf;              // per-bounce (direct, w) [2*K][gstride]
+    uint32_t gstride;             // threads in the persistent grid
+    int full_counters;            // 1: also count inner/leaf/tritest (SURVEY §8d bytes)
 };
+
+// Workspace the persistent kernel needs for a grid of `threads` lanes.
+inline size_t persistent_gstack_bytes(uint32_t depth, uint32_t threads) { return (size_t)depth * threads * 8; }
+inline size_t persistent_pathbuf_bytes(int K, uint32_t threads) { return (size_t)2 * K * threads * 16; }
+// Persistent grid geometry chosen by launch_render (block threads, blocks).
+void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);
 
 struct QueryArgs {
     DevScene S;
