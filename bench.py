@@ -72,7 +72,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza", help="cornell | cornell_box | sponza | sponza_4k")
     ap.add_argument("--spp", type=int, default=0, help="override samples per step (default: config's)")
-    ap.add_argument("--kernel", type=int, default=-1)
+    ap.add_argument("--kernel", type=int, default=-1, help="0 persistent (default), 1 one-thread-per-pixel")
+    ap.add_argument("--variant", type=int, default=-1, help="persistent-kernel variant (default 0)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -105,6 +106,8 @@ def main():
     dev.upload(kd.describe())
     if args.kernel >= 0:
         dev.set_option("kernel", args.kernel)
+    if args.variant >= 0:
+        dev.set_option("variant", args.variant)
     if rank == 0:
         log("scene %s: %d tris, load+kd+upload %.1fs" % (args.config, model.num_triangles, time.time() - t0))
     xres, yres, k, seed = info["xres"], info["yres"], info["k"], info["seed"]

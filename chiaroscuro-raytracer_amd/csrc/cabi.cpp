@@ -36,6 +36,7 @@ struct cr_ctx {
     // options
     int kernel = 0;
     int full_counters = 1;
+    int variant = 0;
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
 };
@@ -117,6 +118,7 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.counters = c->d_counters;
     A.work = c->d_work;
     A.full_counters = c->full_counters;
+    A.variant = c->variant;
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -444,6 +446,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!c || !key) return CR_E_INVALID;
     if (!std::strcmp(key, "kernel") && (v == 0 || v == 1)) c->kernel = (int)v;
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
+    else if (!std::strcmp(key, "variant") && v >= 0 && v < cr::num_persistent_variants()) c->variant = (int)v;
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);

@@ -46,11 +46,19 @@ struct RenderArgs {
     float4 *pathbuf;              // per-bounce (direct, w) [2*K][gstride]
     uint32_t gstride;             // threads in the persistent grid
     int full_counters;            // 1: also count inner/leaf/tritest (SURVEY §8d bytes)
+    int variant;                  // persistent-kernel variant index (kernels.hip kVariants)
 };
+int num_persistent_variants();
 
-// Workspace the persistent kernel needs for a grid of `threads` lanes.
+// Workspace the persistent kernel needs for a grid of `threads` lanes:
+// stack overflow [depth][threads] x 8 B; lane buffer = PARK_SLOTS parked-state
+// float4s + (direct, w) float4 pairs per bounce, each [slot][threads].
+enum { PARK_SLOTS = 5 };
 inline size_t persistent_gstack_bytes(uint32_t depth, uint32_t threads) { return (size_t)depth * threads * 8; }
-inline size_t persistent_pathbuf_bytes(int K, uint32_t threads) { return (size_t)2 * K * threads * 16; }
+inline size_t persistent_pathbuf_bytes(int K, uint32_t threads) {
+    return (size_t)(PARK_SLOTS + 2 * K) * threads * 16;
+}
+int launch_persistent(const RenderArgs &A, uint32_t waves_per_cu, int num_cus, hipStream_t st);
 // Persistent grid geometry chosen by launch_render (block threads, blocks).
 void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);
 
