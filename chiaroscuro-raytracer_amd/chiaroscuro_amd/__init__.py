@@ -41,7 +41,8 @@ class CrRenderParams(C.Structure):
                 ("nranks", C.c_uint32), ("tile", C.c_uint32)]
 
 
-COUNTER_NAMES = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths", "pixels")
+COUNTER_NAMES = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths", "pixels",
+                 "wave_desc", "wave_tri", "wave_round", "wave_query")
 
 
 class CrCounters(C.Structure):

@@ -161,7 +161,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     HIPCHK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]};
+    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]};
     return CR_OK;
 }
 
@@ -419,7 +419,7 @@ static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, cons
     if (e == hipSuccess) e = hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost);
     hipFree(buf);
     if (e != hipSuccess) return hip_fail(c, e, "intersect");
-    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]};
+    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]};
     return CR_OK;
 }
 

@@ -58,7 +58,7 @@ __device__ __forceinline__ bool traverse(const DevScene &S, const Stack &stk, f3
             const uint32_t a = nd.y & 3u;
             const float split = __uint_as_float(nd.x);
             const float oa = comp(o, a), da = comp(d, a);
-            const float tsplit = (split - oa) / da;
+            const float tsplit = split_distance(split, oa, da);
             const uint32_t below = (oa < split) || (oa == split && da <= 0);
             const uint32_t child = nd.y >> 2;
             if (tsplit >= tmax || tsplit < 0) {

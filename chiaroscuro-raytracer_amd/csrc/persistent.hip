@@ -42,11 +42,14 @@ __device__ __forceinline__ bool traverse_ring(const DevScene &S, uint2 *ring, ui
     for (;;) {
         uint2 nd = S.nodes[node];
         while ((nd.y & 3u) != 3u) {
-            if (FULL) c.inner++;
+            if (FULL) {
+                c.inner++;
+                if (wave_leader()) c.wave_desc++;
+            }
             const uint32_t a = nd.y & 3u;
             const float split = __uint_as_float(nd.x);
             const float oa = comp(o, a), da = comp(d, a);
-            const float tsplit = (split - oa) / da;
+            const float tsplit = split_distance(split, oa, da);
             const uint32_t below = (oa < split) || (oa == split && da <= 0);
             const uint32_t child = nd.y >> 2;
             if (tsplit >= tmax || tsplit < 0) {
@@ -65,7 +68,10 @@ __device__ __forceinline__ bool traverse_ring(const DevScene &S, uint2 *ring, ui
             }
             nd = S.nodes[node];
         }
-        if (FULL) c.leaf++;
+        if (FULL) {
+            c.leaf++;
+            if (wave_leader()) c.wave_round++;
+        }
         const uint32_t first = nd.x, count = nd.y >> 2;
         bool found = false;
         float4 n0, n1, n2;
@@ -75,6 +81,7 @@ __device__ __forceinline__ bool traverse_ring(const DevScene &S, uint2 *ring, ui
             n2 = S.recs[3 * first + 2];
         }
         for (uint32_t j = 0; j < count; j++) {
+            if (FULL && wave_leader()) c.wave_tri++;
             float4 r0, r1, r2;
             if (PF) { // software pipeline: issue triangle j+1's loads before testing j
                 r0 = n0;
@@ -213,6 +220,7 @@ __global__ void __launch_bounds__(256, MINW) render_persistent(RenderArgs A) {
 
     for (;;) {
         if (!__any(state != ST_DONE)) break;
+        if (FULL && wave_leader()) c.wave_query++;
         // ---- one kd query per live lane
         const bool shadow = state == ST_SHADOW;
         c.shadow += wave_count(shadow);

@@ -10,14 +10,21 @@ namespace cr {
 // converged points (flush_counters' `uniform` bit i set -> field i is a wave total).
 struct Ctr {
     uint32_t closest = 0, shadow = 0, inner = 0, leaf = 0, tritest = 0, hit = 0, texhit = 0, paths = 0, pixels = 0;
+    uint32_t wave_desc = 0, wave_tri = 0, wave_round = 0, wave_query = 0; // diagnostics, see chiaro_hip.h
 };
 __device__ __forceinline__ uint32_t wave_count(bool pred) { return (uint32_t)__popcll(__ballot(pred)); }
+// True in exactly one active lane (the lowest): `if (wave_leader()) n++` counts
+// iterations of the enclosing (possibly divergent) loop as the WAVE executes them.
+__device__ __forceinline__ bool wave_leader() {
+    return (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
+}
 
 // Call with the whole wave converged.
 __device__ __forceinline__ void flush_counters(unsigned long long *ctrs, const Ctr &c, uint32_t uniform = 0u) {
-    const uint32_t v[9] = {c.closest, c.shadow, c.inner, c.leaf, c.tritest, c.hit, c.texhit, c.paths, c.pixels};
+    const uint32_t v[13] = {c.closest, c.shadow,  c.inner,    c.leaf,     c.tritest,   c.hit,       c.texhit,
+                            c.paths,   c.pixels, c.wave_desc, c.wave_tri, c.wave_round, c.wave_query};
 #pragma unroll
-    for (int i = 0; i < 9; i++) {
+    for (int i = 0; i < 13; i++) {
         unsigned long long s = v[i];
         if (!(uniform & (1u << i))) {
 #pragma unroll
@@ -39,6 +46,12 @@ __device__ __forceinline__ void ray_box(const DevScene &S, f3 o, f3 d, float &fi
 
 // Moller-Trumbore, kdtree.cpp:219-246 / 293-320.  True when the reference would
 // accept the triangle for a segment ending at tmax (0 <= t < tmax); ux, uy, t set then.
+// The early returns are kept: neighbouring lanes often test the same triangle
+// (coherent camera rays), and a wave-uniform rejection skips the rest (measured:
+// a branch-free form was 10% slower on the sponza stand-in).  The division stays
+// hipcc's correctly rounded one: a shortened exact sequence (rcp + Markstein
+// corrections, valid away from the exponent limits) measured slower once its
+// range check is paid for.
 __device__ __forceinline__ bool tri_test(f3 o, f3 d, float4 r0, float4 r1, float4 r2, float tmax, float &ux,
                                          float &uy, float &t) {
     const f3 v0 = ld3(r0), e1 = ld3(r1), e2 = ld3(r2);
@@ -55,6 +68,9 @@ __device__ __forceinline__ bool tri_test(f3 o, f3 d, float4 r0, float4 r1, float
     t = f * dot(e2, q);
     return t >= 0.f && t < tmax;
 }
+
+// tsplit = (split - oa) / da of a kd node (kdtree.cpp:266), correctly rounded.
+__device__ __forceinline__ float split_distance(float split, float oa, float da) { return (split - oa) / da; }
 
 // src/mesh.cpp:21-35 Texture::getColorAt (texture padded with zeros past its end)
 __device__ __forceinline__ f3 tex_lookup(const DevScene &S, int ti, float u, float v) {

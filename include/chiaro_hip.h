@@ -122,6 +122,15 @@ typedef struct {
     uint64_t texhit;      /* textured hits      */
     uint64_t paths;       /* camera paths       */
     uint64_t pixels;      /* pixels written     */
+    /* SIMD-efficiency diagnostics of the persistent kernel (counting launches
+     * only, cr_set_option "counters" 1): WAVE iterations executed by the kd
+     * descent step, the leaf triangle loop, the traversal rounds (one leaf each)
+     * and the per-query outer loop.  Lane efficiency of a phase =
+     * lane work / (64 * wave iterations), e.g. inner / (64 * wave_desc). */
+    uint64_t wave_desc;
+    uint64_t wave_tri;
+    uint64_t wave_round;
+    uint64_t wave_query;
 } cr_counters;
 
 cr_ctx *cr_create(int device);
