@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -30,8 +31,8 @@ struct cr_ctx {
     uint32_t *d_work = nullptr;
     float *d_accum = nullptr;
     size_t accum_elems = 0;
-    void *d_gstack = nullptr, *d_pathbuf = nullptr;
-    size_t gstack_bytes = 0, pathbuf_bytes = 0;
+    void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr;
+    size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0;
     cr_counters last{};
     // options
     int kernel = 0;
@@ -39,6 +40,7 @@ struct cr_ctx {
     int variant = 0;
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
+    uint32_t refill = 32;
 };
 
 namespace {
@@ -92,6 +94,17 @@ int check_params(cr_ctx *c, const cr_render_params *p) {
 
 uint32_t tile_of(const cr_render_params *p) { return p->tile ? p->tile : 32u; }
 
+// Grow-only device work buffer.
+int grow(cr_ctx *c, void **buf, size_t &cap, size_t need) {
+    if (need <= cap && *buf) return CR_OK;
+    if (*buf) hipFree(*buf);
+    *buf = nullptr;
+    cap = 0;
+    if (hipMalloc(buf, need ? need : 16) != hipSuccess) return fail(c, CR_E_OOM, "work buffer");
+    cap = need;
+    return CR_OK;
+}
+
 void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_render_params *p, float *out, int mode) {
     A.S = c->S;
     std::memcpy(A.cam, cam->eye, 3 * sizeof(float));
@@ -119,6 +132,7 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.work = c->d_work;
     A.full_counters = c->full_counters;
     A.variant = c->variant;
+    A.refill = c->refill;
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -128,35 +142,46 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     HIPCHK(hipSetDevice(c->device));
     cr::RenderArgs A{};
     fill_args(c, A, cam, p, out, mode);
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), st));
     if (c->kernel == 0) {
         uint32_t blk, blocks;
         cr::persistent_geometry(c->num_cus, c->waves_per_cu, blk, blocks);
         A.gstride = blk * blocks;
-        const size_t gs = cr::persistent_gstack_bytes(c->stack_depth, A.gstride);
-        const size_t pb = cr::persistent_pathbuf_bytes(p->k, A.gstride);
-        if (gs > c->gstack_bytes) {
-            if (c->d_gstack) hipFree(c->d_gstack);
-            c->d_gstack = nullptr;
-            c->gstack_bytes = 0;
-            if (hipMalloc(&c->d_gstack, gs) != hipSuccess) return fail(c, CR_E_OOM, "stack overflow area");
-            c->gstack_bytes = gs;
-        }
-        if (pb > c->pathbuf_bytes) {
-            if (c->d_pathbuf) hipFree(c->d_pathbuf);
-            c->d_pathbuf = nullptr;
-            c->pathbuf_bytes = 0;
-            if (hipMalloc(&c->d_pathbuf, pb) != hipSuccess) return fail(c, CR_E_OOM, "path buffer");
-            c->pathbuf_bytes = pb;
-        }
+        // samples per chunk: the per-sample buffer stays within SAMPLE_BUF_BYTES
+        // and the work index within 31 bits
+        const uint64_t per_sample = (uint64_t)A.n_items * 12u;
+        uint64_t chunk = std::max<uint64_t>(1, cr::SAMPLE_BUF_BYTES / std::max<uint64_t>(per_sample, 1));
+        chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(1, (1ull << 31) / std::max<uint32_t>(A.n_items, 1)));
+        chunk = std::min<uint64_t>(chunk, p->spp);
+        const bool chunked = chunk < p->spp;
+        if (int r = grow(c, &c->d_gstack, c->gstack_bytes, cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
+            return r;
+        if (int r = grow(c, &c->d_pathbuf, c->pathbuf_bytes, cr::persistent_pathbuf_bytes(p->k, A.gstride))) return r;
+        if (int r = grow(c, &c->d_samples, c->samples_bytes, per_sample * chunk)) return r;
+        if (chunked)
+            if (int r = grow(c, &c->d_run, c->run_bytes, per_sample)) return r;
         A.gstack = (uint2 *)c->d_gstack;
         A.pathbuf = (float4 *)c->d_pathbuf;
+        A.samples = (float *)c->d_samples;
+        A.run = (float *)c->d_run;
+        HIPCHK(hipEventRecord(c->ev0, st));
+        for (uint32_t s0 = 0; s0 < p->spp; s0 += (uint32_t)chunk) {
+            A.s0 = s0;
+            A.s_count = (uint32_t)std::min<uint64_t>(chunk, p->spp - s0);
+            A.n_work = A.n_items * A.s_count;
+            HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
+            int e = cr::launch_persistent(A, c->waves_per_cu, c->num_cus, st);
+            if (!e) e = cr::launch_sum_samples(A, s0 == 0, s0 + A.s_count == p->spp, st);
+            if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
+        }
+        HIPCHK(hipEventRecord(c->ev1, st));
+    } else {
+        HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
+        HIPCHK(hipEventRecord(c->ev0, st));
+        int e = cr::launch_render(A, c->kernel, c->block, c->waves_per_cu, c->num_cus, st);
+        if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
+        HIPCHK(hipEventRecord(c->ev1, st));
     }
-    HIPCHK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), st));
-    HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
-    HIPCHK(hipEventRecord(c->ev0, st));
-    int e = cr::launch_render(A, c->kernel, c->block, c->waves_per_cu, c->num_cus, st);
-    if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
-    HIPCHK(hipEventRecord(c->ev1, st));
     unsigned long long h[16];
     HIPCHK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -206,6 +231,8 @@ void cr_destroy(cr_ctx *c) {
         if (c->d_accum) hipFree(c->d_accum);
         if (c->d_gstack) hipFree(c->d_gstack);
         if (c->d_pathbuf) hipFree(c->d_pathbuf);
+        if (c->d_samples) hipFree(c->d_samples);
+        if (c->d_run) hipFree(c->d_run);
         if (c->d_counters) hipFree(c->d_counters);
         if (c->d_work) hipFree(c->d_work);
         if (c->ev0) hipEventDestroy(c->ev0);
@@ -449,7 +476,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "variant") && v >= 0 && v < cr::num_persistent_variants()) c->variant = (int)v;
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
-    else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
+    else if (!std::strcmp(key, "refill") && v >= 1 && v <= 64) c->refill = (uint32_t)v;    else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
     return CR_OK;
 }
 

@@ -42,6 +42,38 @@ __device__ __forceinline__ float glm_max(float x, float y) { return x > y ? x : 
 __device__ __forceinline__ float comp(f3 a, uint32_t i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 __device__ __forceinline__ f3 ld3(const float4 v) { return mk(v.x, v.y, v.z); }
 
+// ---------------------------------------------------- exact fast division --
+// Both return exactly the correctly rounded IEEE result the reference's float
+// division gives; the short sequences are only taken inside the ranges where
+// they are proven/checked exact, anything else takes the full division.
+//
+// RN(a/b) given y = rcp_for_div(b) (once per ray and axis): Markstein's
+// correction q0 = RN(a*y), r = a - b*q0 (exact by fma), q = RN(q0 + r*y).
+// Exact when y = RN(1/b) and nothing under/overflows, which the ranges
+// 2^-40 <= |b| <= 2^40 and 2^-60 <= |q0| <= 2^60 guarantee (checked:
+// scripts/markstein_check.c, 1.7e10 pairs half of them next to rounding
+// midpoints; tests/test_gpu_numerics.py on the GPU).
+__device__ __forceinline__ float rcp_for_div(float b) {
+    const float ab = fabsf(b);
+    return (ab >= 0x1p-40f && ab <= 0x1p40f) ? 1.f / b : __builtin_nanf(""); // NaN: always the slow path
+}
+__device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
+    const float q0 = a * y;
+    if (fabsf(q0) >= 0x1p-60f && fabsf(q0) <= 0x1p60f) return __builtin_fmaf(__builtin_fmaf(-q0, b, a), y, q0);
+    return a / b;
+}
+// RN(1/a): hardware reciprocal (1 ulp) + one Newton step with fma.  Checked
+// exhaustively over every float with 2^-100 <= |a| <= 2^100 on gfx950
+// (tests/test_gpu_numerics.py).
+__device__ __forceinline__ float rcp_rn(float a) {
+    const float aa = fabsf(a);
+    if (aa >= 0x1p-100f && aa <= 0x1p100f) {
+        const float y0 = __builtin_amdgcn_rcpf(a);
+        return __builtin_fmaf(__builtin_fmaf(-a, y0, 1.f), y0, y0);
+    }
+    return 1.f / a;
+}
+
 // ---------------------------------------------------------------- RNG --
 // Counter-based URBG (DESIGN.md "RNG"); identical to oracle/oracle.c rng_*.
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {

@@ -47,18 +47,29 @@ struct RenderArgs {
     uint32_t gstride;             // threads in the persistent grid
     int full_counters;            // 1: also count inner/leaf/tritest (SURVEY §8d bytes)
     int variant;                  // persistent-kernel variant index (kernels.hip kVariants)
+    uint32_t refill;              // idle lanes of a wave that trigger a path-state step
+    // (pixel, sample) work items of one launch: samples [s0, s0 + s_count) of
+    // every item, w = item * s_count + (s - s0), n_work = n_items * s_count
+    uint32_t s0, s_count, n_work;
+    float *samples;               // [n_items][s_count][3] path radiance per work item
+    float *run;                   // [n_items][3] running per-pixel sum across sample chunks
 };
 int num_persistent_variants();
 
 // Workspace the persistent kernel needs for a grid of `threads` lanes:
 // stack overflow [depth][threads] x 8 B; lane buffer = PARK_SLOTS parked-state
 // float4s + (direct, w) float4 pairs per bounce, each [slot][threads].
-enum { PARK_SLOTS = 5 };
+enum { PARK_SLOTS = 4 };
 inline size_t persistent_gstack_bytes(uint32_t depth, uint32_t threads) { return (size_t)depth * threads * 8; }
 inline size_t persistent_pathbuf_bytes(int K, uint32_t threads) {
     return (size_t)(PARK_SLOTS + 2 * K) * threads * 16;
 }
+// Sample buffer budget: a render is split into sample chunks whose per-sample
+// buffer fits in this many bytes (whole 1080p x 128 spp frames fit in one).
+enum : uint64_t { SAMPLE_BUF_BYTES = 4ull << 30 };
 int launch_persistent(const RenderArgs &A, uint32_t waves_per_cu, int num_cus, hipStream_t st);
+// Per-pixel in-order sum of one chunk's samples; `last` blends / writes the pixel.
+int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t st);
 // Persistent grid geometry chosen by launch_render (block threads, blocks).
 void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);
 

@@ -1,270 +1,261 @@
-// persistent.hip -- the production render kernel: persistent waves with per-lane
-// path regeneration (cr_set_option "kernel" 0, the default).
+// persistent.hip -- the production render kernel (cr_set_option "kernel" 0, the
+// default): persistent waves, one PATH per lane at a time, resumable kd
+// traversal with dynamic path fetch.
 //
-// Every lane owns one pixel at a time and runs its samples one after another (so
-// the per-pixel sum keeps the reference's sample order, src/rayTracer.cpp:59-62),
-// but a lane never waits for the rest of its wave between queries: each outer
-// iteration every live lane runs exactly ONE kd query -- a camera/bounce ray
-// (closest hit) or a NEE shadow ray (any hit) -- through one shared traversal
-// loop, then advances its own path state machine (shade and start the shadow ray
-// / bounce / finish the sample / take the next pixel).  Pixels are handed out
-// wave-wide: one atomicAdd per refill, lanes ranked by __ballot + mbcnt.
+// Work items are (pixel, sample) pairs in pixel-major order, so the 64 lanes of
+// a wave trace samples of the same few pixels: the camera rays (about 80% of
+// the closest-hit queries on the sponza stand-in) and their NEE rays are close
+// to coherent, which is what the SIMD lanes need.  Each lane writes its path's
+// radiance to a per-sample buffer; a second kernel sums every pixel's samples
+// in sample order (the reference's order, src/rayTracer.cpp:59-62) and blends
+// the layer, so the result is bit-identical to the sequential loop whatever
+// order the paths were traced in.
+//
+// Traversal: one ROUND (descend to a leaf, test it, pop) per outer iteration.
+// A lane whose query ended waits in a result state until `A.refill` lanes of
+// its wave are waiting (or none is traversing); those lanes then run the path
+// state machine (RayTracer::sendRay) up to their next query while the rest of
+// the wave keeps its traversal state in registers.
 //
 // Register budget (the kernel is latency bound: occupancy is the lever, see
 // DESIGN.md "Kernel"):
 //   * traversal stack entries are 8 B {far node, tmax}; the far child's tmin is
 //     the CURRENT tmax at pop time (stack invariant), the top R
 //     entries live in an LDS ring [slot][thread], deeper ones spill to HBM;
-//   * path state not needed by the traversal (running pixel sum, hit shading,
-//     NEE term, RNG, counters of the sample) is parked in a per-lane HBM record
-//     across each query instead of occupying VGPRs;
+//   * path state not needed by the traversal (hit shading, NEE term, RNG,
+//     bounce count, work item) is parked in a per-lane HBM record across the
+//     traversal rounds instead of occupying VGPRs;
 //   * per-bounce (direct, w) pairs for the back-to-front fold go to HBM too.
 #include "render_common.hpp"
 
 namespace cr {
 
-enum : uint32_t { ST_NEED_PIXEL = 0, ST_NEW_SAMPLE = 1, ST_CLOSEST = 2, ST_SHADOW = 3, ST_DONE = 4 };
+enum : uint32_t {
+    ST_NEED_WORK = 0, // take the next (pixel, sample) item
+    ST_CLOSEST = 2,   // closest-hit query in flight
+    ST_SHADOW = 3,    // NEE shadow query in flight
+    ST_DONE = 4,      // no work left
+    ST_HIT = 5,       // query results waiting for the path state machine
+    ST_MISS = 6,
+    ST_OCCLUDED = 7,
+    ST_VISIBLE = 8,
+};
+enum : int { T_CLOSEST = 0, T_SHADOW = 1, T_HIT = 5, T_TEXHIT = 6, T_PATHS = 7, T_PIXELS = 8, T_N = 9 };
 
-template <int R, bool FULL, bool PF>
-__device__ __forceinline__ bool traverse_ring(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
-                                              uint32_t gid, f3 o, f3 d, bool shadow, float limit, uint32_t exclude,
-                                              uint32_t &tri, float &bx, float &by, Ctr &c) {
-    float tmin, tmax;
-    ray_box(S, o, d, tmin, tmax);
-    if (shadow) {
-        if (tmax < 0 || tmax < tmin || tmin > limit) return false;
-        tmax = std_min(tmax, limit);
-    } else {
-        if (tmax < 0 || tmax < tmin) return false;
-    }
-    const uint32_t bdim = blockDim.x, tid = threadIdx.x;
-    uint32_t sp = 0, nl = 0, node = 0;
-    for (;;) {
-        uint2 nd = S.nodes[node];
-        while ((nd.y & 3u) != 3u) {
-            if (FULL) {
-                c.inner++;
-                if (wave_leader()) c.wave_desc++;
-            }
-            const uint32_t a = nd.y & 3u;
-            const float split = __uint_as_float(nd.x);
-            const float oa = comp(o, a), da = comp(d, a);
-            const float tsplit = split_distance(split, oa, da);
-            const uint32_t below = (oa < split) || (oa == split && da <= 0);
-            const uint32_t child = nd.y >> 2;
-            if (tsplit >= tmax || tsplit < 0) {
-                node = child + (1u - below);
-            } else if (tsplit <= tmin) {
-                node = child + below;
-            } else {
-                const uint2 e = make_uint2(child + below, __float_as_uint(tmax));
-                const uint32_t slot = (sp & (R - 1)) * bdim + tid;
-                if (nl == R) gstk[(size_t)(sp - R) * gstride + gid] = ring[slot]; // spill the oldest
-                else nl++;
-                ring[slot] = e;
-                sp++;
-                node = child + (1u - below);
-                tmax = tsplit;
-            }
-            nd = S.nodes[node];
-        }
-        if (FULL) {
-            c.leaf++;
-            if (wave_leader()) c.wave_round++;
-        }
-        const uint32_t first = nd.x, count = nd.y >> 2;
-        bool found = false;
-        float4 n0, n1, n2;
-        if (PF && count) {
-            n0 = S.recs[3 * first];
-            n1 = S.recs[3 * first + 1];
-            n2 = S.recs[3 * first + 2];
-        }
-        for (uint32_t j = 0; j < count; j++) {
-            if (FULL && wave_leader()) c.wave_tri++;
-            float4 r0, r1, r2;
-            if (PF) { // software pipeline: issue triangle j+1's loads before testing j
-                r0 = n0;
-                r1 = n1;
-                r2 = n2;
-                if (j + 1 < count) {
-                    n0 = S.recs[3 * (first + j + 1)];
-                    n1 = S.recs[3 * (first + j + 1) + 1];
-                    n2 = S.recs[3 * (first + j + 1) + 2];
-                }
-            } else {
-                r0 = S.recs[3 * (first + j)];
-                r1 = S.recs[3 * (first + j) + 1];
-                r2 = S.recs[3 * (first + j) + 2];
-            }
-            const uint32_t id = __float_as_uint(r0.w);
-            if (shadow && id == exclude) continue;
-            if (FULL) c.tritest++;
-            float ux, uy, t;
-            if (tri_test(o, d, r0, r1, r2, tmax, ux, uy, t)) {
-                if (shadow) return true;
-                bx = ux;
-                by = uy;
-                tmax = t;
-                tri = id;
-                found = true;
-            }
-        }
-        if (found) return true;
-        if (sp == 0) return false;
-        sp--;
-        uint2 e;
-        if (nl) {
-            e = ring[(sp & (R - 1)) * bdim + tid];
-            nl--;
-        } else {
-            e = gstk[(size_t)sp * gstride + gid];
-        }
-        node = e.x;
-        tmin = tmax; // == the popped entry's split distance (stack invariant)
-        tmax = __uint_as_float(e.y);
-    }
+// Per-query tallies are wave-aggregated LDS atomics: the state machine runs in
+// divergent code, so a wave total cannot be kept wave-uniform in registers.
+__device__ __forceinline__ void tally(unsigned long long *tl, int i, bool pred) {
+    const uint64_t b = __ballot(pred);
+    if (b && wave_leader()) atomicAdd(&tl[i], (unsigned long long)__popcll(b));
 }
 
 // Parked lane state, float4 slots [slot][gstride]:
-//   0 temp.xyz | s        1 direct.xyz | k       2 fcol.xyz | item
-//   3 normal.xyz | rng.key  4 contrib.xyz | rng.ctr
+//   0 direct.xyz | k     1 fcol.xyz | work item
+//   2 normal.xyz | rng.key   3 contrib.xyz | rng.ctr
 struct Lane {
-    f3 temp, direct, fcol, normal, contrib;
-    uint32_t s, k, item;
+    f3 direct, fcol, normal, contrib;
+    uint32_t k, w;
     Rng rng;
 };
 __device__ __forceinline__ float4 pk(f3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 __device__ __forceinline__ void park(float4 *buf, uint32_t gstride, uint32_t gid, const Lane &L) {
-    buf[gid] = pk(L.temp, L.s);
-    buf[(size_t)gstride + gid] = pk(L.direct, L.k);
-    buf[(size_t)2 * gstride + gid] = pk(L.fcol, L.item);
-    buf[(size_t)3 * gstride + gid] = pk(L.normal, L.rng.key);
-    buf[(size_t)4 * gstride + gid] = pk(L.contrib, L.rng.ctr);
+    buf[gid] = pk(L.direct, L.k);
+    buf[(size_t)gstride + gid] = pk(L.fcol, L.w);
+    buf[(size_t)2 * gstride + gid] = pk(L.normal, L.rng.key);
+    buf[(size_t)3 * gstride + gid] = pk(L.contrib, L.rng.ctr);
 }
 __device__ __forceinline__ void unpark(const float4 *buf, uint32_t gstride, uint32_t gid, Lane &L) {
     const float4 a = buf[gid], b = buf[(size_t)gstride + gid], c = buf[(size_t)2 * gstride + gid],
-                 d = buf[(size_t)3 * gstride + gid], e = buf[(size_t)4 * gstride + gid];
-    L.temp = ld3(a);
-    L.s = __float_as_uint(a.w);
-    L.direct = ld3(b);
-    L.k = __float_as_uint(b.w);
-    L.fcol = ld3(c);
-    L.item = __float_as_uint(c.w);
-    L.normal = ld3(d);
-    L.rng.key = __float_as_uint(d.w);
-    L.contrib = ld3(e);
-    L.rng.ctr = __float_as_uint(e.w);
+                 d = buf[(size_t)3 * gstride + gid];
+    L.direct = ld3(a);
+    L.k = __float_as_uint(a.w);
+    L.fcol = ld3(b);
+    L.w = __float_as_uint(b.w);
+    L.normal = ld3(c);
+    L.rng.key = __float_as_uint(c.w);
+    L.contrib = ld3(d);
+    L.rng.ctr = __float_as_uint(d.w);
 }
 
-// Pixel refill (wave-wide, converged) + camera ray of a new sample.
-__device__ __forceinline__ void regenerate(const RenderArgs &A, Lane &L, uint32_t &state, f3 &o, f3 &d, Ctr &c) {
-    const uint32_t lane = threadIdx.x & 63u;
-    for (;;) {
-        const uint64_t need = __ballot(state == ST_NEED_PIXEL);
-        if (!need) break;
-        const uint32_t n = (uint32_t)__popcll(need);
-        const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1u;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(A.work, n);
-        base = __shfl(base, (int)leader, 64);
-        if (state == ST_NEED_PIXEL) {
-            const uint32_t rank =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            const uint32_t item = base + rank;
-            uint32_t px, py;
-            if (item >= A.n_items) {
-                state = ST_DONE;
-            } else if (item_pixel(A, item, px, py)) {
-                state = ST_NEW_SAMPLE;
-                L.item = item;
-                L.s = 0;
-                L.temp = mk(0.f, 0.f, 0.f);
-            } // else: a partial-tile pixel outside the image: fetch again
+// Traversal registers of a query in flight.  r = per-axis rcp_for_div(d) for
+// the exact short split-distance division (FD builds, device_math.hpp).
+struct Trav {
+    uint32_t node, sp, nl;
+    float tmin, tmax;
+    f3 r;
+};
+
+// Root-box clip (kdtree.cpp:196-208, 276-283); false: the query ends without a hit.
+__device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool shadow, float limit, Trav &T) {
+    const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    ray_box_inv(S, o, inv, T.tmin, T.tmax);
+    if (T.tmax < 0 || T.tmax < T.tmin) return false;
+    if (shadow) {
+        if (T.tmin > limit) return false;
+        T.tmax = std_min(T.tmax, limit);
+    }
+    const float nan = __builtin_nanf("");
+    T.r = mk(fabsf(d.x) >= 0x1p-40f && fabsf(d.x) <= 0x1p40f ? inv.x : nan,
+             fabsf(d.y) >= 0x1p-40f && fabsf(d.y) <= 0x1p40f ? inv.y : nan,
+             fabsf(d.z) >= 0x1p-40f && fabsf(d.z) <= 0x1p40f ? inv.z : nan);
+    T.node = T.sp = T.nl = 0;
+    return true;
+}
+
+// One traversal round (kdtree.cpp:250-330 as an explicit stack): descend to the
+// next leaf, test it, pop.  Returns the lane's new state: unchanged while the
+// query continues, else its result (a closest hit leaves {bx, by, tri} in d:
+// the direction is dead by then).
+// (Speculative descent -- lanes that reached their leaf early descending toward
+// the next one, Aila & Laine's postponed leaves -- is exact here too but
+// measured slower: the merged descent loop costs more than the idle lanes.)
+template <int R, bool FULL, bool PF, bool FD>
+__device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
+                                               uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
+                                               Ctr &c) {
+    const uint32_t bdim = blockDim.x, tid = threadIdx.x;
+    uint2 nd = S.nodes[T.node];
+    while ((nd.y & 3u) != 3u) {
+        if (FULL) {
+            c.inner++;
+            if (wave_leader()) c.wave_desc++;
+        }
+        const uint32_t a = nd.y & 3u;
+        const float split = __uint_as_float(nd.x);
+        const float oa = comp(o, a), da = comp(d, a);
+        const float tsplit = FD ? div_by_rcp(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
+        const uint32_t below = (oa < split) || (oa == split && da <= 0);
+        const uint32_t child = nd.y >> 2;
+        if (tsplit >= T.tmax || tsplit < 0) {
+            T.node = child + (1u - below);
+        } else if (tsplit <= T.tmin) {
+            T.node = child + below;
+        } else {
+            const uint2 e = make_uint2(child + below, __float_as_uint(T.tmax));
+            const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
+            if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
+            else T.nl++;
+            ring[slot] = e;
+            T.sp++;
+            T.node = child + (1u - below);
+            T.tmax = tsplit;
+        }
+        nd = S.nodes[T.node];
+    }
+    if (FULL) {
+        c.leaf++;
+        if (wave_leader()) c.wave_round++;
+    }
+    const uint32_t first = nd.x, count = nd.y >> 2;
+    bool found = false, occluded = false;
+    uint32_t tri = 0;
+    float bx = 0.f, by = 0.f;
+    float4 n0, n1, n2;
+    if (PF && count) {
+        n0 = S.recs[3 * first];
+        n1 = S.recs[3 * first + 1];
+        n2 = S.recs[3 * first + 2];
+    }
+    for (uint32_t j = 0; j < count; j++) {
+        if (FULL && wave_leader()) c.wave_tri++;
+        float4 r0, r1, r2;
+        if (PF) { // software pipeline: issue triangle j+1's loads before testing j
+            r0 = n0;
+            r1 = n1;
+            r2 = n2;
+            if (j + 1 < count) {
+                n0 = S.recs[3 * (first + j + 1)];
+                n1 = S.recs[3 * (first + j + 1) + 1];
+                n2 = S.recs[3 * (first + j + 1) + 2];
+            }
+        } else {
+            r0 = S.recs[3 * (first + j)];
+            r1 = S.recs[3 * (first + j) + 1];
+            r2 = S.recs[3 * (first + j) + 2];
+        }
+        const uint32_t id = __float_as_uint(r0.w);
+        if (shadow && id == exclude) continue;
+        if (FULL) c.tritest++;
+        float ux, uy, t;
+        if (tri_test(o, d, r0, r1, r2, T.tmax, ux, uy, t)) {
+            if (shadow) {
+                occluded = true;
+                break;
+            }
+            bx = ux;
+            by = uy;
+            T.tmax = t;
+            tri = id;
+            found = true;
         }
     }
-    c.paths += wave_count(state == ST_NEW_SAMPLE);
-    if (state == ST_NEW_SAMPLE) {
-        uint32_t px, py;
-        item_pixel(A, L.item, px, py);
-        L.rng = rng_make(A.seed, A.layer, py * A.xres + px, L.s);
-        o = mk(A.cam[0], A.cam[1], A.cam[2]);
-        d = camera_dir(A, px, py, L.rng);
-        L.k = 1;
-        state = ST_CLOSEST;
+    if (occluded) return ST_OCCLUDED;
+    if (found) {
+        d = mk(bx, by, __uint_as_float(tri));
+        return ST_HIT;
     }
+    if (T.sp == 0) return shadow ? ST_VISIBLE : ST_MISS;
+    T.sp--;
+    uint2 e;
+    if (T.nl) {
+        e = ring[(T.sp & (R - 1)) * bdim + tid];
+        T.nl--;
+    } else {
+        e = gstk[(size_t)T.sp * gstride + gid];
+    }
+    T.node = e.x;
+    T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
+    T.tmax = __uint_as_float(e.y);
+    return shadow ? ST_SHADOW : ST_CLOSEST;
 }
 
-template <int R, bool FULL, bool PF, int MINW>
-__global__ void __launch_bounds__(256, MINW) render_persistent(RenderArgs A) {
-    extern __shared__ uint2 ring_lds[];
+// Work item w of this launch -> (rank-local pixel item, sample index).
+__device__ __forceinline__ void work_item(const RenderArgs &A, uint32_t w, uint32_t &item, uint32_t &s) {
+    item = w / A.s_count;
+    s = A.s0 + (w - item * A.s_count);
+}
+
+// Path state machine of one lane (RayTracer::sendRay, rayTracer.cpp:76-135):
+// consume the finished query's result, then shade / start the shadow ray /
+// bounce / finish the path / take the next item, until the lane has a new
+// query in flight (ST_CLOSEST / ST_SHADOW, traversal set up) or is ST_DONE.
+__device__ __forceinline__ void path_advance(const RenderArgs &A, Lane &L, uint32_t &state, f3 &o, f3 &d,
+                                             float &limit, uint32_t &exclude, Trav &T, float4 *dw, uint32_t gstride,
+                                             uint32_t gid, unsigned long long *tl) {
     const DevScene &S = A.S;
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t gstride = A.gstride;
-    float4 *lbuf = A.pathbuf;
-    float4 *dw = A.pathbuf + (size_t)PARK_SLOTS * gstride;
-    Ctr c = {};
-
-    uint32_t state = ST_NEED_PIXEL;
-    f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
-    float limit = 0.f;
-    uint32_t exclude = 0xffffffffu;
-    {
-        Lane L;
-        L.temp = L.direct = L.fcol = L.normal = L.contrib = mk(0.f, 0.f, 0.f);
-        L.s = L.k = L.item = 0;
-        L.rng = Rng{0u, 0u};
-        regenerate(A, L, state, o, d, c);
-        park(lbuf, gstride, gid, L);
-    }
-
-    for (;;) {
-        if (!__any(state != ST_DONE)) break;
-        if (FULL && wave_leader()) c.wave_query++;
-        // ---- one kd query per live lane
-        const bool shadow = state == ST_SHADOW;
-        c.shadow += wave_count(shadow);
-        c.closest += wave_count(state == ST_CLOSEST);
-        uint32_t t = 0;
-        float bx = 0.f, by = 0.f;
-        bool h = false;
-        if (state == ST_CLOSEST || state == ST_SHADOW)
-            h = traverse_ring<R, FULL, PF>(S, ring_lds, A.gstack, gstride, gid, o, d, shadow, limit, exclude, t, bx,
-                                           by, c);
-        c.hit += wave_count(state == ST_CLOSEST && h);
-
-        // ---- advance the path state machine (RayTracer::sendRay, rayTracer.cpp:76-135)
-        Lane L;
-        unpark(lbuf, gstride, gid, L);
-        bool bounce = false, finish = false, textured = false, pixel_done = false;
+    const uint32_t lane = threadIdx.x & 63u;
+    do {
+        bool bounce = false, finish = false, textured = false;
         f3 tail = mk(0.f, 0.f, 0.f);
-        if (state == ST_SHADOW) {
-            if (!h) L.direct = add(L.direct, L.contrib);
+        tally(tl, T_HIT, state == ST_HIT);
+        if (state == ST_VISIBLE) {
+            L.direct = add(L.direct, L.contrib);
             bounce = true;
-        } else if (state == ST_CLOSEST) {
-            if (!h) {
-                tail = mk(A.bg[0], A.bg[1], A.bg[2]);
-                finish = true;
+        } else if (state == ST_OCCLUDED) {
+            bounce = true;
+        } else if (state == ST_MISS) {
+            tail = mk(A.bg[0], A.bg[1], A.bg[2]);
+            finish = true;
+        } else if (state == ST_HIT) {
+            const HitShade hs = shade_hit(S, o, __float_as_uint(d.z), d.x, d.y, (int)L.k);
+            textured = hs.textured;
+            L.normal = hs.normal;
+            L.fcol = hs.fcol;
+            L.direct = hs.direct;
+            if (S.nlights) {
+                const Nee n = sample_light(S, hs.p, hs.normal, hs.fcol, L.rng);
+                L.contrib = n.contrib;
+                o = n.origin; // == p + 0.001 n, also the origin of the next bounce
+                d = n.dir;
+                limit = n.distance;
+                exclude = n.light;
+                state = ST_SHADOW;
             } else {
-                const HitShade hs = shade_hit(S, o, t, bx, by, (int)L.k);
-                textured = hs.textured;
-                L.normal = hs.normal;
-                L.fcol = hs.fcol;
-                L.direct = hs.direct;
-                if (S.nlights) {
-                    const Nee n = sample_light(S, hs.p, hs.normal, hs.fcol, L.rng);
-                    L.contrib = n.contrib;
-                    o = n.origin; // == p + 0.001 n, also the origin of the next bounce
-                    d = n.dir;
-                    limit = n.distance;
-                    exclude = n.light;
-                    state = ST_SHADOW;
-                } else {
-                    o = add(hs.p, muls(hs.normal, 0.001f));
-                    bounce = true;
-                }
+                o = add(hs.p, muls(hs.normal, 0.001f));
+                bounce = true;
             }
         }
+        tally(tl, T_TEXHIT, textured);
         if (bounce) {
             if ((int)L.k == A.K) {
                 tail = L.direct;
@@ -297,40 +288,149 @@ __global__ void __launch_bounds__(256, MINW) render_persistent(RenderArgs A) {
                 const float4 Wj = dw[(size_t)(2 * j + 1) * gstride + gid];
                 acc = add(ld3(Dj), mul(ld3(Wj), acc));
             }
-            L.temp = add(L.temp, acc);
-            L.s++;
-            if (L.s == A.spp) {
-                uint32_t px, py;
-                item_pixel(A, L.item, px, py);
-                write_pixel(A, px, py, L.item, L.temp);
-                pixel_done = true;
-                state = ST_NEED_PIXEL;
-            } else {
-                state = ST_NEW_SAMPLE;
+            float *out = A.samples + 3 * (size_t)L.w; // [item][sample] == work-item order
+            out[0] = acc.x;
+            out[1] = acc.y;
+            out[2] = acc.z;
+            state = ST_NEED_WORK;
+        }
+        // item fetch: one atomicAdd per group of lanes that need work, lanes
+        // ranked by __ballot + mbcnt (consecutive lanes get consecutive samples)
+        bool fresh = false;
+        for (;;) {
+            const uint64_t need = __ballot(state == ST_NEED_WORK);
+            if (!need) break;
+            const uint32_t n = (uint32_t)__popcll(need);
+            const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(A.work, n);
+            base = __shfl(base, (int)leader, 64);
+            if (state == ST_NEED_WORK) {
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint32_t w = base + rank;
+                uint32_t item, s, px, py;
+                work_item(A, w, item, s);
+                if (w >= A.n_work) {
+                    state = ST_DONE;
+                } else if (item_pixel(A, item, px, py)) {
+                    // new path: camera ray (rayTracer.cpp:61)
+                    L.w = w;
+                    L.rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
+                    o = mk(A.cam[0], A.cam[1], A.cam[2]);
+                    d = camera_dir(A, px, py, L.rng);
+                    L.k = 1;
+                    state = ST_CLOSEST;
+                    fresh = true;
+                } // else: a partial-tile pixel outside the image: fetch again
             }
         }
-        c.texhit += wave_count(textured);
-        c.pixels += wave_count(pixel_done);
-        regenerate(A, L, state, o, d, c);
+        tally(tl, T_PATHS, fresh);
+        // issue the query
+        tally(tl, T_CLOSEST, state == ST_CLOSEST);
+        tally(tl, T_SHADOW, state == ST_SHADOW);
+        if (state == ST_CLOSEST || state == ST_SHADOW) {
+            const bool shadow = state == ST_SHADOW;
+            if (!trav_begin(S, o, d, shadow, limit, T)) state = shadow ? ST_VISIBLE : ST_MISS;
+        }
+    } while (state != ST_CLOSEST && state != ST_SHADOW && state != ST_DONE);
+}
+
+template <int R, bool FULL, bool PF, int MINW, bool FD>
+__global__ void __launch_bounds__(256, MINW) render_dynamic(RenderArgs A) {
+    extern __shared__ uint2 ring_lds[];
+    __shared__ unsigned long long tl[T_N];
+    if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
+    __syncthreads();
+    const DevScene &S = A.S;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t gstride = A.gstride;
+    float4 *lbuf = A.pathbuf;
+    float4 *dw = A.pathbuf + (size_t)PARK_SLOTS * gstride;
+    Ctr c = {};
+
+    uint32_t state = ST_NEED_WORK;
+    f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
+    float limit = 0.f;
+    uint32_t exclude = 0xffffffffu;
+    Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
+    {
+        Lane L;
+        L.direct = L.fcol = L.normal = L.contrib = mk(0.f, 0.f, 0.f);
+        L.k = L.w = 0;
+        L.rng = Rng{0u, 0u};
         park(lbuf, gstride, gid, L);
     }
-    // closest, shadow, hit, texhit, paths, pixels are wave tallies
-    flush_counters(A.counters, c, (1u << 0) | (1u << 1) | (1u << 5) | (1u << 6) | (1u << 7) | (1u << 8));
+    for (;;) {
+        const bool busy = state == ST_CLOSEST || state == ST_SHADOW;
+        const bool idle = !busy && state != ST_DONE;
+        const uint64_t idle_m = __ballot(idle), busy_m = __ballot(busy);
+        if (idle_m && (busy_m == 0 || (uint32_t)__popcll(idle_m) >= A.refill)) {
+            if (FULL && wave_leader()) c.wave_query++;
+            if (idle) {
+                Lane L;
+                unpark(lbuf, gstride, gid, L);
+                path_advance(A, L, state, o, d, limit, exclude, T, dw, gstride, gid, tl);
+                park(lbuf, gstride, gid, L);
+            }
+        }
+        const bool go = state == ST_CLOSEST || state == ST_SHADOW;
+        if (!__any(go)) {
+            if (!__any(state != ST_DONE)) break;
+            continue;
+        }
+        if (go)
+            state = trav_round<R, FULL, PF, FD>(S, ring_lds, A.gstack, gstride, gid, o, d, state == ST_SHADOW,
+                                                exclude, T, c);
+    }
+    flush_counters(A.counters, c, 0u);
+    __syncthreads();
+    if (threadIdx.x < T_N && tl[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], tl[threadIdx.x]);
+}
+
+// Per pixel: add this launch's samples in sample order onto the running sum
+// (A.run, carried across sample chunks), then on the last chunk blend the
+// layer into the frame / write the tile mean (write_pixel).
+__global__ void __launch_bounds__(256) sum_samples(RenderArgs A, int first, int last) {
+    const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t px = 0, py = 0;
+    const bool valid = item < A.n_items && item_pixel(A, item, px, py);
+    if (valid) {
+        f3 temp = mk(0.f, 0.f, 0.f);
+        if (!first) temp = mk(A.run[3 * (size_t)item], A.run[3 * (size_t)item + 1], A.run[3 * (size_t)item + 2]);
+        const float *sm = A.samples + 3 * (size_t)item * A.s_count;
+        for (uint32_t s = 0; s < A.s_count; s++) temp = add(temp, mk(sm[3 * s], sm[3 * s + 1], sm[3 * s + 2]));
+        if (last) {
+            write_pixel(A, px, py, item, temp);
+        } else {
+            A.run[3 * (size_t)item] = temp.x;
+            A.run[3 * (size_t)item + 1] = temp.y;
+            A.run[3 * (size_t)item + 2] = temp.z;
+        }
+    }
+    const uint64_t b = __ballot(valid && last);
+    if (b && (threadIdx.x & 63u) == 0) atomicAdd(&A.counters[T_PIXELS], (unsigned long long)__popcll(b));
 }
 
 // Variants (cr_set_option "variant"): LDS ring depth R, software-pipelined leaf
-// loads PF, minimum waves per SIMD MINW (caps VGPRs).  The counting build (full
-// counters) is one fixed variant: the counts do not depend on the variant.
+// loads PF, minimum waves per SIMD MINW (caps VGPRs), short exact split
+// division FD.  The counting build (full counters) is one fixed variant per
+// FD: the counts do not depend on the variant.
 struct Variant {
     void (*fn)(RenderArgs);
+    void (*counting)(RenderArgs);
     int ring;
 };
-#define CR_VARIANT(R, PF, W) {render_persistent<R, false, PF, W>, R}
-// Measured on MI355X, sponza stand-in 1080p x 8 spp (profiles/r01_sweep_*.txt):
-// (8, PF, 8 waves) 275 Mray/s > (4, PF, 8) 274 > (8, -, 8) 258 > (8, PF, 6) 246 > (8, PF, 4) 196.
+#define CR_DYNAMIC(R, PF, W, FD) {render_dynamic<R, false, PF, W, FD>, render_dynamic<8, true, true, 1, FD>, R}
+// History on MI355X, sponza stand-in 1080p x 8 spp (profiles/r01_sweep_*.txt):
+//   per-query loop, wave waits for its longest query (8, PF, 8 waves)   287 Mray/s
+//   dynamic fetch, one pixel (all its samples) per lane (8, PF, 6)     382
+//     + speculative descent 360; + query registers spilled around the state
+//     machine 376; + per-XCD pixel bands 340 (the shared front keeps the
+//     Infinity-Cache working set small): none kept
 static const Variant kVariants[] = {
-    CR_VARIANT(8, true, 8), CR_VARIANT(4, true, 8), CR_VARIANT(8, false, 8), CR_VARIANT(8, true, 6),
-    CR_VARIANT(8, true, 1),
+    CR_DYNAMIC(8, true, 6, false), CR_DYNAMIC(8, true, 6, true), CR_DYNAMIC(8, true, 8, false),
+    CR_DYNAMIC(4, true, 6, false), CR_DYNAMIC(8, false, 6, false), CR_DYNAMIC(8, true, 5, false),
 };
 static const int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 int num_persistent_variants() { return kNumVariants; }
@@ -344,15 +444,21 @@ void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, ui
 int launch_persistent(const RenderArgs &A, uint32_t waves_per_cu, int num_cus, hipStream_t st) {
     uint32_t blk, blocks;
     persistent_geometry(num_cus, waves_per_cu, blk, blocks);
-    if (A.gstride < blk * blocks) return (int)hipErrorInvalidValue;
+    if (A.gstride < blk * blocks || !A.samples || A.s_count == 0) return (int)hipErrorInvalidValue;
+    const Variant &v = kVariants[(A.variant >= 0 && A.variant < kNumVariants) ? A.variant : 0];
     if (A.full_counters) {
         const size_t lds = (size_t)8 * blk * sizeof(uint2);
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(render_persistent<8, true, true, 1>), dim3(blocks), dim3(blk), lds, st, A);
+        hipLaunchKernelGGL(v.counting, dim3(blocks), dim3(blk), lds, st, A);
     } else {
-        const Variant &v = kVariants[(A.variant >= 0 && A.variant < kNumVariants) ? A.variant : 0];
         const size_t lds = (size_t)v.ring * blk * sizeof(uint2);
         hipLaunchKernelGGL(v.fn, dim3(blocks), dim3(blk), lds, st, A);
     }
+    return (int)hipGetLastError();
+}
+
+int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t st) {
+    const uint32_t blocks = (A.n_items + 255) / 256;
+    if (blocks) hipLaunchKernelGGL(sum_samples, dim3(blocks), dim3(256), 0, st, A, first ? 1 : 0, last ? 1 : 0);
     return (int)hipGetLastError();
 }
 

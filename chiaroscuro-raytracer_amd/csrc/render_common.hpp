@@ -35,6 +35,15 @@ __device__ __forceinline__ void flush_counters(unsigned long long *ctrs, const C
 }
 
 // kdtree.cpp:196-208 slab test against the padded root box
+// inv = the correctly rounded 1/d per axis (what the reference's 1.f/d gives).
+__device__ __forceinline__ void ray_box_inv(const DevScene &S, f3 o, f3 inv, float &first, float &second) {
+    const float dix = inv.x, diy = inv.y, diz = inv.z;
+    const float txmin = (S.bmin.x - o.x) * dix, txmax = (S.bmax.x - o.x) * dix;
+    const float tymin = (S.bmin.y - o.y) * diy, tymax = (S.bmax.y - o.y) * diy;
+    const float tzmin = (S.bmin.z - o.z) * diz, tzmax = (S.bmax.z - o.z) * diz;
+    first = std_max(std_max(std_min(txmin, txmax), std_min(tymin, tymax)), std_min(tzmin, tzmax));
+    second = std_min(std_min(std_max(txmin, txmax), std_max(tymin, tymax)), std_max(tzmin, tzmax));
+}
 __device__ __forceinline__ void ray_box(const DevScene &S, f3 o, f3 d, float &first, float &second) {
     const float diy = 1.f / d.y, dix = 1.f / d.x, diz = 1.f / d.z;
     const float txmin = (S.bmin.x - o.x) * dix, txmax = (S.bmax.x - o.x) * dix;
@@ -48,17 +57,15 @@ __device__ __forceinline__ void ray_box(const DevScene &S, f3 o, f3 d, float &fi
 // accept the triangle for a segment ending at tmax (0 <= t < tmax); ux, uy, t set then.
 // The early returns are kept: neighbouring lanes often test the same triangle
 // (coherent camera rays), and a wave-uniform rejection skips the rest (measured:
-// a branch-free form was 10% slower on the sponza stand-in).  The division stays
-// hipcc's correctly rounded one: a shortened exact sequence (rcp + Markstein
-// corrections, valid away from the exponent limits) measured slower once its
-// range check is paid for.
+// a branch-free form was 10% slower on the sponza stand-in).  f = RN(1/aa) as
+// the reference's 1.f/a, by rcp_rn (exact, checked over every float in range).
 __device__ __forceinline__ bool tri_test(f3 o, f3 d, float4 r0, float4 r1, float4 r2, float tmax, float &ux,
                                          float &uy, float &t) {
     const f3 v0 = ld3(r0), e1 = ld3(r1), e2 = ld3(r2);
     const f3 p = cross(d, e2);
     const float aa = dot(e1, p);
     if (aa < 1.19209290e-7F && aa > -1.19209290e-7F) return false;
-    const float f = 1.f / aa;
+    const float f = rcp_rn(aa);
     const f3 sv = sub(o, v0);
     ux = f * dot(sv, p);
     if (ux < 0.f || ux > 1.f) return false;

@@ -169,7 +169,11 @@ int cr_get_counters(cr_ctx *ctx, cr_counters *out);
 /* Device time (ms) of the last render kernel, HIP events on its own stream. */
 float cr_last_kernel_ms(cr_ctx *ctx);
 /* Kernel variant / tuning knobs: "kernel" (0 = persistent wave-regeneration,
- * 1 = one-thread-per-pixel), "block", "waves_per_cu". Returns CR_OK or CR_E_INVALID. */
+ * 1 = one-thread-per-pixel), "variant" (persistent-kernel build, 0 = default),
+ * "refill" (1..64: idle lanes of a wave that trigger a path-state step in the
+ * dynamic-fetch variants), "counters" (1 = also count inner/leaf/tritest and
+ * the wave_* diagnostics; 0 = only the per-query tallies, for timed launches),
+ * "block", "waves_per_cu".  Returns CR_OK or CR_E_INVALID. */
 int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
 int cr_synchronize(cr_ctx *ctx);
 

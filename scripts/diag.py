@@ -16,6 +16,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="sponza")
     ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--refill", type=int, default=16)
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -30,6 +32,8 @@ def main():
     cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], i["xres"], i["yres"])
     frame = torch.zeros((i["yres"], i["xres"], 3), dtype=torch.float32, device="cuda")
     dev.set_option("counters", 1)
+    dev.set_option("variant", args.variant)
+    dev.set_option("refill", args.refill)
     p = ca.render_params(i["xres"], i["yres"], args.spp, i["k"], i["seed"])
     dev.render_device(cam, p, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="")
     ap.add_argument("--waves", default="0", help="comma list of waves_per_cu values (0 = default)")
+    ap.add_argument("--refill", default="16", help="comma list of refill thresholds (dynamic variants)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -47,13 +48,15 @@ def main():
         except RuntimeError:
             break
     waves = [int(w) for w in args.waves.split(",")]
+    refills = [int(f) for f in args.refill.split(",")]
     res = {}
     ref = None
     for r in range(args.rounds):
         for v in ok:
-            for w in waves:
+            for w, f in [(w, f) for w in waves for f in refills]:
                 dev.set_option("variant", v)
                 dev.set_option("waves_per_cu", w)
+                dev.set_option("refill", f)
                 p = ca.render_params(xres, yres, args.spp, k, seed, layer=1)
                 dev.render_device(cam, p, frame.data_ptr(), stream)
                 torch.cuda.synchronize()
@@ -62,13 +65,13 @@ def main():
                     ref = frame.clone()
                 else:
                     assert torch.equal(frame, ref), "variant %d changed the image" % v
-                res.setdefault((v, w), []).append((dev.last_kernel_ms(), c["closest"] + c["shadow"]))
+                res.setdefault((v, w, f), []).append((dev.last_kernel_ms(), c["closest"] + c["shadow"]))
         print("round %d done" % r, file=sys.stderr, flush=True)
-    for (v, w), xs in sorted(res.items()):
+    for (v, w, f), xs in sorted(res.items()):
         ms = [x[0] for x in xs]
         rays = xs[0][1]
         med = statistics.median(ms)
-        print(json.dumps({"variant": v, "waves_per_cu": w, "median_ms": round(med, 2), "min_ms": round(min(ms), 2),
+        print(json.dumps({"variant": v, "waves_per_cu": w, "refill": f, "median_ms": round(med, 2), "min_ms": round(min(ms), 2),
                           "mray_s": round(rays / med / 1e3, 1)}), flush=True)
 
 
