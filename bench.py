@@ -83,6 +83,7 @@ def main():
 
     import chiaroscuro_amd as ca
     from chiaroscuro_amd import scenes
+    from chiaroscuro_amd.tiles import DistributedFrame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -115,24 +116,14 @@ def main():
     cam = ca.camera(info["VP"], info["LA"], info["UP"], info["yview"], xres, yres)
     tile = 32
     stream = torch.cuda.current_stream().cuda_stream
-    frame = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda")
-    p0 = ca.render_params(xres, yres, spp, k, seed, nranks=world, tile=tile)
-    max_tiles = ca.Device.tiles_for_rank(p0, 0)
-    tiles = torch.zeros((max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda") if world > 1 else None
-    gathered = (torch.zeros((world, max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda")
-                if world > 1 and rank == 0 else None)
+    fr = DistributedFrame(dev, xres, yres, rank, world, tile, dist)
+    tiles = fr.tiles
 
     totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0}
 
     def step(layer, record):
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
-        if world == 1:
-            dev.render_device(cam, p, frame.data_ptr(), stream)
-        else:
-            dev.render_tiles_device(cam, p, tiles.data_ptr(), stream)
-            dist.gather(tiles, [gathered[r] for r in range(world)] if rank == 0 else None, dst=0)
-            if rank == 0:
-                dev.blend_tiles_device(p, gathered.data_ptr(), frame.data_ptr(), stream)
+        fr.render_layer(cam, p, stream)
         if record:
             c = dev.counters()
             totals["rays"] += c["closest"] + c["shadow"]

@@ -1,0 +1,79 @@
+"""Multi-GPU frame protocol: tile split + one gather per layer.
+
+The frame is cut into `tile`×`tile` tiles, row-major; tile t belongs to rank
+t % nranks.  Each rank renders its tiles' batch means into a compact
+[ntiles_r][tile][tile][3] buffer (cr_render_tiles_device), rank 0 gathers the
+buffers over torch.distributed (RCCL over xGMI on GPUs, gloo in the CPU tests)
+and unpermutes + blends the layer on the device (cr_blend_tiles_device):
+    frame = (frame * (L - 1) + mean) / L           (src/rayTracer.cpp:64)
+Every (pixel, sample) is independent and the RNG key holds the global pixel
+index, so the image does not depend on the number of ranks.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class TileLayout:
+    xres: int
+    yres: int
+    nranks: int = 1
+    tile: int = 32
+
+    @property
+    def tiles_x(self) -> int:
+        return (self.xres + self.tile - 1) // self.tile
+
+    @property
+    def tiles_y(self) -> int:
+        return (self.yres + self.tile - 1) // self.tile
+
+    @property
+    def ntiles(self) -> int:
+        return self.tiles_x * self.tiles_y
+
+    def tiles_for_rank(self, rank: int) -> int:
+        """== cr_tiles_for_rank: tiles t < ntiles with t % nranks == rank."""
+        n = self.ntiles
+        return n // self.nranks + (1 if rank < n % self.nranks else 0)
+
+    @property
+    def max_tiles(self) -> int:
+        return self.tiles_for_rank(0)
+
+    def tile_origin(self, rank: int, local: int):
+        """Pixel origin (x0, y0) of the rank's local tile `local`."""
+        t = rank + local * self.nranks
+        return (t % self.tiles_x) * self.tile, (t // self.tiles_x) * self.tile
+
+
+class DistributedFrame:
+    """One rank's side of a layer: render my tiles, gather to rank 0, blend.
+
+    dev      chiaroscuro_amd.Device of this rank
+    dist     torch.distributed (initialised), or None for a single rank
+    """
+
+    def __init__(self, dev, xres: int, yres: int, rank: int, nranks: int, tile: int = 32, dist=None):
+        import torch
+        self.dev, self.dist, self.rank = dev, dist, rank
+        self.layout = TileLayout(xres, yres, nranks, tile)
+        L = self.layout
+        self.frame = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda") if rank == 0 or nranks == 1 \
+            else None
+        self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda") \
+            if nranks > 1 else None
+        self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda") \
+            if nranks > 1 and rank == 0 else None
+
+    def render_layer(self, cam, params, stream: int = 0):
+        """params: chiaroscuro_amd.render_params(..., layer=L, rank, nranks, tile)."""
+        L = self.layout
+        if L.nranks == 1:
+            self.dev.render_device(cam, params, self.frame.data_ptr(), stream)
+            return
+        self.dev.render_tiles_device(cam, params, self.tiles.data_ptr(), stream)
+        self.dist.gather(self.tiles, [self.gathered[r] for r in range(L.nranks)] if self.rank == 0 else None, dst=0)
+        if self.rank == 0:
+            self.dev.blend_tiles_device(params, self.gathered.data_ptr(), self.frame.data_ptr(), stream)
