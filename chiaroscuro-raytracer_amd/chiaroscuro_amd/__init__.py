@@ -42,7 +42,7 @@ class CrRenderParams(C.Structure):
 
 
 COUNTER_NAMES = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths", "pixels",
-                 "wave_desc", "wave_tri", "wave_round", "wave_query")
+                 "wave_desc", "wave_tri", "wave_round", "wave_query", "wave_desc_uniform", "wave_tri_uniform")
 
 
 class CrCounters(C.Structure):

@@ -31,8 +31,8 @@ struct cr_ctx {
     uint32_t *d_work = nullptr;
     float *d_accum = nullptr;
     size_t accum_elems = 0;
-    void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr;
-    size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0;
+    void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
+    size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
     cr_counters last{};
     // options
     int kernel = 0;
@@ -41,6 +41,7 @@ struct cr_ctx {
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
     uint32_t refill = 16; // sweep: 8 -> 548, 16 -> 608 Mray/s (sponza 1080p x 128 spp)
+    uint32_t wf_paths = 16u << 20; // wavefront kernel: paths in flight per chunk
 };
 
 namespace {
@@ -143,9 +144,11 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     cr::RenderArgs A{};
     fill_args(c, A, cam, p, out, mode);
     HIPCHK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), st));
-    if (c->kernel == 0) {
+    if (c->kernel == 0 || c->kernel == 2) {
+        const bool wf = c->kernel == 2;
         uint32_t blk, blocks;
-        cr::persistent_geometry(c->num_cus, c->waves_per_cu, blk, blocks);
+        if (wf) cr::wf_trace_geometry(c->full_counters ? -1 : c->variant, c->num_cus, blk, blocks);
+        else cr::persistent_geometry(c->num_cus, c->waves_per_cu, blk, blocks);
         A.gstride = blk * blocks;
         // samples per chunk: the per-sample buffer stays within SAMPLE_BUF_BYTES
         // and the work index within 31 bits
@@ -156,21 +159,62 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         const bool chunked = chunk < p->spp;
         if (int r = grow(c, &c->d_gstack, c->gstack_bytes, cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
             return r;
-        if (int r = grow(c, &c->d_pathbuf, c->pathbuf_bytes, cr::persistent_pathbuf_bytes(p->k, A.gstride))) return r;
         if (int r = grow(c, &c->d_samples, c->samples_bytes, per_sample * chunk)) return r;
         if (chunked)
             if (int r = grow(c, &c->d_run, c->run_bytes, per_sample)) return r;
         A.gstack = (uint2 *)c->d_gstack;
-        A.pathbuf = (float4 *)c->d_pathbuf;
         A.samples = (float *)c->d_samples;
         A.run = (float *)c->d_run;
+        cr::WfArgs W{};
+        if (wf) {
+            // path slots per wavefront chunk, and the queues / state carved from one buffer
+            const uint64_t P = std::min<uint64_t>((uint64_t)A.n_items * chunk, c->wf_paths);
+            const size_t f4 = 16 * (size_t)P;
+            const size_t need = (4 + 1 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 8 * (size_t)P +
+                                cr::WF_CNT * sizeof(uint32_t) + 4096;
+            if (int r = grow(c, &c->d_wf, c->wf_bytes, need)) return r;
+            char *b = (char *)c->d_wf;
+            auto take = [&](size_t bytes) {
+                char *r = b;
+                b += (bytes + 255) & ~(size_t)255;
+                return r;
+            };
+            W.ray[0] = (float4 *)take(2 * f4);
+            W.ray[1] = (float4 *)take(2 * f4);
+            W.hit = (uint4 *)take(f4);
+            W.sray = (float4 *)take(2 * f4);
+            W.ps = (float4 *)take(cr::WF_STATE * f4);
+            W.dw = (float4 *)take(2 * (size_t)p->k * f4);
+            W.sexcl = (uint32_t *)take(4 * (size_t)P);
+            W.occ = (uint32_t *)take(4 * (size_t)P);
+            W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
+            W.gstack = A.gstack;
+            W.gstride = A.gstride;
+            W.P = (uint32_t)P;
+        } else {
+            if (int r = grow(c, &c->d_pathbuf, c->pathbuf_bytes, cr::persistent_pathbuf_bytes(p->k, A.gstride)))
+                return r;
+            A.pathbuf = (float4 *)c->d_pathbuf;
+        }
         HIPCHK(hipEventRecord(c->ev0, st));
         for (uint32_t s0 = 0; s0 < p->spp; s0 += (uint32_t)chunk) {
             A.s0 = s0;
             A.s_count = (uint32_t)std::min<uint64_t>(chunk, p->spp - s0);
             A.n_work = A.n_items * A.s_count;
-            HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
-            int e = cr::launch_persistent(A, c->waves_per_cu, c->num_cus, st);
+            int e = 0;
+            if (wf) {
+                const uint32_t P = W.P;
+                for (uint32_t w0 = 0; w0 < A.n_work && !e; w0 += P) {
+                    W.w0 = w0;
+                    W.P = std::min(P, A.n_work - w0);
+                    HIPCHK(hipMemsetAsync(W.cnt, 0, cr::WF_CNT * sizeof(uint32_t), st));
+                    e = cr::launch_wavefront_chunk(A, W, c->num_cus, st);
+                }
+                W.P = P;
+            } else {
+                HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
+                e = cr::launch_persistent(A, c->waves_per_cu, c->num_cus, st);
+            }
             if (!e) e = cr::launch_sum_samples(A, s0 == 0, s0 + A.s_count == p->spp, st);
             if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
         }
@@ -186,7 +230,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     HIPCHK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]};
+    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13], h[14]};
     return CR_OK;
 }
 
@@ -233,6 +277,7 @@ void cr_destroy(cr_ctx *c) {
         if (c->d_pathbuf) hipFree(c->d_pathbuf);
         if (c->d_samples) hipFree(c->d_samples);
         if (c->d_run) hipFree(c->d_run);
+        if (c->d_wf) hipFree(c->d_wf);
         if (c->d_counters) hipFree(c->d_counters);
         if (c->d_work) hipFree(c->d_work);
         if (c->ev0) hipEventDestroy(c->ev0);
@@ -272,16 +317,17 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     }
     // leaf-ordered triangle records {A,id},{B-A},{C-A}: e1/e2 computed exactly as
     // intersectRayTriangle does each time (kdtree.cpp:222-223), so bit-identical.
-    std::vector<float4> recs((size_t)3 * d->n_refs);
+    std::vector<float4> recs((size_t)cr::REC_STRIDE * d->n_refs, make_float4(0.f, 0.f, 0.f, 0.f));
     for (uint32_t r = 0; r < d->n_refs; r++) {
         const uint32_t t = d->refs[r];
         if (t >= nt) return fail(c, CR_E_INVALID, "leaf ref out of range");
         const float *p = d->tri_pos + 9 * (size_t)t;
         float idf;
         std::memcpy(&idf, &t, 4);
-        recs[3 * (size_t)r] = make_float4(p[0], p[1], p[2], idf);
-        recs[3 * (size_t)r + 1] = make_float4(p[3] - p[0], p[4] - p[1], p[5] - p[2], 0.f);
-        recs[3 * (size_t)r + 2] = make_float4(p[6] - p[0], p[7] - p[1], p[8] - p[2], 0.f);
+        float4 *q = recs.data() + (size_t)cr::REC_STRIDE * r;
+        q[0] = make_float4(p[0], p[1], p[2], idf);
+        q[1] = make_float4(p[3] - p[0], p[4] - p[1], p[5] - p[2], 0.f);
+        q[2] = make_float4(p[6] - p[0], p[7] - p[1], p[8] - p[2], 0.f);
     }
     std::vector<float4> tri((size_t)3 * nt), mn(nt), mkd(nt), mke(nt);
     std::vector<float2> muv((size_t)3 * nt);
@@ -446,7 +492,7 @@ static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, cons
     if (e == hipSuccess) e = hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost);
     hipFree(buf);
     if (e != hipSuccess) return hip_fail(c, e, "intersect");
-    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12]};
+    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13], h[14]};
     return CR_OK;
 }
 
@@ -471,12 +517,15 @@ float cr_last_kernel_ms(cr_ctx *c) { return c ? c->last_ms : 0.f; }
 
 int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!c || !key) return CR_E_INVALID;
-    if (!std::strcmp(key, "kernel") && (v == 0 || v == 1)) c->kernel = (int)v;
+    const int64_t nvar = std::max(cr::num_persistent_variants(), cr::num_wf_variants());
+    if (!std::strcmp(key, "kernel") && (v == 0 || v == 1 || v == 2)) c->kernel = (int)v;
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
-    else if (!std::strcmp(key, "variant") && v >= 0 && v < cr::num_persistent_variants()) c->variant = (int)v;
+    else if (!std::strcmp(key, "variant") && v >= 0 && v < nvar) c->variant = (int)v; // clamped per kernel
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
-    else if (!std::strcmp(key, "refill") && v >= 1 && v <= 64) c->refill = (uint32_t)v;    else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
+    else if (!std::strcmp(key, "refill") && v >= 1 && v <= 64) c->refill = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
+    else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
     return CR_OK;
 }
 

@@ -79,12 +79,12 @@ __device__ __forceinline__ bool traverse(const DevScene &S, const Stack &stk, f3
         const uint32_t first = nd.x, count = nd.y >> 2;
         bool found = false;
         for (uint32_t j = 0; j < count; j++) {
-            const float4 r0 = S.recs[3 * (first + j)];
-            const uint32_t id = __float_as_uint(r0.w);
+            const TriRec r = load_rec(S, first + j);
+            const uint32_t id = rec_id(r);
             if (SHADOW && id == exclude) continue;
             c.tritest++;
             float ux, uy, t;
-            if (tri_test(o, d, r0, S.recs[3 * (first + j) + 1], S.recs[3 * (first + j) + 2], tmax, ux, uy, t)) {
+            if (tri_test(o, d, r, tmax, ux, uy, t)) {
                 if (SHADOW) return true;
                 bx = ux;
                 by = uy;

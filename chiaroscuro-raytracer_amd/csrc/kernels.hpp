@@ -6,6 +6,9 @@
 namespace cr {
 
 enum { MODE_BLEND = 0, MODE_TILES = 1 };
+// float4 per triangle record.  3 (48 B, 1.5 lines per test on average) beat 4
+// (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
+enum { REC_STRIDE = 3 };
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one
 // texel past the row/image end for coords == 1.0 (src/mesh.cpp:23-30) and three
@@ -14,7 +17,10 @@ __host__ __device__ inline uint64_t tex_pad(int w, int nc) { return (uint64_t)(w
 
 struct DevScene {
     const uint2 *nodes;   // {split bits | first ref, axis | child<<2 ; leaf: 3 | count<<2}
-    const float4 *recs;   // 3 per leaf ref: {A, id bits}, {B-A, 0}, {C-A, 0}
+    // REC_STRIDE float4 per leaf reference, AoS: {A, tri id bits}, {e1 = B-A, 0},
+    // {e2 = C-A, 0} -- bitwise what the reference computes per test.  (A 40-B SoA
+    // split measured 15% slower: three cache lines per test instead of one or two.)
+    const float4 *recs;
     const float4 *tri;    // 3 per triangle: A, B, C
     const float4 *mat_n;  // normal, w = emissive flag bits
     const float4 *mat_kd; // Kd, w = texture index (int bits, -1 none)
@@ -70,6 +76,33 @@ enum : uint64_t { SAMPLE_BUF_BYTES = 4ull << 30 };
 int launch_persistent(const RenderArgs &A, uint32_t waves_per_cu, int num_cus, hipStream_t st);
 // Per-pixel in-order sum of one chunk's samples; `last` blends / writes the pixel.
 int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t st);
+
+// Wavefront path tracer (wavefront.hip, cr_set_option "kernel" 2): the paths of
+// work items [w0, w0 + P) advance one bounce per generation through separate
+// kernels (camera, closest trace, shade, shadow trace, bounce) that exchange
+// rays through queues in HBM.
+enum : uint32_t { WF_CNT = 256 }; // counters: closest count [g], shadow count [64+g], work [128+g], [192+g]
+enum { WF_STATE = 5 };            // path-state float4 slots per path
+struct WfArgs {
+    uint32_t P;       // path slots of this chunk
+    uint32_t w0;      // first work item of the chunk
+    float4 *ray[2];   // closest rays, by generation parity: [2P] {o, path}, {d, 0}
+    uint4 *hit;       // [P] closest result of ray i: {tri, bx bits, by bits, 1} / {0, 0, 0, 0}
+    float4 *sray;     // [2P] shadow rays {o, path}, {d, limit}
+    uint32_t *sexcl;  // [P] light triangle the shadow ray ignores
+    uint32_t *occ;    // [P] shadow result of shadow ray j
+    uint32_t *cnt;    // [WF_CNT] zeroed per chunk
+    float4 *ps;       // [WF_STATE][P] path state
+    float4 *dw;       // [2K][P] (direct, w) per bounce
+    uint2 *gstack;    // trace kernels' stack overflow [depth][gstride]
+    uint32_t gstride; // threads of the trace grid
+};
+// rays 2x2 float4, hit 1, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs
+inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 1 + 2 + WF_STATE + 2 * K) * 16 + 8; }
+int num_wf_variants();
+void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
+// One chunk: camera generation + K x (closest, shade, shadow, bounce).
+int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st);
 // Persistent grid geometry chosen by launch_render (block threads, blocks).
 void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);
 

@@ -26,28 +26,9 @@
 //     bounce count, work item) is parked in a per-lane HBM record across the
 //     traversal rounds instead of occupying VGPRs;
 //   * per-bounce (direct, w) pairs for the back-to-front fold go to HBM too.
-#include "render_common.hpp"
+#include "traverse.hpp"
 
 namespace cr {
-
-enum : uint32_t {
-    ST_NEED_WORK = 0, // take the next (pixel, sample) item
-    ST_CLOSEST = 2,   // closest-hit query in flight
-    ST_SHADOW = 3,    // NEE shadow query in flight
-    ST_DONE = 4,      // no work left
-    ST_HIT = 5,       // query results waiting for the path state machine
-    ST_MISS = 6,
-    ST_OCCLUDED = 7,
-    ST_VISIBLE = 8,
-};
-enum : int { T_CLOSEST = 0, T_SHADOW = 1, T_HIT = 5, T_TEXHIT = 6, T_PATHS = 7, T_PIXELS = 8, T_N = 9 };
-
-// Per-query tallies are wave-aggregated LDS atomics: the state machine runs in
-// divergent code, so a wave total cannot be kept wave-uniform in registers.
-__device__ __forceinline__ void tally(unsigned long long *tl, int i, bool pred) {
-    const uint64_t b = __ballot(pred);
-    if (b && wave_leader()) atomicAdd(&tl[i], (unsigned long long)__popcll(b));
-}
 
 // Parked lane state, float4 slots [slot][gstride]:
 //   0 direct.xyz | k     1 fcol.xyz | work item
@@ -57,7 +38,6 @@ struct Lane {
     uint32_t k, w;
     Rng rng;
 };
-__device__ __forceinline__ float4 pk(f3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 __device__ __forceinline__ void park(float4 *buf, uint32_t gstride, uint32_t gid, const Lane &L) {
     buf[gid] = pk(L.direct, L.k);
     buf[(size_t)gstride + gid] = pk(L.fcol, L.w);
@@ -75,138 +55,6 @@ __device__ __forceinline__ void unpark(const float4 *buf, uint32_t gstride, uint
     L.rng.key = __float_as_uint(c.w);
     L.contrib = ld3(d);
     L.rng.ctr = __float_as_uint(d.w);
-}
-
-// Traversal registers of a query in flight.  r = per-axis rcp_for_div(d) for
-// the exact short split-distance division (FD builds, device_math.hpp).
-struct Trav {
-    uint32_t node, sp, nl;
-    float tmin, tmax;
-    f3 r;
-};
-
-// Root-box clip (kdtree.cpp:196-208, 276-283); false: the query ends without a hit.
-__device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool shadow, float limit, Trav &T) {
-    const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
-    ray_box_inv(S, o, inv, T.tmin, T.tmax);
-    if (T.tmax < 0 || T.tmax < T.tmin) return false;
-    if (shadow) {
-        if (T.tmin > limit) return false;
-        T.tmax = std_min(T.tmax, limit);
-    }
-    const float nan = __builtin_nanf("");
-    T.r = mk(fabsf(d.x) >= 0x1p-40f && fabsf(d.x) <= 0x1p40f ? inv.x : nan,
-             fabsf(d.y) >= 0x1p-40f && fabsf(d.y) <= 0x1p40f ? inv.y : nan,
-             fabsf(d.z) >= 0x1p-40f && fabsf(d.z) <= 0x1p40f ? inv.z : nan);
-    T.node = T.sp = T.nl = 0;
-    return true;
-}
-
-// One traversal round (kdtree.cpp:250-330 as an explicit stack): descend to the
-// next leaf, test it, pop.  Returns the lane's new state: unchanged while the
-// query continues, else its result (a closest hit leaves {bx, by, tri} in d:
-// the direction is dead by then).
-// (Speculative descent -- lanes that reached their leaf early descending toward
-// the next one, Aila & Laine's postponed leaves -- is exact here too but
-// measured slower: the merged descent loop costs more than the idle lanes.)
-template <int R, bool FULL, bool PF, bool FD>
-__device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
-                                               uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
-                                               Ctr &c) {
-    const uint32_t bdim = blockDim.x, tid = threadIdx.x;
-    uint2 nd = S.nodes[T.node];
-    while ((nd.y & 3u) != 3u) {
-        if (FULL) {
-            c.inner++;
-            if (wave_leader()) c.wave_desc++;
-        }
-        const uint32_t a = nd.y & 3u;
-        const float split = __uint_as_float(nd.x);
-        const float oa = comp(o, a), da = comp(d, a);
-        const float tsplit = FD ? div_by_rcp(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
-        const uint32_t below = (oa < split) || (oa == split && da <= 0);
-        const uint32_t child = nd.y >> 2;
-        if (tsplit >= T.tmax || tsplit < 0) {
-            T.node = child + (1u - below);
-        } else if (tsplit <= T.tmin) {
-            T.node = child + below;
-        } else {
-            const uint2 e = make_uint2(child + below, __float_as_uint(T.tmax));
-            const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
-            if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
-            else T.nl++;
-            ring[slot] = e;
-            T.sp++;
-            T.node = child + (1u - below);
-            T.tmax = tsplit;
-        }
-        nd = S.nodes[T.node];
-    }
-    if (FULL) {
-        c.leaf++;
-        if (wave_leader()) c.wave_round++;
-    }
-    const uint32_t first = nd.x, count = nd.y >> 2;
-    bool found = false, occluded = false;
-    uint32_t tri = 0;
-    float bx = 0.f, by = 0.f;
-    float4 n0, n1, n2;
-    if (PF && count) {
-        n0 = S.recs[3 * first];
-        n1 = S.recs[3 * first + 1];
-        n2 = S.recs[3 * first + 2];
-    }
-    for (uint32_t j = 0; j < count; j++) {
-        if (FULL && wave_leader()) c.wave_tri++;
-        float4 r0, r1, r2;
-        if (PF) { // software pipeline: issue triangle j+1's loads before testing j
-            r0 = n0;
-            r1 = n1;
-            r2 = n2;
-            if (j + 1 < count) {
-                n0 = S.recs[3 * (first + j + 1)];
-                n1 = S.recs[3 * (first + j + 1) + 1];
-                n2 = S.recs[3 * (first + j + 1) + 2];
-            }
-        } else {
-            r0 = S.recs[3 * (first + j)];
-            r1 = S.recs[3 * (first + j) + 1];
-            r2 = S.recs[3 * (first + j) + 2];
-        }
-        const uint32_t id = __float_as_uint(r0.w);
-        if (shadow && id == exclude) continue;
-        if (FULL) c.tritest++;
-        float ux, uy, t;
-        if (tri_test(o, d, r0, r1, r2, T.tmax, ux, uy, t)) {
-            if (shadow) {
-                occluded = true;
-                break;
-            }
-            bx = ux;
-            by = uy;
-            T.tmax = t;
-            tri = id;
-            found = true;
-        }
-    }
-    if (occluded) return ST_OCCLUDED;
-    if (found) {
-        d = mk(bx, by, __uint_as_float(tri));
-        return ST_HIT;
-    }
-    if (T.sp == 0) return shadow ? ST_VISIBLE : ST_MISS;
-    T.sp--;
-    uint2 e;
-    if (T.nl) {
-        e = ring[(T.sp & (R - 1)) * bdim + tid];
-        T.nl--;
-    } else {
-        e = gstk[(size_t)T.sp * gstride + gid];
-    }
-    T.node = e.x;
-    T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
-    T.tmax = __uint_as_float(e.y);
-    return shadow ? ST_SHADOW : ST_CLOSEST;
 }
 
 // Work item w of this launch -> (rank-local pixel item, sample index).

@@ -11,6 +11,7 @@ namespace cr {
 struct Ctr {
     uint32_t closest = 0, shadow = 0, inner = 0, leaf = 0, tritest = 0, hit = 0, texhit = 0, paths = 0, pixels = 0;
     uint32_t wave_desc = 0, wave_tri = 0, wave_round = 0, wave_query = 0; // diagnostics, see chiaro_hip.h
+    uint32_t wave_desc_uniform = 0, wave_tri_uniform = 0;
 };
 __device__ __forceinline__ uint32_t wave_count(bool pred) { return (uint32_t)__popcll(__ballot(pred)); }
 // True in exactly one active lane (the lowest): `if (wave_leader()) n++` counts
@@ -21,10 +22,11 @@ __device__ __forceinline__ bool wave_leader() {
 
 // Call with the whole wave converged.
 __device__ __forceinline__ void flush_counters(unsigned long long *ctrs, const Ctr &c, uint32_t uniform = 0u) {
-    const uint32_t v[13] = {c.closest, c.shadow,  c.inner,    c.leaf,     c.tritest,   c.hit,       c.texhit,
-                            c.paths,   c.pixels, c.wave_desc, c.wave_tri, c.wave_round, c.wave_query};
+    const uint32_t v[15] = {c.closest, c.shadow,  c.inner,    c.leaf,     c.tritest,   c.hit,       c.texhit,
+                            c.paths,   c.pixels, c.wave_desc, c.wave_tri, c.wave_round, c.wave_query,
+                            c.wave_desc_uniform, c.wave_tri_uniform};
 #pragma unroll
-    for (int i = 0; i < 13; i++) {
+    for (int i = 0; i < 15; i++) {
         unsigned long long s = v[i];
         if (!(uniform & (1u << i))) {
 #pragma unroll
@@ -59,9 +61,18 @@ __device__ __forceinline__ void ray_box(const DevScene &S, f3 o, f3 d, float &fi
 // (coherent camera rays), and a wave-uniform rejection skips the rest (measured:
 // a branch-free form was 10% slower on the sponza stand-in).  f = RN(1/aa) as
 // the reference's 1.f/a, by rcp_rn (exact, checked over every float in range).
-__device__ __forceinline__ bool tri_test(f3 o, f3 d, float4 r0, float4 r1, float4 r2, float tmax, float &ux,
-                                         float &uy, float &t) {
-    const f3 v0 = ld3(r0), e1 = ld3(r1), e2 = ld3(r2);
+struct TriRec {
+    float4 a; // A, tri id bits
+    float4 b; // e1
+    float4 c; // e2
+};
+__device__ __forceinline__ TriRec load_rec(const DevScene &S, uint32_t ref) {
+    const float4 *p = S.recs + (size_t)REC_STRIDE * ref;
+    return TriRec{p[0], p[1], p[2]};
+}
+__device__ __forceinline__ uint32_t rec_id(const TriRec &r) { return __float_as_uint(r.a.w); }
+__device__ __forceinline__ bool tri_test(f3 o, f3 d, const TriRec &r, float tmax, float &ux, float &uy, float &t) {
+    const f3 v0 = ld3(r.a), e1 = ld3(r.b), e2 = ld3(r.c);
     const f3 p = cross(d, e2);
     const float aa = dot(e1, p);
     if (aa < 1.19209290e-7F && aa > -1.19209290e-7F) return false;

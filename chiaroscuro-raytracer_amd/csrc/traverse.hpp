@@ -1,0 +1,179 @@
+// traverse.hpp -- the resumable kd traversal shared by the persistent megakernel
+// (persistent.hip) and the wavefront trace kernels (wavefront.hip).
+#pragma once
+#include "render_common.hpp"
+
+namespace cr {
+
+enum : uint32_t {
+    ST_NEED_WORK = 0, // lane has no query: take the next item / ray
+    ST_CLOSEST = 2,   // closest-hit query in flight
+    ST_SHADOW = 3,    // NEE shadow query in flight
+    ST_DONE = 4,      // no work left
+    ST_HIT = 5,       // query results
+    ST_MISS = 6,
+    ST_OCCLUDED = 7,
+    ST_VISIBLE = 8,
+};
+
+// True when every active lane holds the same x.
+__device__ __forceinline__ bool wave_uniform(uint32_t x) {
+    return __ballot(x == (uint32_t)__builtin_amdgcn_readfirstlane(x)) == __ballot(1);
+}
+
+// Traversal registers of a query in flight.  r = per-axis rcp_for_div(d) for
+// the exact short split-distance division (FD builds, device_math.hpp).
+struct Trav {
+    uint32_t node, sp, nl;
+    float tmin, tmax;
+    f3 r;
+};
+
+// Root-box clip (kdtree.cpp:196-208, 276-283); false: the query ends without a hit.
+__device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool shadow, float limit, Trav &T) {
+    const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    ray_box_inv(S, o, inv, T.tmin, T.tmax);
+    if (T.tmax < 0 || T.tmax < T.tmin) return false;
+    if (shadow) {
+        if (T.tmin > limit) return false;
+        T.tmax = std_min(T.tmax, limit);
+    }
+    const float nan = __builtin_nanf("");
+    T.r = mk(fabsf(d.x) >= 0x1p-40f && fabsf(d.x) <= 0x1p40f ? inv.x : nan,
+             fabsf(d.y) >= 0x1p-40f && fabsf(d.y) <= 0x1p40f ? inv.y : nan,
+             fabsf(d.z) >= 0x1p-40f && fabsf(d.z) <= 0x1p40f ? inv.z : nan);
+    T.node = T.sp = T.nl = 0;
+    return true;
+}
+
+// One traversal round (kdtree.cpp:250-330 as an explicit stack): descend to the
+// next leaf, test it, pop.  Returns the lane's new state: unchanged while the
+// query continues, else its result (a closest hit leaves {bx, by, tri} in d:
+// the direction is dead by then).
+//   Stack: entries {far node, tmax at push}; the top R live in an LDS ring
+//   [slot][thread] (blockDim.x threads), deeper ones spill to gstk
+//   [depth][gstride].  On pop the interval is [current tmax, entry.tmax]: the
+//   current tmax equals the push-time tsplit (stack invariant).
+// (Speculative descent -- lanes that reached their leaf early descending toward
+// the next one, Aila & Laine's postponed leaves -- is exact here too but
+// measured slower: the merged descent loop costs more than the idle lanes.)
+template <int R, bool FULL, bool PF, bool FD>
+__device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
+                                               uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
+                                               Ctr &c) {
+    const uint32_t bdim = blockDim.x, tid = threadIdx.x;
+    uint2 nd = S.nodes[T.node];
+    while ((nd.y & 3u) != 3u) {
+        if (FULL) {
+            c.inner++;
+            const bool uni = wave_uniform(T.node);
+            if (wave_leader()) {
+                c.wave_desc++;
+                c.wave_desc_uniform += uni;
+            }
+        }
+        const uint32_t a = nd.y & 3u;
+        const float split = __uint_as_float(nd.x);
+        const float oa = comp(o, a), da = comp(d, a);
+        const float tsplit = FD ? div_by_rcp(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
+        const uint32_t below = (oa < split) || (oa == split && da <= 0);
+        const uint32_t child = nd.y >> 2;
+        if (tsplit >= T.tmax || tsplit < 0) {
+            T.node = child + (1u - below);
+        } else if (tsplit <= T.tmin) {
+            T.node = child + below;
+        } else {
+            const uint2 e = make_uint2(child + below, __float_as_uint(T.tmax));
+            const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
+            if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
+            else T.nl++;
+            ring[slot] = e;
+            T.sp++;
+            T.node = child + (1u - below);
+            T.tmax = tsplit;
+        }
+        nd = S.nodes[T.node];
+    }
+    if (FULL) {
+        c.leaf++;
+        if (wave_leader()) c.wave_round++;
+    }
+    const uint32_t first = nd.x, count = nd.y >> 2;
+    bool found = false, occluded = false;
+    uint32_t tri = 0;
+    float bx = 0.f, by = 0.f;
+    TriRec nx;
+    if (PF && count) nx = load_rec(S, first);
+    for (uint32_t j = 0; j < count; j++) {
+        if (FULL) {
+            const bool uni = wave_uniform(first + j);
+            if (wave_leader()) {
+                c.wave_tri++;
+                c.wave_tri_uniform += uni;
+            }
+        }
+        TriRec r;
+        if (PF) { // software pipeline: issue triangle j+1's loads before testing j
+            r = nx;
+            if (j + 1 < count) nx = load_rec(S, first + j + 1);
+        } else {
+            r = load_rec(S, first + j);
+        }
+        const uint32_t id = rec_id(r);
+        if (shadow && id == exclude) continue;
+        if (FULL) c.tritest++;
+        float ux, uy, t;
+        if (tri_test(o, d, r, T.tmax, ux, uy, t)) {
+            if (shadow) {
+                occluded = true;
+                break;
+            }
+            bx = ux;
+            by = uy;
+            T.tmax = t;
+            tri = id;
+            found = true;
+        }
+    }
+    if (occluded) return ST_OCCLUDED;
+    if (found) {
+        d = mk(bx, by, __uint_as_float(tri));
+        return ST_HIT;
+    }
+    if (T.sp == 0) return shadow ? ST_VISIBLE : ST_MISS;
+    T.sp--;
+    uint2 e;
+    if (T.nl) {
+        e = ring[(T.sp & (R - 1)) * bdim + tid];
+        T.nl--;
+    } else {
+        e = gstk[(size_t)T.sp * gstride + gid];
+    }
+    T.node = e.x;
+    T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
+    T.tmax = __uint_as_float(e.y);
+    return shadow ? ST_SHADOW : ST_CLOSEST;
+}
+
+// Per-query tallies are wave-aggregated LDS atomics: the callers run in
+// divergent code, so a wave total cannot be kept wave-uniform in registers.
+enum : int { T_CLOSEST = 0, T_SHADOW = 1, T_HIT = 5, T_TEXHIT = 6, T_PATHS = 7, T_PIXELS = 8, T_N = 9 };
+__device__ __forceinline__ void tally(unsigned long long *tl, int i, bool pred) {
+    const uint64_t b = __ballot(pred);
+    if (b && wave_leader()) atomicAdd(&tl[i], (unsigned long long)__popcll(b));
+}
+
+__device__ __forceinline__ float4 pk(f3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
+
+// Wave-aggregated append: one atomicAdd per wave, slots in lane order.
+__device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
+    const uint64_t m = __ballot(pred);
+    if (!m) return 0;
+    const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1u;
+    uint32_t base = 0;
+    if ((threadIdx.x & 63u) == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader, 64);
+    return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+} // namespace cr

@@ -1,0 +1,308 @@
+// wavefront.hip -- wavefront path tracer (cr_set_option "kernel" 2).
+//
+// The megakernel (persistent.hip) keeps every lane's traversal registers live
+// while other lanes of its wave shade, so its register peak is traversal +
+// shading and it runs at 6 waves/SIMD; occupancy measured as its main lever
+// (2 -> 6 waves/SIMD: 260 -> 563 Mray/s).  Here the same per-path arithmetic is
+// split by phase into kernels that exchange work through queues in HBM:
+//
+//   wf_camera                 one closest ray per path of the chunk
+//   for g = 1..K:
+//     wf_trace<closest>(g)    resumable traversal only: small register file,
+//                             high occupancy, lanes refill from the queue
+//     wf_shade(g)             hit reconstruction, emission, NEE light sample
+//                             -> shadow-ray queue (rayTracer.cpp:80-99)
+//     wf_trace<shadow>(g)
+//     wf_bounce(g)            NEE result, RR, BRDF sample -> next closest queue,
+//                             or finish the path (back-to-front fold)
+//
+// Paths keep their (pixel, sample) RNG keys and draw order, and every path
+// writes its radiance to samples[w]; sum_samples adds them per pixel in sample
+// order, so the image is bit-identical to the megakernel's and the oracle's.
+// Queue appends are wave-aggregated (one atomic per wave, lane order kept), so
+// neighbouring paths -- samples of the same pixel -- stay neighbours in the
+// queues and the trace waves stay coherent.
+#include "traverse.hpp"
+
+namespace cr {
+
+enum : uint32_t { NO_SLOT = 0xffffffffu };
+
+__device__ __forceinline__ uint32_t *cnt_closest(const WfArgs &W, uint32_t g) { return W.cnt + g; }
+__device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 64 + g; }
+__device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 128 + g; }
+__device__ __forceinline__ uint32_t *work_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 192 + g; }
+
+__device__ __forceinline__ void flush_tallies(const RenderArgs &A, unsigned long long *tl) {
+    __syncthreads();
+    if (threadIdx.x < T_N && tl[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], tl[threadIdx.x]);
+}
+
+// Back-to-front fold of a finished path (r_j = D_j + W_j * r_{j+1}) into samples[w].
+__device__ __forceinline__ void finish_path(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t k, f3 tail) {
+    f3 acc = tail;
+    for (int j = (int)k - 2; j >= 0; j--) {
+        const float4 Dj = W.dw[(size_t)(2 * j) * W.P + p];
+        const float4 Wj = W.dw[(size_t)(2 * j + 1) * W.P + p];
+        acc = add(ld3(Dj), mul(ld3(Wj), acc));
+    }
+    float *out = A.samples + 3 * (size_t)(W.w0 + p);
+    out[0] = acc.x;
+    out[1] = acc.y;
+    out[2] = acc.z;
+}
+
+// Path state slots [slot][P]: 0 {direct, k}  1 {fcol, rng.key}  2 {normal, rng.ctr}
+//                             3 {contrib, shadow slot}  4 {next origin, -}
+__device__ __forceinline__ float4 &PS(const WfArgs &W, int slot, uint32_t p) { return W.ps[(size_t)slot * W.P + p]; }
+
+// ---------------------------------------------------------------- camera --
+__global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
+    __shared__ unsigned long long tl[T_N];
+    if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t base = blockIdx.x * blockDim.x; base < W.P; base += gridDim.x * blockDim.x) {
+        const uint32_t p = base + threadIdx.x;
+        const uint32_t w = W.w0 + p;
+        uint32_t item = 0, s = 0, px = 0, py = 0;
+        bool valid = p < W.P && w < A.n_work;
+        if (valid) {
+            item = w / A.s_count;
+            s = A.s0 + (w - item * A.s_count);
+            valid = item_pixel(A, item, px, py); // partial-tile pixels outside the image: no path
+        }
+        const uint32_t i = wave_append(cnt_closest(W, 1), valid);
+        tally(tl, T_PATHS, valid);
+        if (valid) { // rayTracer.cpp:58-62: jittered camera ray of sample s
+            Rng rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
+            const f3 d = camera_dir(A, px, py, rng);
+            PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), 1u);
+            PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key);
+            PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
+            W.ray[1][2 * (size_t)i] = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(p));
+            W.ray[1][2 * (size_t)i + 1] = pk(d, 0u);
+        }
+    }
+    flush_tallies(A, tl);
+}
+
+// ----------------------------------------------------------------- trace --
+// Persistent: every lane runs one query at a time through trav_round; when
+// `A.refill` lanes of a wave have finished (or none is busy) they take the
+// next rays of the queue (one atomicAdd per wave).
+template <bool SHADOW, bool FULL, int R, int MINW>
+__global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
+    extern __shared__ uint2 ring_lds[];
+    const DevScene &S = A.S;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t n = SHADOW ? *cnt_shadow(W, g) : *cnt_closest(W, g);
+    uint32_t *work = SHADOW ? work_shadow(W, g) : work_closest(W, g);
+    const float4 *rays = SHADOW ? W.sray : W.ray[g & 1];
+    Ctr c = {};
+    uint32_t state = ST_NEED_WORK, idx = 0, exclude = 0;
+    f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
+    Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
+    const uint32_t busy_st = SHADOW ? ST_SHADOW : ST_CLOSEST;
+    for (;;) {
+        const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
+        if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= A.refill)) {
+            for (;;) { // refill; a ray culled by the root box is answered at once and refetched
+                const uint64_t m = __ballot(state == ST_NEED_WORK);
+                if (!m) break;
+                const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1u;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(work, (uint32_t)__popcll(m));
+                base = __shfl(base, (int)leader, 64);
+                if (state == ST_NEED_WORK) {
+                    idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (idx >= n) {
+                        state = ST_DONE;
+                    } else {
+                        const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
+                        o = ld3(r0);
+                        d = ld3(r1);
+                        if (SHADOW) exclude = W.sexcl[idx];
+                        if (trav_begin(S, o, d, SHADOW, r1.w, T)) {
+                            state = busy_st;
+                        } else if (SHADOW) {
+                            W.occ[idx] = 0u; // culled: visible (kdtree.cpp:285-287)
+                        } else {
+                            W.hit[idx] = make_uint4(0u, 0u, 0u, 0u);
+                        }
+                    }
+                }
+            }
+        }
+        if (!__any(state == busy_st)) {
+            if (!__any(state != ST_DONE)) break;
+            continue;
+        }
+        if (state == busy_st) {
+            const uint32_t r = trav_round<R, FULL, true, false>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
+                                                                 exclude, T, c);
+            if (r != busy_st) {
+                if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
+                else W.hit[idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
+                                                           __float_as_uint(d.y), 1u)
+                                              : make_uint4(0u, 0u, 0u, 0u);
+                state = ST_NEED_WORK;
+            }
+        }
+    }
+    if (FULL) flush_counters(A.counters, c, 0u);
+    if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(&A.counters[SHADOW ? T_SHADOW : T_CLOSEST], n);
+}
+
+// ----------------------------------------------------------------- shade --
+// RayTracer::sendRay up to the shadow query (rayTracer.cpp:80-99) for every
+// closest ray of generation g; misses finish their path with the background.
+__global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
+    __shared__ unsigned long long tl[T_N];
+    if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
+    __syncthreads();
+    const DevScene &S = A.S;
+    const uint32_t n = *cnt_closest(W, g);
+    const float4 *rays = W.ray[g & 1];
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const bool in = i < n;
+        uint4 h = make_uint4(0u, 0u, 0u, 0u);
+        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (in) {
+            h = W.hit[i];
+            r0 = rays[2 * (size_t)i];
+        }
+        const uint32_t p = __float_as_uint(r0.w);
+        const bool hit = in && h.w != 0u;
+        bool textured = false, nee = false;
+        f3 sorg = mk(0.f, 0.f, 0.f), sdir = mk(0.f, 0.f, 0.f);
+        float sdist = 0.f;
+        uint32_t slight = 0;
+        if (in && !hit) {
+            finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
+        } else if (hit) {
+            const uint32_t k = __float_as_uint(PS(W, 0, p).w);
+            const HitShade hs = shade_hit(S, ld3(r0), h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
+            textured = hs.textured;
+            Rng rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
+            f3 contrib = mk(0.f, 0.f, 0.f), next = add(hs.p, muls(hs.normal, 0.001f));
+            if (S.nlights) {
+                const Nee e = sample_light(S, hs.p, hs.normal, hs.fcol, rng);
+                contrib = e.contrib;
+                next = e.origin;
+                sorg = e.origin;
+                sdir = e.dir;
+                sdist = e.distance;
+                slight = e.light;
+                nee = true;
+            }
+            PS(W, 0, p) = pk(hs.direct, k);
+            PS(W, 1, p) = pk(hs.fcol, rng.key);
+            PS(W, 2, p) = pk(hs.normal, rng.ctr);
+            PS(W, 4, p) = pk(next, 0u);
+            if (!nee) PS(W, 3, p) = pk(contrib, NO_SLOT);
+            else PS(W, 3, p) = pk(contrib, 0u); // slot set below
+        }
+        const uint32_t j = wave_append(cnt_shadow(W, g), nee);
+        if (nee) {
+            PS(W, 3, p).w = __uint_as_float(j);
+            W.sray[2 * (size_t)j] = pk(sorg, p);
+            W.sray[2 * (size_t)j + 1] = make_float4(sdir.x, sdir.y, sdir.z, sdist);
+            W.sexcl[j] = slight;
+        }
+        tally(tl, T_HIT, hit);
+        tally(tl, T_TEXHIT, textured);
+    }
+    flush_tallies(A, tl);
+}
+
+// ---------------------------------------------------------------- bounce --
+// NEE result, then the k == K cut, BRDF sample and Russian roulette
+// (rayTracer.cpp:100-134): either the next closest ray of generation g + 1 or
+// the end of the path.
+__global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_t g) {
+    const uint32_t n = *cnt_closest(W, g);
+    const float4 *rays = W.ray[g & 1];
+    float4 *next_rays = W.ray[(g + 1) & 1];
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        bool live = i < n && W.hit[min(i, n - 1)].w != 0u;
+        uint32_t p = 0, k = 0;
+        bool cont = false;
+        f3 wi = mk(0.f, 0.f, 0.f), org = mk(0.f, 0.f, 0.f);
+        if (live) {
+            p = __float_as_uint(rays[2 * (size_t)i].w);
+            const float4 s0 = PS(W, 0, p), s1 = PS(W, 1, p), s2 = PS(W, 2, p), s3 = PS(W, 3, p);
+            k = __float_as_uint(s0.w);
+            f3 direct = ld3(s0);
+            const f3 fcol = ld3(s1), normal = ld3(s2);
+            Rng rng{__float_as_uint(s1.w), __float_as_uint(s2.w)};
+            const uint32_t slot = __float_as_uint(s3.w);
+            if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(s3));
+            if ((int)k == A.K) {
+                finish_path(A, W, p, k, direct);
+            } else {
+                const float sx = rng_uniform(rng, -1.f, 1.f);
+                const float sy = rng_uniform(rng, -1.f, 1.f);
+                float pdf;
+                sample_wi(normal, sx, sy, wi, pdf);
+                const float Kmax = std_max(std_max(fcol.x, fcol.y), fcol.z);
+                if (pdf == 0.f || rng_uniform(rng, 0.f, 1.f) > Kmax) {
+                    finish_path(A, W, p, k, direct);
+                } else {
+                    const float cosine = fabsf(dot(normal, wi));
+                    const f3 w = divs(muls(fcol, cosine), pdf * Kmax);
+                    W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(direct, 0u);
+                    W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
+                    PS(W, 0, p) = pk(direct, k + 1);
+                    PS(W, 2, p).w = __uint_as_float(rng.ctr);
+                    org = ld3(PS(W, 4, p));
+                    cont = true;
+                }
+            }
+        }
+        const uint32_t j = wave_append(cnt_closest(W, g + 1), cont);
+        if (cont) {
+            next_rays[2 * (size_t)j] = pk(org, p);
+            next_rays[2 * (size_t)j + 1] = pk(wi, 0u);
+        }
+    }
+}
+
+// --------------------------------------------------------------- launch --
+struct WfVariant {
+    void (*closest)(RenderArgs, WfArgs, uint32_t);
+    void (*shadow)(RenderArgs, WfArgs, uint32_t);
+    int ring, waves_per_simd;
+};
+#define CR_WF(R, W) {wf_trace<false, false, R, W>, wf_trace<true, false, R, W>, R, W}
+static const WfVariant kWf[] = {CR_WF(4, 8), CR_WF(8, 8), CR_WF(4, 10), CR_WF(4, 12), CR_WF(8, 6)};
+static const WfVariant kWfCount = {wf_trace<false, true, 8, 1>, wf_trace<true, true, 8, 1>, 8, 4};
+static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
+int num_wf_variants() { return kNumWf; }
+
+void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks) {
+    const WfVariant &v = kWf[(variant >= 0 && variant < kNumWf) ? variant : 0];
+    block = 256;
+    blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)v.waves_per_simd; // 4 SIMDs, 4 waves/block
+}
+
+int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st) {
+    const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
+    uint32_t blk, blocks;
+    wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
+    if (W.gstride < blk * blocks) return (int)hipErrorInvalidValue;
+    const size_t lds = (size_t)v.ring * blk * sizeof(uint2);
+    const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
+    hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
+    for (uint32_t g = 1; g <= (uint32_t)A.K; g++) {
+        hipLaunchKernelGGL(v.closest, dim3(blocks), dim3(blk), lds, st, A, W, g);
+        hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
+        hipLaunchKernelGGL(wf_bounce, dim3(sgrid), dim3(256), 0, st, A, W, g);
+    }
+    return (int)hipGetLastError();
+}
+
+} // namespace cr

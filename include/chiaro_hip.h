@@ -131,6 +131,10 @@ typedef struct {
     uint64_t wave_tri;
     uint64_t wave_round;
     uint64_t wave_query;
+    /* of wave_desc / wave_tri: iterations whose node / triangle is the same for
+     * every active lane (a scalar load would serve the whole wave) */
+    uint64_t wave_desc_uniform;
+    uint64_t wave_tri_uniform;
 } cr_counters;
 
 cr_ctx *cr_create(int device);

@@ -50,6 +50,8 @@ def main():
         "eff_query": round(rays / (64 * max(c["wave_query"], 1)), 3),
         "rounds_per_query_wave": round(c["wave_round"] / max(c["wave_query"], 1), 1),
         "leaves_per_query_lane": round(c["leaf"] / rays, 1),
+        "uniform_desc": round(c["wave_desc_uniform"] / max(c["wave_desc"], 1), 3),
+        "uniform_tri": round(c["wave_tri_uniform"] / max(c["wave_tri"], 1), 3),
     })
     print(json.dumps(out))
 

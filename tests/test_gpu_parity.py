@@ -31,6 +31,21 @@ def sponza(ca, po, scenes):
     return Pair(ca, po, scenes.config_rtc("sponza"))
 
 
+@pytest.fixture(scope="module")
+def nanobox(ca, po, scenes):
+    return Pair(ca, po, scenes.config_rtc("nanobox"))
+
+
+@pytest.mark.parametrize("kernel", [0, 1, 2])
+def test_nanobox_textured_bitexact(ca, nanobox, kernel):
+    """C3 stand-in: RGB / RGBA / 1-channel textures, wrapped UVs, UV == 1 seams,
+    explicit vertex normals (Texture::getColorAt, src/mesh.cpp:21-35)."""
+    g, gc, o, oc = _render_both(ca, nanobox, 96, 54, 3, kernel=kernel)
+    assert_bitwise(g, o, "nanobox 96x54x3")
+    assert {k: gc[k] for k in ORACLE_KEYS} == oc
+    assert oc["texhit"] > oc["hit"] // 2 and o.mean() > 0.01
+
+
 def _render_both(ca, pair, xres, yres, spp, k=6, seed=0xC41A05C0, layer=1, kernel=None, accum=None):
     cam = pair.camera(ca, xres, yres)
     p = ca.render_params(xres, yres, spp, k, seed, layer=layer)
@@ -43,7 +58,7 @@ def _render_both(ca, pair, xres, yres, spp, k=6, seed=0xC41A05C0, layer=1, kerne
     return g, gc, o, oc
 
 
-@pytest.mark.parametrize("kernel", [0, 1])
+@pytest.mark.parametrize("kernel", [0, 1, 2])
 def test_cornell_bitexact(ca, cornell, kernel):
     g, gc, o, oc = _render_both(ca, cornell, 64, 64, 4, kernel=kernel)
     assert_bitwise(g, o, "cornell 64x64x4")
@@ -52,15 +67,17 @@ def test_cornell_bitexact(ca, cornell, kernel):
     assert o.mean() > 0.01  # lit
 
 
-def test_cornell_mm_bitexact_odd_size(ca, cornell_mm):
+@pytest.mark.parametrize("kernel", [0, 2])
+def test_cornell_mm_bitexact_odd_size(ca, cornell_mm, kernel):
     # non-multiple-of-tile image: edge tiles are partial
-    g, gc, o, oc = _render_both(ca, cornell_mm, 45, 37, 16)
+    g, gc, o, oc = _render_both(ca, cornell_mm, 45, 37, 16, kernel=kernel)
     assert_bitwise(g, o, "cornell_box 45x37x16")
     assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-def test_sponza_bitexact_small(ca, sponza):
-    g, gc, o, oc = _render_both(ca, sponza, 96, 54, 2)
+@pytest.mark.parametrize("kernel", [0, 2])
+def test_sponza_bitexact_small(ca, sponza, kernel):
+    g, gc, o, oc = _render_both(ca, sponza, 96, 54, 2, kernel=kernel)
     assert_bitwise(g, o, "sponza 96x54x2")
     assert {k: gc[k] for k in ORACLE_KEYS} == oc
     assert oc["tritest"] > 100 * oc["closest"] / 10

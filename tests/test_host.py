@@ -94,12 +94,14 @@ def test_obj_loader_assimp_semantics(ca, tmp_path):
     assert (t["tex"] == -1).all()
 
 
-@pytest.mark.parametrize("config", ["cornell", "cornell_box", "sponza"])
+@pytest.mark.parametrize("config", ["cornell", "cornell_box", "nanobox", "sponza"])
 def test_host_kdtree_equals_oracle(ca, po, scenes, config):
     sc = ca.Scene(scenes.config_rtc(config))
     m = ca.Model(sc)
     host = ca.KDTree(m, sc).export()
     orc = po.OracleScene(m.triangles(), leaf_size=sc.info["leaf_size"], build_threads=8).kd_export()
+    if config == "nanobox":
+        assert len(m.textures()) == 4 and (m.triangles()["tex"] >= 0).sum() > 20000
     for k in ("is_leaf", "axis", "child", "leaf_first", "leaf_count", "refs"):
         np.testing.assert_array_equal(host[k], orc[k], err_msg=k)
     for k in ("split", "box"):
