@@ -72,8 +72,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza", help="cornell | cornell_box | sponza | sponza_4k")
     ap.add_argument("--spp", type=int, default=0, help="override samples per step (default: config's)")
-    ap.add_argument("--kernel", type=int, default=-1, help="0 persistent (default), 1 one-thread-per-pixel")
-    ap.add_argument("--variant", type=int, default=-1, help="persistent-kernel variant (default 0)")
+    ap.add_argument("--kernel", type=int, default=-1,
+                    help="2 wavefront (default), 0 persistent megakernel, 1 one-thread-per-pixel")
+    ap.add_argument("--variant", type=int, default=-1, help="kernel build variant (default: the kernel's)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -183,19 +184,26 @@ def main():
         kms = totals["kernel_ms"] / max(totals["launches"], 1)
         bytes_per_launch = totals["bytes"]  # counting pass: one launch, same size as a timed one
         achieved = bytes_per_launch / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+        # measured fabric bytes of one render pass, from the committed rocprofv3 PMC
+        # summary of this same configuration (scripts/prof_summary.py); null if none
         traffic = None
         pmc = ROOT / "profiles" / ("pmc_%s.json" % args.config)
         if pmc.exists():
             try:
-                traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+                pj = json.loads(pmc.read_text())
+                if pj.get("spp") == spp and pj.get("n_gpus") == world:
+                    traffic = pj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        kernel_name = {0: "persistent megakernel", 1: "thread per pixel", 2: "wavefront"}[
+            args.kernel if args.kernel >= 0 else 2]
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(model.triangles(), info, info["leaf_size"], cam.as_array(), xres, yres, spp, k, seed,
                                args.cpu_budget)
         label = {"sponza": "sponza_standin (Sponza-Crytek stand-in, ~261k tris) 1920x1080",
                  "sponza_4k": "sponza_standin (Sponza-Crytek stand-in) 3840x2160",
+                 "nanobox": "nanobox_standin (textured nanosuit-in-a-box stand-in, ~20k tris) 1920x1080",
                  "cornell": "cornell_unit 256x256", "cornell_box": "cornell_box_lit 1024x1024"}[args.config]
         out = {
             "metric": "Mray/s (primary+secondary) on sponza_crytek 1080p; 1/2/4/8-GPU scaling",
@@ -215,7 +223,10 @@ def main():
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "render", "kernel_ms": round(kms, 3),
+                         # unit = one render pass (one layer): the wavefront's camera, K x (closest
+                         # trace, shade, shadow trace, bounce) and sum kernels, HIP events around
+                         # them on their stream; the two trace kernels are ~95% of it
+                         "kernel": "render pass (%s)" % kernel_name, "kernel_ms": round(kms, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch)},
             "cpu_baseline": cpu,
         }

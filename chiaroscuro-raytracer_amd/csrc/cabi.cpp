@@ -35,13 +35,16 @@ struct cr_ctx {
     size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
     cr_counters last{};
     // options
-    int kernel = 0;
+    // Defaults from sweeps on MI355X, sponza stand-in 1080p x 128 spp:
+    //   wavefront (kernel 2), trace variant 1, refill 48, 256M paths in flight: 801 Mray/s
+    //   persistent megakernel (kernel 0), variant 0, refill 16:                 615 Mray/s
+    int kernel = 2;
     int full_counters = 1;
-    int variant = 0;
+    int variant = -1;       // -1: the kernel's default build
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
-    uint32_t refill = 16; // sweep: 8 -> 548, 16 -> 608 Mray/s (sponza 1080p x 128 spp)
-    uint32_t wf_paths = 16u << 20; // wavefront kernel: paths in flight per chunk
+    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 48 wavefront)
+    uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
 };
 
 namespace {
@@ -132,8 +135,8 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.counters = c->d_counters;
     A.work = c->d_work;
     A.full_counters = c->full_counters;
-    A.variant = c->variant;
-    A.refill = c->refill;
+    A.refill = c->refill ? c->refill : (c->kernel == 2 ? 48u : 16u);
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 1 : 0);
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -147,7 +150,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     if (c->kernel == 0 || c->kernel == 2) {
         const bool wf = c->kernel == 2;
         uint32_t blk, blocks;
-        if (wf) cr::wf_trace_geometry(c->full_counters ? -1 : c->variant, c->num_cus, blk, blocks);
+        if (wf) cr::wf_trace_geometry(c->full_counters ? -1 : A.variant, c->num_cus, blk, blocks);
         else cr::persistent_geometry(c->num_cus, c->waves_per_cu, blk, blocks);
         A.gstride = blk * blocks;
         // samples per chunk: the per-sample buffer stays within SAMPLE_BUF_BYTES
@@ -168,7 +171,14 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         cr::WfArgs W{};
         if (wf) {
             // path slots per wavefront chunk, and the queues / state carved from one buffer
-            const uint64_t P = std::min<uint64_t>((uint64_t)A.n_items * chunk, c->wf_paths);
+            // ... at most ~40% of the currently free HBM (the buffer is reused, so only a
+            // growth needs the headroom)
+            uint64_t P = std::min<uint64_t>((uint64_t)A.n_items * chunk, c->wf_paths);
+            size_t freeb = 0, totalb = 0;
+            if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+                const uint64_t cap = (uint64_t)((freeb + c->wf_bytes) * 0.4) / cr::wf_bytes_per_path(p->k);
+                P = std::max<uint64_t>(std::min<uint64_t>(P, cap), std::min<uint64_t>(P, 1u << 20));
+            }
             const size_t f4 = 16 * (size_t)P;
             const size_t need = (4 + 1 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 8 * (size_t)P +
                                 cr::WF_CNT * sizeof(uint32_t) + 4096;
@@ -520,10 +530,10 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     const int64_t nvar = std::max(cr::num_persistent_variants(), cr::num_wf_variants());
     if (!std::strcmp(key, "kernel") && (v == 0 || v == 1 || v == 2)) c->kernel = (int)v;
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
-    else if (!std::strcmp(key, "variant") && v >= 0 && v < nvar) c->variant = (int)v; // clamped per kernel
+    else if (!std::strcmp(key, "variant") && v >= -1 && v < nvar) c->variant = (int)v; // -1 default; clamped per kernel
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
-    else if (!std::strcmp(key, "refill") && v >= 1 && v <= 64) c->refill = (uint32_t)v;
+    else if (!std::strcmp(key, "refill") && v >= 0 && v <= 64) c->refill = (uint32_t)v; // 0: per-kernel default
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
     return CR_OK;

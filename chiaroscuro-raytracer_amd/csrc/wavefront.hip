@@ -26,7 +26,32 @@
 
 namespace cr {
 
-enum : uint32_t { NO_SLOT = 0xffffffffu };
+enum : uint32_t { NO_SLOT = 0xffffffffu, NO_PATH = 0xffffffffu };
+
+// Block-aggregated append (call with the whole block, uniformly): one global
+// atomicAdd per block instead of one per wave -- same-address atomics from
+// every wave of the grid serialise in one L2 slice.  Slots keep lane order
+// within a wave and wave order within the block.
+__device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, uint32_t *lds /* [5] */) {
+    const uint64_t m = __ballot(pred);
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (lane == 0) lds[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (uint32_t w = 0; w < (blockDim.x >> 6); w++) {
+            const uint32_t c = lds[w];
+            lds[w] = s;
+            s += c;
+        }
+        lds[4] = s ? atomicAdd(counter, s) : 0u;
+    }
+    __syncthreads();
+    const uint32_t slot = lds[4] + lds[wave] +
+                          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    __syncthreads(); // lds reused by the next call
+    return slot;
+}
 
 __device__ __forceinline__ uint32_t *cnt_closest(const WfArgs &W, uint32_t g) { return W.cnt + g; }
 __device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 64 + g; }
@@ -71,18 +96,23 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
             s = A.s0 + (w - item * A.s_count);
             valid = item_pixel(A, item, px, py); // partial-tile pixels outside the image: no path
         }
-        const uint32_t i = wave_append(cnt_closest(W, 1), valid);
         tally(tl, T_PATHS, valid);
+        // ray p of generation 1 is path p's camera ray (no compaction: the few
+        // partial-tile paths get a dead ray, path = NO_PATH)
         if (valid) { // rayTracer.cpp:58-62: jittered camera ray of sample s
             Rng rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
             const f3 d = camera_dir(A, px, py, rng);
             PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), 1u);
             PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key);
             PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
-            W.ray[1][2 * (size_t)i] = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(p));
-            W.ray[1][2 * (size_t)i + 1] = pk(d, 0u);
+            W.ray[1][2 * (size_t)p] = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(p));
+            W.ray[1][2 * (size_t)p + 1] = pk(d, 0u);
+        } else if (p < W.P) {
+            W.ray[1][2 * (size_t)p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(NO_PATH));
+            W.ray[1][2 * (size_t)p + 1] = make_float4(0.f, 0.f, 1.f, 0.f);
         }
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_closest(W, 1) = W.P;
     flush_tallies(A, tl);
 }
 
@@ -99,7 +129,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     uint32_t *work = SHADOW ? work_shadow(W, g) : work_closest(W, g);
     const float4 *rays = SHADOW ? W.sray : W.ray[g & 1];
     Ctr c = {};
-    uint32_t state = ST_NEED_WORK, idx = 0, exclude = 0;
+    uint32_t state = ST_NEED_WORK, idx = 0, exclude = 0, issued = 0;
     f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
     const uint32_t busy_st = SHADOW ? ST_SHADOW : ST_CLOSEST;
@@ -123,7 +153,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         o = ld3(r0);
                         d = ld3(r1);
                         if (SHADOW) exclude = W.sexcl[idx];
-                        if (trav_begin(S, o, d, SHADOW, r1.w, T)) {
+                        if (!SHADOW && __float_as_uint(r0.w) == NO_PATH) {
+                            W.hit[idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
+                        } else if (issued++, trav_begin(S, o, d, SHADOW, r1.w, T)) {
                             state = busy_st;
                         } else if (SHADOW) {
                             W.occ[idx] = 0u; // culled: visible (kdtree.cpp:285-287)
@@ -150,8 +182,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             }
         }
     }
-    if (FULL) flush_counters(A.counters, c, 0u);
-    if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(&A.counters[SHADOW ? T_SHADOW : T_CLOSEST], n);
+    if (SHADOW) c.shadow = issued; // queries, box-culled ones included
+    else c.closest = issued;
+    flush_counters(A.counters, c, 0u);
 }
 
 // ----------------------------------------------------------------- shade --
@@ -159,6 +192,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
 // closest ray of generation g; misses finish their path with the background.
 __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
+    __shared__ uint32_t app[5];
     if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
     __syncthreads();
     const DevScene &S = A.S;
@@ -180,7 +214,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
         float sdist = 0.f;
         uint32_t slight = 0;
         if (in && !hit) {
-            finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
+            if (p != NO_PATH) finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
         } else if (hit) {
             const uint32_t k = __float_as_uint(PS(W, 0, p).w);
             const HitShade hs = shade_hit(S, ld3(r0), h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
@@ -204,7 +238,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
             if (!nee) PS(W, 3, p) = pk(contrib, NO_SLOT);
             else PS(W, 3, p) = pk(contrib, 0u); // slot set below
         }
-        const uint32_t j = wave_append(cnt_shadow(W, g), nee);
+        const uint32_t j = block_append(cnt_shadow(W, g), nee, app);
         if (nee) {
             PS(W, 3, p).w = __uint_as_float(j);
             W.sray[2 * (size_t)j] = pk(sorg, p);
@@ -222,6 +256,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
 // (rayTracer.cpp:100-134): either the next closest ray of generation g + 1 or
 // the end of the path.
 __global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_t g) {
+    __shared__ uint32_t app[5];
     const uint32_t n = *cnt_closest(W, g);
     const float4 *rays = W.ray[g & 1];
     float4 *next_rays = W.ray[(g + 1) & 1];
@@ -262,7 +297,7 @@ __global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_
                 }
             }
         }
-        const uint32_t j = wave_append(cnt_closest(W, g + 1), cont);
+        const uint32_t j = block_append(cnt_closest(W, g + 1), cont, app);
         if (cont) {
             next_rays[2 * (size_t)j] = pk(org, p);
             next_rays[2 * (size_t)j + 1] = pk(wi, 0u);

@@ -16,8 +16,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="sponza")
     ap.add_argument("--spp", type=int, default=8)
-    ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--refill", type=int, default=16)
+    ap.add_argument("--kernel", type=int, default=2)
+    ap.add_argument("--variant", type=int, default=-1)
+    ap.add_argument("--refill", type=int, default=0)
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -32,6 +33,7 @@ def main():
     cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], i["xres"], i["yres"])
     frame = torch.zeros((i["yres"], i["xres"], 3), dtype=torch.float32, device="cuda")
     dev.set_option("counters", 1)
+    dev.set_option("kernel", args.kernel)
     dev.set_option("variant", args.variant)
     dev.set_option("refill", args.refill)
     p = ca.render_params(i["xres"], i["yres"], args.spp, i["k"], i["seed"])

@@ -2,10 +2,14 @@
 
     python scripts/prof_summary.py gpurun_out/prof_r01 r01 [--config sponza]
 
+The profiled command is bench.py: `warmup + steps` timed render passes plus ONE
+counting pass (the FULL-counter trace build), each pass ending with one
+sum_samples dispatch.  A render pass is the unit of `roofline` in bench.py.
+
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
-  profiles/<tag>_pmc.json           per-kernel PMC averages per dispatch + derived figures
-  profiles/pmc_<config>.json        fabric bytes per launch of the timed render kernel,
+  profiles/<tag>_pmc.json           per-kernel PMC sums / averages + per-pass totals
+  profiles/pmc_<config>.json        fabric bytes per render pass (timed kernels only),
                                     read by bench.py for roofline.traffic
 Derived (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are KiB of
 L2 memory-side requests; gfx950 tallies 128-B read requests at 64 B, so reads
@@ -22,12 +26,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def pmc(dirpath):
-    out = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in Path(dirpath).glob("*/pmc_counter_collection.csv"):
-        for r in csv.DictReader(open(f)):
-            out[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in out.items()}
+def is_counting(name: str) -> bool:
+    return ", true, " in name and "wf_trace" in name or "render_dynamic<8, true" in name
 
 
 def main():
@@ -37,40 +37,54 @@ def main():
     prof.mkdir(exist_ok=True)
     stats = next(src.glob("trace/*kernel_stats.csv"))
     shutil.copy(stats, prof / ("%s_kernel_stats.csv" % tag))
-    rows = list(csv.DictReader(open(stats)))
-    durations = {r["Name"]: float(r["AverageNs"]) for r in rows}
-    counters = pmc(src)
-    summary = {}
-    for name, c in counters.items():
-        if "render_" not in name and "sum_samples" not in name:
+    rows = {r["Name"]: r for r in csv.DictReader(open(stats))}
+    passes = int(rows[next(n for n in rows if "sum_samples" in n)]["Calls"])  # timed + counting passes
+    # PMC: sum per kernel over its dispatches (one pass per counter group)
+    sums = collections.defaultdict(lambda: collections.defaultdict(float))
+    for f in src.glob("*/pmc_counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            sums[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    summary, per_pass = {}, collections.defaultdict(float)
+    for name, r in rows.items():
+        if not any(k in name for k in ("render_", "wf_", "sum_samples")):
             continue
-        e = dict(c)
+        counting = is_counting(name)
+        frames = 1 if counting else (passes - 1 if "wf_trace" in name or "render_dynamic" in name else passes)
+        e = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "total_ns": float(r["TotalDurationNs"]),
+             "counting_build": counting, "passes": frames}
+        c = sums.get(name, {})
+        e.update({k: v for k, v in c.items()})
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            e["fabric_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+            e["fabric_bytes_total"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
             e["l2_hit_rate"] = c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1.0)
         if "SQ_WAVE_CYCLES" in c:
             w = c["SQ_WAVE_CYCLES"]
             e["wave_time_split"] = {k: c.get(k, 0.0) / w for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY",
                                                                    "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU")}
-        d = durations.get(name)
-        if d:
-            e["avg_duration_ns"] = d
-            if "fabric_bytes_per_launch" in e:
-                e["fabric_GBps"] = e["fabric_bytes_per_launch"] / d
         summary[name] = e
-    (prof / ("%s_pmc.json" % tag)).write_text(json.dumps(summary, indent=1, sort_keys=True))
-    timed = [n for n in summary if "render_dynamic" in n and "true, true, 1" not in n]
-    if timed:
-        t = summary[timed[0]]
-        (prof / ("pmc_%s.json" % config)).write_text(json.dumps({
-            "kernel": timed[0], "source": "profiles/%s_pmc.json" % tag,
-            "hbm_bytes_per_launch": t.get("fabric_bytes_per_launch"),
-            "note": "2*FETCH_SIZE+WRITE_SIZE (KiB) per dispatch; includes Infinity-Cache hits (upper bound on HBM)",
-        }, indent=1))
+        if not counting:
+            per_pass["duration_ns"] += e["total_ns"] / frames
+            if "fabric_bytes_total" in e:
+                per_pass["fabric_bytes"] += e["fabric_bytes_total"] / frames
+            for k in ("SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "TCC_HIT_sum", "TCC_MISS_sum"):
+                if k in c:
+                    per_pass[k] += c[k] / frames
+    per_pass["fabric_GBps"] = per_pass["fabric_bytes"] / max(per_pass["duration_ns"], 1.0)
+    out = {"render_pass": dict(per_pass), "kernels": summary, "passes_profiled": passes}
+    (prof / ("%s_pmc.json" % tag)).write_text(json.dumps(out, indent=1, sort_keys=True))
+    spp = int(sys.argv[sys.argv.index("--spp") + 1]) if "--spp" in sys.argv else 128
+    (prof / ("pmc_%s.json" % config)).write_text(json.dumps({
+        "source": "profiles/%s_pmc.json" % tag, "spp": spp, "n_gpus": 1,
+        "hbm_bytes_per_launch": per_pass["fabric_bytes"],
+        "unit": "one render pass (all timed kernels of one layer)",
+        "note": "2*FETCH_SIZE+WRITE_SIZE (KiB) summed over the pass's dispatches; includes Infinity-Cache hits "
+                "(upper bound on HBM bytes)",
+    }, indent=1))
+    print(json.dumps(out["render_pass"], indent=1))
     for n, e in summary.items():
-        print(n[:70], {k: (round(v, 4) if isinstance(v, float) else v) for k, v in e.items()
-                       if k in ("avg_duration_ns", "fabric_bytes_per_launch", "fabric_GBps", "l2_hit_rate")})
+        print("%-70s calls %3d avg %10.3f ms%s" % (n[:70], e["calls"], e["avg_ns"] / 1e6,
+                                                   "  (counting)" if e["counting_build"] else ""))
 
 
 if __name__ == "__main__":

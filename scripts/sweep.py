@@ -27,10 +27,10 @@ def main():
     ap.add_argument("--config", default="sponza")
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--kernel", default="0", help="0 persistent megakernel, 2 wavefront")
-    ap.add_argument("--variants", default="0")
+    ap.add_argument("--kernel", default="2", help="0 persistent megakernel, 2 wavefront (default)")
+    ap.add_argument("--variants", default="-1", help="-1 = the kernel's default build")
     ap.add_argument("--waves", default="0", help="waves_per_cu (persistent kernel; 0 = default)")
-    ap.add_argument("--refill", default="16", help="refill thresholds")
+    ap.add_argument("--refill", default="0", help="refill thresholds (0 = the kernel's default)")
     ap.add_argument("--wf-paths", default="0", help="wavefront paths per chunk (0 = default)")
     args = ap.parse_args()
     import torch
@@ -59,7 +59,7 @@ def main():
             dev.set_option("variant", v)
             dev.set_option("waves_per_cu", w)
             dev.set_option("refill", f)
-            dev.set_option("wf_paths", wp or (16 << 20))
+            dev.set_option("wf_paths", wp or (256 << 20))
             p = ca.render_params(xres, yres, args.spp, k, seed, layer=1)
             dev.render_device(cam, p, frame.data_ptr(), stream)
             torch.cuda.synchronize()
