@@ -35,14 +35,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(pair_tris, info, leaf, cam, xres, yres, spp, k, seed, budget_s):
+def cpu_baseline(pair_tris, textures, info, leaf, cam, xres, yres, spp, k, seed, budget_s):
     """Oracle restatement (OpenMP over rows, dynamic schedule) on a row sample."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle as po
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     t0 = time.time()
-    osc = po.OracleScene(pair_tris, leaf_size=leaf, build_threads=threads)
+    osc = po.OracleScene(pair_tris, leaf_size=leaf, textures=textures, build_threads=threads)
     log("cpu_baseline: oracle kd build %.1fs" % (time.time() - t0))
     # calibrate on every 8th row at 1 spp, then size (rows, spp) to ~budget_s
     step = 8
@@ -199,7 +199,8 @@ def main():
             args.kernel if args.kernel >= 0 else 2]
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(model.triangles(), info, info["leaf_size"], cam.as_array(), xres, yres, spp, k, seed,
+            cpu = cpu_baseline(model.triangles(), model.textures(), info, info["leaf_size"], cam.as_array(), xres,
+                               yres, spp, k, seed,
                                args.cpu_budget)
         label = {"sponza": "sponza_standin (Sponza-Crytek stand-in, ~261k tris) 1920x1080",
                  "sponza_4k": "sponza_standin (Sponza-Crytek stand-in) 3840x2160",

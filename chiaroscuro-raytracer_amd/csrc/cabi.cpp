@@ -44,6 +44,7 @@ struct cr_ctx {
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
     uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 48 wavefront)
+    uint32_t refill_shadow = 0; // wavefront shadow trace; 0: same as refill
     uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
 };
 
@@ -135,7 +136,9 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.counters = c->d_counters;
     A.work = c->d_work;
     A.full_counters = c->full_counters;
-    A.refill = c->refill ? c->refill : (c->kernel == 2 ? 48u : 16u);
+    // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783)
+    A.refill = c->refill ? c->refill : (c->kernel == 2 ? 56u : 16u);
+    A.refill_shadow = c->refill_shadow ? c->refill_shadow : (c->refill ? c->refill : 48u);
     A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 1 : 0);
 }
 
@@ -534,6 +537,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
     else if (!std::strcmp(key, "refill") && v >= 0 && v <= 64) c->refill = (uint32_t)v; // 0: per-kernel default
+    else if (!std::strcmp(key, "refill_shadow") && v >= 0 && v <= 64) c->refill_shadow = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
     return CR_OK;

@@ -53,7 +53,8 @@ struct RenderArgs {
     uint32_t gstride;             // threads in the persistent grid
     int full_counters;            // 1: also count inner/leaf/tritest (SURVEY §8d bytes)
     int variant;                  // persistent-kernel variant index (kernels.hip kVariants)
-    uint32_t refill;              // idle lanes of a wave that trigger a path-state step
+    uint32_t refill;              // idle lanes of a wave that trigger a path-state step / ray fetch
+    uint32_t refill_shadow;       // wavefront shadow-trace kernel's threshold
     // (pixel, sample) work items of one launch: samples [s0, s0 + s_count) of
     // every item, w = item * s_count + (s - s0), n_work = n_items * s_count
     uint32_t s0, s_count, n_work;

@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     const uint32_t busy_st = SHADOW ? ST_SHADOW : ST_CLOSEST;
     for (;;) {
         const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
-        if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= A.refill)) {
+        if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= (SHADOW ? A.refill_shadow : A.refill))) {
             for (;;) { // refill; a ray culled by the root box is answered at once and refetched
                 const uint64_t m = __ballot(state == ST_NEED_WORK);
                 if (!m) break;

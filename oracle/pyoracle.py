@@ -97,6 +97,9 @@ class OracleScene:
             data = np.ascontiguousarray(data, np.uint8)
             self._tex.append(data)
             L.or_scene_add_texture(self.h, w, h, nc, _p(data, C.c_uint8))
+        tex = np.asarray(t["tex"])
+        if len(tex) and int(tex.max()) >= len(self._tex):
+            raise ValueError("triangle texture index %d but %d textures given" % (int(tex.max()), len(self._tex)))
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

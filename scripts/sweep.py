@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--waves", default="0", help="waves_per_cu (persistent kernel; 0 = default)")
     ap.add_argument("--refill", default="0", help="refill thresholds (0 = the kernel's default)")
     ap.add_argument("--wf-paths", default="0", help="wavefront paths per chunk (0 = default)")
+    ap.add_argument("--refill-shadow", default="0", help="wavefront shadow-trace thresholds (0 = refill)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -49,16 +50,17 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     dev.set_option("counters", 0)
     configs = list(itertools.product(ints(args.kernel), ints(args.variants), ints(args.waves), ints(args.refill),
-                                     ints(args.wf_paths)))
+                                     ints(args.wf_paths), ints(args.refill_shadow)))
     res = {}
     ref = None
     for r in range(args.rounds):
         for cfg in configs:
-            kern, v, w, f, wp = cfg
+            kern, v, w, f, wp, fs = cfg
             dev.set_option("kernel", kern)
             dev.set_option("variant", v)
             dev.set_option("waves_per_cu", w)
             dev.set_option("refill", f)
+            dev.set_option("refill_shadow", fs)
             dev.set_option("wf_paths", wp or (256 << 20))
             p = ca.render_params(xres, yres, args.spp, k, seed, layer=1)
             dev.render_device(cam, p, frame.data_ptr(), stream)
@@ -74,8 +76,9 @@ def main():
         ms = [x[0] for x in xs]
         rays = xs[0][1]
         med = statistics.median(ms)
-        kern, v, w, f, wp = cfg
-        print(json.dumps({"kernel": kern, "variant": v, "waves_per_cu": w, "refill": f, "wf_paths": wp,
+        kern, v, w, f, wp, fs = cfg
+        print(json.dumps({"kernel": kern, "variant": v, "waves_per_cu": w, "refill": f, "refill_shadow": fs,
+                          "wf_paths": wp,
                           "median_ms": round(med, 2), "min_ms": round(min(ms), 2),
                           "mray_s": round(rays / med / 1e3, 1)}), flush=True)
 

@@ -99,7 +99,8 @@ def test_host_kdtree_equals_oracle(ca, po, scenes, config):
     sc = ca.Scene(scenes.config_rtc(config))
     m = ca.Model(sc)
     host = ca.KDTree(m, sc).export()
-    orc = po.OracleScene(m.triangles(), leaf_size=sc.info["leaf_size"], build_threads=8).kd_export()
+    orc = po.OracleScene(m.triangles(), leaf_size=sc.info["leaf_size"], textures=m.textures(),
+                         build_threads=8).kd_export()
     if config == "nanobox":
         assert len(m.textures()) == 4 and (m.triangles()["tex"] >= 0).sum() > 20000
     for k in ("is_leaf", "axis", "child", "leaf_first", "leaf_count", "refs"):
