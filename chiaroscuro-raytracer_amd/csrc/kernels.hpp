@@ -97,13 +97,28 @@ struct WfArgs {
     float4 *dw;       // [2K][P] (direct, w) per bounce
     uint2 *gstack;    // trace kernels' stack overflow [depth][gstride]
     uint32_t gstride; // threads of the trace grid
+    // queue ordering (raysort.hip): shade / bounce write a sort key and the slot
+    // per appended ray into key[0] / perm[0]; the host sorts them and hands the
+    // trace kernel the permutation (`order`, null = queue order)
+    uint32_t *key[2], *perm[2];
+    const uint32_t *order;
+    void *sort_tmp;
+    size_t sort_tmp_bytes;
+    int sort;         // 1: write keys and sort the queues of large generations
+    int key_bits;     // significant key bits
+    uint32_t sort_min;   // queues shorter than this are traced in append order
+    uint32_t sort_tile;  // log2 of the pixel sub-tile edge of the key (3: 8x8 pixels)
+    uint32_t dir_res;    // octahedral direction bins per axis (8: 64 bins; power of two)
 };
 // rays 2x2 float4, hit 1, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs
-inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 1 + 2 + WF_STATE + 2 * K) * 16 + 8; }
+inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 1 + 2 + WF_STATE + 2 * K) * 16 + 8 + 16; } // + sort
 int num_wf_variants();
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
 // One chunk: camera generation + K x (closest, shade, shadow, bounce).
 int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st);
+int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
+               hipStream_t st);
+size_t wf_sort_tmp_bytes(uint32_t n, int key_bits);
 // Persistent grid geometry chosen by launch_render (block threads, blocks).
 void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);
 

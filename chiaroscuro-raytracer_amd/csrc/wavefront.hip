@@ -58,6 +58,34 @@ __device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { r
 __device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 128 + g; }
 __device__ __forceinline__ uint32_t *work_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 192 + g; }
 
+// Queue sort key (raysort.hip): 8x8-pixel sub-tile of the path's pixel, then an
+// 8x8 octahedral direction bin.  Any deterministic key is exact -- it only
+// orders the work.
+__device__ __forceinline__ uint32_t dir_bin(f3 d, uint32_t res) {
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    if (!(s > 0.f)) return 0u;
+    float u = d.x / s, v = d.z / s;
+    if (d.y < 0.f) {
+        const float uu = (1.f - fabsf(v)) * (u >= 0.f ? 1.f : -1.f), vv = (1.f - fabsf(u)) * (v >= 0.f ? 1.f : -1.f);
+        u = uu;
+        v = vv;
+    }
+    const float h = 0.5f * (float)res;
+    const uint32_t bu = (uint32_t)min((int)res - 1, max(0, (int)((u + 1.f) * h)));
+    const uint32_t bv = (uint32_t)min((int)res - 1, max(0, (int)((v + 1.f) * h)));
+    // Morton order: consecutive keys stay close in direction along both axes
+    uint32_t m = 0;
+    for (uint32_t b = 0; (1u << b) < res; b++) m |= ((bu >> b) & 1u) << (2 * b + 1) | ((bv >> b) & 1u) << (2 * b);
+    return m;
+}
+__device__ __forceinline__ uint32_t sort_key(const RenderArgs &A, const WfArgs &W, uint32_t p, f3 dir) {
+    const uint32_t item = (W.w0 + p) / A.s_count;
+    const uint32_t T = A.tile, TT = T * T, lt = item / TT, o = item - lt * TT, sh = W.sort_tile;
+    const uint32_t S = (T + (1u << sh) - 1) >> sh;
+    const uint32_t sub = ((o / T) >> sh) * S + ((o % T) >> sh);
+    return (lt * S * S + sub) * (W.dir_res * W.dir_res) + dir_bin(dir, W.dir_res);
+}
+
 __device__ __forceinline__ void flush_tallies(const RenderArgs &A, unsigned long long *tl) {
     __syncthreads();
     if (threadIdx.x < T_N && tl[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], tl[threadIdx.x]);
@@ -149,6 +177,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                     if (idx >= n) {
                         state = ST_DONE;
                     } else {
+                        if (W.order) idx = W.order[idx]; // sorted queue: results still go to slot idx
                         const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
                         o = ld3(r0);
                         d = ld3(r1);
@@ -244,6 +273,10 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
             W.sray[2 * (size_t)j] = pk(sorg, p);
             W.sray[2 * (size_t)j + 1] = make_float4(sdir.x, sdir.y, sdir.z, sdist);
             W.sexcl[j] = slight;
+            if (W.sort) {
+                W.key[0][j] = sort_key(A, W, p, sdir);
+                W.perm[0][j] = j;
+            }
         }
         tally(tl, T_HIT, hit);
         tally(tl, T_TEXHIT, textured);
@@ -301,6 +334,10 @@ __global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_
         if (cont) {
             next_rays[2 * (size_t)j] = pk(org, p);
             next_rays[2 * (size_t)j + 1] = pk(wi, 0u);
+            if (W.sort) {
+                W.key[0][j] = sort_key(A, W, p, wi);
+                W.perm[0][j] = j;
+            }
         }
     }
 }
@@ -323,21 +360,53 @@ void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &bloc
     blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)v.waves_per_simd; // 4 SIMDs, 4 waves/block
 }
 
-int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st) {
+// Sorts the queue whose keys the previous kernel wrote; returns the permutation
+// for the trace kernel (nullptr: trace in queue order).
+static const uint32_t *order_queue(const WfArgs &W, const uint32_t *dcount, hipStream_t st, int &err) {
+    if (!W.sort) return nullptr;
+    uint32_t n = 0;
+    if ((err = (int)hipMemcpyAsync(&n, dcount, sizeof(n), hipMemcpyDeviceToHost, st)) ||
+        (err = (int)hipStreamSynchronize(st)))
+        return nullptr;
+    if (n < W.sort_min) return nullptr;
+    uint32_t *keys[2] = {W.key[0], W.key[1]}, *vals[2] = {W.perm[0], W.perm[1]};
+    size_t tb = W.sort_tmp_bytes;
+    const int sel = sort_queue(keys, vals, n, W.key_bits, W.sort_tmp, tb, st);
+    if (sel < 0) {
+        err = (int)hipErrorUnknown;
+        return nullptr;
+    }
+    return vals[sel];
+}
+
+int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st) {
+    WfArgs W = W0;
     const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     if (W.gstride < blk * blocks) return (int)hipErrorInvalidValue;
     const size_t lds = (size_t)v.ring * blk * sizeof(uint2);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
+    int err = 0;
+    W.order = nullptr; // generation-1 closest rays: path order is already coherent (camera rays)
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
-    for (uint32_t g = 1; g <= (uint32_t)A.K; g++) {
+    for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
         hipLaunchKernelGGL(v.closest, dim3(blocks), dim3(blk), lds, st, A, W, g);
         hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        W.order = order_queue(W, W.cnt + 64 + g, st, err);
         hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
         hipLaunchKernelGGL(wf_bounce, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        if (g < (uint32_t)A.K) W.order = order_queue(W, W.cnt + g + 1, st, err);
     }
-    return (int)hipGetLastError();
+    return err ? err : (int)hipGetLastError();
+}
+
+// Bytes of sort workspace for queues of up to n rays (temp storage only).
+size_t wf_sort_tmp_bytes(uint32_t n, int key_bits) {
+    size_t tb = 0;
+    uint32_t *k[2] = {nullptr, nullptr}, *v[2] = {nullptr, nullptr};
+    sort_queue(k, v, n, key_bits, nullptr, tb, nullptr);
+    return tb;
 }
 
 } // namespace cr

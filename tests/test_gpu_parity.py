@@ -36,6 +36,25 @@ def nanobox(ca, po, scenes):
     return Pair(ca, po, scenes.config_rtc("nanobox"))
 
 
+@pytest.mark.parametrize("tile_dir", [(3, 8), (1, 2), (5, 32)])
+def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
+    """Queue sorting reorders the trace work only: force it on every queue (the
+    default sorts queues of >= 1M rays) with several key layouts."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_sort_min", 0)
+        pair.dev.set_option("wf_sort_tile", tile_dir[0])
+        pair.dev.set_option("wf_dir_res", tile_dir[1])
+        try:
+            g, gc, o, oc = _render_both(ca, pair, x, y, s)
+        finally:
+            pair.dev.set_option("wf_sort_min", 1 << 20)
+            pair.dev.set_option("wf_sort_tile", 4)
+            pair.dev.set_option("wf_dir_res", 32)
+        assert_bitwise(g, o, "sorted wavefront %dx%dx%d" % (x, y, s))
+        assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
 @pytest.mark.parametrize("kernel", [0, 1, 2])
 def test_nanobox_textured_bitexact(ca, nanobox, kernel):
     """C3 stand-in: RGB / RGBA / 1-channel textures, wrapped UVs, UV == 1 seams,
