@@ -45,6 +45,7 @@ struct cr_ctx {
     uint32_t waves_per_cu = 0;
     uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 48 wavefront)
     uint32_t refill_shadow = 0; // wavefront shadow trace; 0: same as refill
+    uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: same as refill
     uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
     int wf_sort = 1;                // wavefront: sort large shadow / secondary queues for coherence
     uint32_t wf_sort_min = 1u << 20; // ... of at least this many rays
@@ -145,7 +146,11 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783)
     A.refill = c->refill ? c->refill : (c->kernel == 2 ? 56u : 16u);
     A.refill_shadow = c->refill_shadow ? c->refill_shadow : (c->refill ? c->refill : 48u);
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 1 : 0);
+    // camera rays (64 samples of one pixel per wave): lock-step is best, 64 -> 933 vs 56 -> 924 Mray/s
+    A.refill_camera = c->refill_camera ? c->refill_camera : (c->refill ? c->refill : (c->kernel == 2 ? 64u : 16u));
+    // wavefront trace builds (wavefront.hip kWf): 2 = LDS ring 8, 8 waves/SIMD, scalar loads for
+    // wave-uniform nodes / leaves: 1003 vs 935 Mray/s for the same build without them (variant 1)
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 2 : 0);
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -564,6 +569,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
     else if (!std::strcmp(key, "refill") && v >= 0 && v <= 64) c->refill = (uint32_t)v; // 0: per-kernel default
     else if (!std::strcmp(key, "refill_shadow") && v >= 0 && v <= 64) c->refill_shadow = (uint32_t)v;
+    else if (!std::strcmp(key, "refill_camera") && v >= 0 && v <= 64) c->refill_camera = (uint32_t)v;
     else if (!std::strcmp(key, "wf_sort") && (v == 0 || v == 1)) c->wf_sort = (int)v;
     else if (!std::strcmp(key, "wf_sort_min") && v >= 0 && v <= (1ll << 31)) c->wf_sort_min = (uint32_t)v;
     else if (!std::strcmp(key, "wf_sort_tile") && v >= 0 && v <= 5) c->wf_sort_tile = (uint32_t)v;

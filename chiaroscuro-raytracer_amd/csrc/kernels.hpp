@@ -55,6 +55,7 @@ struct RenderArgs {
     int variant;                  // persistent-kernel variant index (kernels.hip kVariants)
     uint32_t refill;              // idle lanes of a wave that trigger a path-state step / ray fetch
     uint32_t refill_shadow;       // wavefront shadow-trace kernel's threshold
+    uint32_t refill_camera;       // wavefront closest trace of generation 1 (camera rays)
     // (pixel, sample) work items of one launch: samples [s0, s0 + s_count) of
     // every item, w = item * s_count + (s - s0), n_work = n_items * s_count
     uint32_t s0, s_count, n_work;

@@ -57,12 +57,38 @@ __device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool s
 // (Speculative descent -- lanes that reached their leaf early descending toward
 // the next one, Aila & Laine's postponed leaves -- is exact here too but
 // measured slower: the merged descent loop costs more than the idle lanes.)
-template <int R, bool FULL, bool PF, bool FD>
+// Scalar-memory loads for wave-uniform addresses (SC builds): when every active
+// lane wants the same node / leaf, one s_load serves the wave and the vector
+// memory address path -- the measured bottleneck -- is not used at all.  The
+// data is read-only for the whole launch, so the scalar cache is coherent.
+typedef unsigned int cr_v2u __attribute__((ext_vector_type(2)));
+typedef float cr_v4f __attribute__((ext_vector_type(4)));
+typedef float cr_v8f __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint2 sload_node(const uint2 *p) {
+    cr_v2u r;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
+    return make_uint2(r.x, r.y);
+}
+__device__ __forceinline__ TriRec sload_rec(const float4 *p) {
+    cr_v8f a;
+    cr_v4f b;
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(a), "=s"(b)
+                 : "s"(p));
+    return TriRec{make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]),
+                  make_float4(b[0], b[1], b[2], b[3])};
+}
+template <bool SC> __device__ __forceinline__ uint2 load_node(const DevScene &S, uint32_t node) {
+    if (SC && wave_uniform(node)) return sload_node(S.nodes + __builtin_amdgcn_readfirstlane(node));
+    return S.nodes[node];
+}
+
+template <int R, bool FULL, bool PF, bool FD, bool SC = false>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c) {
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
-    uint2 nd = S.nodes[T.node];
+    uint2 nd = load_node<SC>(S, T.node);
     while ((nd.y & 3u) != 3u) {
         if (FULL) {
             c.inner++;
@@ -92,7 +118,7 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             T.node = child + (1u - below);
             T.tmax = tsplit;
         }
-        nd = S.nodes[T.node];
+        nd = load_node<SC>(S, T.node);
     }
     if (FULL) {
         c.leaf++;
@@ -102,37 +128,53 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
     bool found = false, occluded = false;
     uint32_t tri = 0;
     float bx = 0.f, by = 0.f;
-    TriRec nx;
-    if (PF && count) nx = load_rec(S, first);
-    for (uint32_t j = 0; j < count; j++) {
-        if (FULL) {
-            const bool uni = wave_uniform(first + j);
-            if (wave_leader()) {
-                c.wave_tri++;
-                c.wave_tri_uniform += uni;
-            }
-        }
-        TriRec r;
-        if (PF) { // software pipeline: issue triangle j+1's loads before testing j
-            r = nx;
-            if (j + 1 < count) nx = load_rec(S, first + j + 1);
-        } else {
-            r = load_rec(S, first + j);
-        }
+    // one triangle of the leaf (kdtree.cpp:235-246 / 309-320); false: stop the leaf
+    auto test = [&](const TriRec &r) -> bool {
         const uint32_t id = rec_id(r);
-        if (shadow && id == exclude) continue;
+        if (shadow && id == exclude) return true;
         if (FULL) c.tritest++;
         float ux, uy, t;
         if (tri_test(o, d, r, T.tmax, ux, uy, t)) {
             if (shadow) {
                 occluded = true;
-                break;
+                return false;
             }
             bx = ux;
             by = uy;
             T.tmax = t;
             tri = id;
             found = true;
+        }
+        return true;
+    };
+    auto tally_tri = [&](uint32_t ref) {
+        if (FULL) {
+            const bool uni = wave_uniform(ref);
+            if (wave_leader()) {
+                c.wave_tri++;
+                c.wave_tri_uniform += uni;
+            }
+        }
+    };
+    if (SC && wave_uniform(first)) { // every lane at the same leaf: scalar loads
+        const float4 *base = S.recs + (size_t)REC_STRIDE * __builtin_amdgcn_readfirstlane(first);
+        for (uint32_t j = 0; j < count; j++) {
+            tally_tri(first + j);
+            if (!test(sload_rec(base + (size_t)REC_STRIDE * j))) break;
+        }
+    } else {
+        TriRec nx;
+        if (PF && count) nx = load_rec(S, first);
+        for (uint32_t j = 0; j < count; j++) {
+            tally_tri(first + j);
+            TriRec r;
+            if (PF) { // software pipeline: issue triangle j+1's loads before testing j
+                r = nx;
+                if (j + 1 < count) nx = load_rec(S, first + j + 1);
+            } else {
+                r = load_rec(S, first + j);
+            }
+            if (!test(r)) break;
         }
     }
     if (occluded) return ST_OCCLUDED;

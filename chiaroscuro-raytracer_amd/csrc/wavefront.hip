@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // Persistent: every lane runs one query at a time through trav_round; when
 // `A.refill` lanes of a wave have finished (or none is busy) they take the
 // next rays of the queue (one atomicAdd per wave).
-template <bool SHADOW, bool FULL, int R, int MINW>
+template <bool SHADOW, bool FULL, int R, int MINW, bool SC>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
@@ -161,9 +161,10 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
     const uint32_t busy_st = SHADOW ? ST_SHADOW : ST_CLOSEST;
+    const uint32_t refill = SHADOW ? A.refill_shadow : (g == 1 ? A.refill_camera : A.refill);
     for (;;) {
         const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
-        if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= (SHADOW ? A.refill_shadow : A.refill))) {
+        if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= refill)) {
             for (;;) { // refill; a ray culled by the root box is answered at once and refetched
                 const uint64_t m = __ballot(state == ST_NEED_WORK);
                 if (!m) break;
@@ -200,7 +201,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, true, false>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
+            const uint32_t r = trav_round<R, FULL, true, false, SC>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
                                                                  exclude, T, c);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
@@ -348,9 +349,10 @@ struct WfVariant {
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd;
 };
-#define CR_WF(R, W) {wf_trace<false, false, R, W>, wf_trace<true, false, R, W>, R, W}
-static const WfVariant kWf[] = {CR_WF(4, 8), CR_WF(8, 8), CR_WF(4, 10), CR_WF(4, 12), CR_WF(8, 6)};
-static const WfVariant kWfCount = {wf_trace<false, true, 8, 1>, wf_trace<true, true, 8, 1>, 8, 4};
+#define CR_WF(R, W, SC) {wf_trace<false, false, R, W, SC>, wf_trace<true, false, R, W, SC>, R, W}
+static const WfVariant kWf[] = {CR_WF(4, 8, false), CR_WF(8, 8, false), CR_WF(8, 8, true), CR_WF(8, 6, false),
+                                CR_WF(8, 6, true)};
+static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
 

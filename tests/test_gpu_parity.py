@@ -55,6 +55,20 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
+    """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
+    wave-uniform nodes / leaves) renders the same bits."""
+    sponza.dev.set_option("kernel", 2)
+    sponza.dev.set_option("variant", variant)
+    try:
+        g, gc, o, oc = _render_both(ca, sponza, 80, 45, 4)
+    finally:
+        sponza.dev.set_option("variant", -1)
+    assert_bitwise(g, o, "wavefront variant %d" % variant)
+    assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
 @pytest.mark.parametrize("kernel", [0, 1, 2])
 def test_nanobox_textured_bitexact(ca, nanobox, kernel):
     """C3 stand-in: RGB / RGBA / 1-channel textures, wrapped UVs, UV == 1 seams,
