@@ -53,6 +53,8 @@ struct cr_ctx {
     // (16x16, 32x32 Morton) 930; (32x32, 32x32) 914 Mray/s
     uint32_t wf_sort_tile = 4;      // key: log2 pixel sub-tile edge
     uint32_t wf_dir_res = 32;       // key: direction bins per octahedral axis
+    int wf_world_keys = 2;          // key: world-space origins for queues starting at hits of gen >= 2
+    uint32_t wf_world_bits = 6;     // key: Morton bits per axis of the origin
 };
 
 namespace {
@@ -199,6 +201,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             const uint64_t nkeys = (uint64_t)(A.n_items / (T * T)) * sub * sub * c->wf_dir_res * c->wf_dir_res;
             int key_bits = 1;
             while (key_bits < 32 && (1ull << key_bits) < nkeys) key_bits++;
+            const uint64_t nworld = (1ull << (3 * c->wf_world_bits)) * c->wf_dir_res * c->wf_dir_res;
+            while (c->wf_world_keys && key_bits < 32 && (1ull << key_bits) < nworld) key_bits++;
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits) : 0;
             const size_t need = (4 + 1 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 8 * (size_t)P +
                                 (c->wf_sort ? 16 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
@@ -224,6 +228,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             W.sort_min = c->wf_sort_min;
             W.sort_tile = c->wf_sort_tile;
             W.dir_res = c->wf_dir_res;
+            W.world_keys = nworld <= (1ull << 32) ? c->wf_world_keys : 0;
+            W.world_bits = c->wf_world_bits;
             if (c->wf_sort) {
                 for (int i = 0; i < 2; i++) {
                     W.key[i] = (uint32_t *)take(4 * (size_t)P);
@@ -571,6 +577,8 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "refill_shadow") && v >= 0 && v <= 64) c->refill_shadow = (uint32_t)v;
     else if (!std::strcmp(key, "refill_camera") && v >= 0 && v <= 64) c->refill_camera = (uint32_t)v;
     else if (!std::strcmp(key, "wf_sort") && (v == 0 || v == 1)) c->wf_sort = (int)v;
+    else if (!std::strcmp(key, "wf_world_keys") && v >= 0 && v <= 64) c->wf_world_keys = (int)v;
+    else if (!std::strcmp(key, "wf_world_bits") && v >= 1 && v <= 10) c->wf_world_bits = (uint32_t)v;
     else if (!std::strcmp(key, "wf_sort_min") && v >= 0 && v <= (1ll << 31)) c->wf_sort_min = (uint32_t)v;
     else if (!std::strcmp(key, "wf_sort_tile") && v >= 0 && v <= 5) c->wf_sort_tile = (uint32_t)v;
     else if (!std::strcmp(key, "wf_dir_res") && v >= 1 && v <= 256 && (v & (v - 1)) == 0)

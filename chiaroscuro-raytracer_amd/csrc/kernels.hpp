@@ -110,6 +110,9 @@ struct WfArgs {
     uint32_t sort_min;   // queues shorter than this are traced in append order
     uint32_t sort_tile;  // log2 of the pixel sub-tile edge of the key (3: 8x8 pixels)
     uint32_t dir_res;    // octahedral direction bins per axis (8: 64 bins; power of two)
+    int world_keys;      // g > 0: world-space origin keys for queues whose rays start at hits of
+                         // generation >= g (shadow queue g, closest queue g + 1); 0: pixel keys only
+    uint32_t world_bits; // bits per axis of the origin's Morton code
 };
 // rays 2x2 float4, hit 1, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs
 inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 1 + 2 + WF_STATE + 2 * K) * 16 + 8 + 16; } // + sort

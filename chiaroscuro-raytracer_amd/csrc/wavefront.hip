@@ -78,6 +78,21 @@ __device__ __forceinline__ uint32_t dir_bin(f3 d, uint32_t res) {
     for (uint32_t b = 0; (1u << b) < res; b++) m |= ((bu >> b) & 1u) << (2 * b + 1) | ((bv >> b) & 1u) << (2 * b);
     return m;
 }
+// World-space variant for rays whose origins are not tied to their pixel (the
+// shadow rays of bounce >= 2 and the closest rays of bounce >= 3): a 3-D Morton
+// code of the origin in the scene box (WORLD_BITS per axis), then the direction.
+__device__ __forceinline__ uint32_t world_key(const RenderArgs &A, const WfArgs &W, f3 o, f3 dir) {
+    const DevScene &S = A.S;
+    const uint32_t WORLD_BITS = W.world_bits;
+    const float sc = (float)(1u << WORLD_BITS);
+    const uint32_t qx = (uint32_t)min((int)sc - 1, max(0, (int)((o.x - S.bmin.x) / (S.bmax.x - S.bmin.x) * sc)));
+    const uint32_t qy = (uint32_t)min((int)sc - 1, max(0, (int)((o.y - S.bmin.y) / (S.bmax.y - S.bmin.y) * sc)));
+    const uint32_t qz = (uint32_t)min((int)sc - 1, max(0, (int)((o.z - S.bmin.z) / (S.bmax.z - S.bmin.z) * sc)));
+    uint32_t m = 0;
+    for (uint32_t b = 0; b < WORLD_BITS; b++)
+        m |= ((qx >> b) & 1u) << (3 * b + 2) | ((qy >> b) & 1u) << (3 * b + 1) | ((qz >> b) & 1u) << (3 * b);
+    return m * (W.dir_res * W.dir_res) + dir_bin(dir, W.dir_res);
+}
 __device__ __forceinline__ uint32_t sort_key(const RenderArgs &A, const WfArgs &W, uint32_t p, f3 dir) {
     const uint32_t item = (W.w0 + p) / A.s_count;
     const uint32_t T = A.tile, TT = T * T, lt = item / TT, o = item - lt * TT, sh = W.sort_tile;
@@ -275,7 +290,8 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
             W.sray[2 * (size_t)j + 1] = make_float4(sdir.x, sdir.y, sdir.z, sdist);
             W.sexcl[j] = slight;
             if (W.sort) {
-                W.key[0][j] = sort_key(A, W, p, sdir);
+                W.key[0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sorg, sdir)
+                                                                            : sort_key(A, W, p, sdir);
                 W.perm[0][j] = j;
             }
         }
@@ -336,7 +352,8 @@ __global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_
             next_rays[2 * (size_t)j] = pk(org, p);
             next_rays[2 * (size_t)j + 1] = pk(wi, 0u);
             if (W.sort) {
-                W.key[0][j] = sort_key(A, W, p, wi);
+                W.key[0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
+                                                                            : sort_key(A, W, p, wi);
                 W.perm[0][j] = j;
             }
         }

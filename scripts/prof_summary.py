@@ -46,7 +46,7 @@ def main():
             sums[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
     summary, per_pass = {}, collections.defaultdict(float)
     for name, r in rows.items():
-        if not any(k in name for k in ("render_", "wf_", "sum_samples")):
+        if not any(k in name for k in ("render_", "wf_", "sum_samples", "rocprim")):  # rocprim: queue sorts
             continue
         counting = is_counting(name)
         frames = 1 if counting else (passes - 1 if "wf_trace" in name or "render_dynamic" in name else passes)
