@@ -62,3 +62,16 @@ def test_oracle_is_not_linked_by_product():
     for lib in ("libchiaro_hip.so", "libchiaroscuro.so"):
         data = (ROOT / "chiaroscuro-raytracer_amd" / "lib" / lib).read_bytes()
         assert b"liboracle" not in data and b"or_render" not in data
+
+
+def test_cli_fails_loudly_without_gpu(scenes):
+    """bin/chiaroscuro (the reference main.cpp counterpart) exits non-zero with a
+    message when no GPU is usable -- it never renders on the CPU."""
+    import subprocess
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    exe = ROOT / "chiaroscuro-raytracer_amd" / "bin" / "chiaroscuro"
+    r = subprocess.run([str(exe), str(scenes.config_rtc("cornell")), "xres", "8", "yres", "8", "output",
+                        "/tmp/chiaro_cli_nogpu.pfm"], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "chiaroscuro:" in r.stderr

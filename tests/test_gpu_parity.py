@@ -219,3 +219,33 @@ def test_raytracer_api_layers(ca, scenes):
     assert rt.layers == 3
     rt.rayTrace((0.0, 1.1, 2.9), i["LA"], i["UP"], i["yview"])
     assert rt.layers == 1
+
+
+def read_pfm(path):
+    """PFM (little-endian, rows bottom-to-top) -> [H][W][3] float32, row 0 = top."""
+    data = open(path, "rb").read()
+    parts = data.split(b"\n", 3)
+    assert parts[0] == b"PF"
+    w, h = (int(v) for v in parts[1].split())
+    assert float(parts[2]) < 0
+    return np.frombuffer(parts[3], dtype="<f4", count=w * h * 3).reshape(h, w, 3)[::-1]
+
+
+def test_cli_offline_render_matches_oracle(ca, po, scenes, tmp_path):
+    """bin/chiaroscuro scene.rtc tokens... layers 2 -> PFM equal to the oracle's
+    two progressive layers (main.cpp:5-21 + rayTracer.cpp:17-74 end to end)."""
+    import subprocess
+    from helpers import Pair
+    rtc = scenes.config_rtc("nanobox")
+    out = tmp_path / "nb.pfm"
+    exe = scenes.default_dir().parent.parent / "bin" / "chiaroscuro"
+    r = subprocess.run([str(exe), str(rtc), "xres", "64", "yres", "36", "samples", "3", "output", str(out),
+                        "layers", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    g = read_pfm(out)
+    pair = Pair(ca, po, rtc, "xres", "64", "yres", "36", "samples", "3", device=False)
+    i = pair.info
+    cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], 64, 36).as_array()
+    o, _ = pair.oracle.render(cam, 64, 36, 3, i["k"], i["seed"], layer=1)
+    o, _ = pair.oracle.render(cam, 64, 36, 3, i["k"], i["seed"], layer=2, pixels=o)
+    assert_bitwise(g, o, "cli nanobox 64x36x3, 2 layers")
