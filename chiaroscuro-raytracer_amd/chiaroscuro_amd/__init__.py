@@ -303,6 +303,7 @@ class KDTree:
         rc = libs()[1].chiaro_kdtree_describe(self._h, self._scene._h, C.byref(d))
         if rc:
             raise RuntimeError("describe: " + _host_err())
+        d._owner = self  # the descriptor points into this tree's host arrays: keep it alive
         return d
 
     def __del__(self):
