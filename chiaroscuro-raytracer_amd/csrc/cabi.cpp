@@ -367,7 +367,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     }
     // leaf-ordered triangle records {A,id},{B-A},{C-A}: e1/e2 computed exactly as
     // intersectRayTriangle does each time (kdtree.cpp:222-223), so bit-identical.
-    std::vector<float4> recs((size_t)cr::REC_STRIDE * d->n_refs, make_float4(0.f, 0.f, 0.f, 0.f));
+    std::vector<float4> recs((size_t)cr::REC_STRIDE * (d->n_refs + cr::REC_PAD), make_float4(0.f, 0.f, 0.f, 0.f));
     for (uint32_t r = 0; r < d->n_refs; r++) {
         const uint32_t t = d->refs[r];
         if (t >= nt) return fail(c, CR_E_INVALID, "leaf ref out of range");

@@ -66,8 +66,10 @@ struct TriRec {
     float4 b; // e1
     float4 c; // e2
 };
+// 32-bit byte offset from the SGPR base (global_load saddr + voffset: one VGPR
+// of address per lane, not two); cr_upload_scene keeps the records under 4 GiB.
 __device__ __forceinline__ TriRec load_rec(const DevScene &S, uint32_t ref) {
-    const float4 *p = S.recs + (size_t)REC_STRIDE * ref;
+    const float4 *p = (const float4 *)((const char *)S.recs + (ref * (uint32_t)(16 * REC_STRIDE)));
     return TriRec{p[0], p[1], p[2]};
 }
 __device__ __forceinline__ uint32_t rec_id(const TriRec &r) { return __float_as_uint(r.a.w); }

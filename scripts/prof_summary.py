@@ -18,6 +18,7 @@ figure is L2-miss (fabric) traffic, an upper bound on HBM bytes.
 """
 import collections
 import csv
+import re
 import json
 import shutil
 import sys
@@ -27,7 +28,8 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def is_counting(name: str) -> bool:
-    return ", true, " in name and "wf_trace" in name or "render_dynamic<8, true" in name
+    # FULL is the second template argument of both trace kernels
+    return re.search(r"(wf_trace|render_dynamic)<\w+, true,", name) is not None
 
 
 def main():

@@ -5,7 +5,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-mem}; shift
-ARGS=${@:-"--kernel 0 --rounds 1"}
+ARGS=${@:-"--grid kernel=2 --rounds 1"}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 i=0
