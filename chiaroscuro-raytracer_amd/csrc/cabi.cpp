@@ -36,16 +36,16 @@ struct cr_ctx {
     cr_counters last{};
     // options
     // Defaults from sweeps on MI355X, sponza stand-in 1080p x 128 spp:
-    //   wavefront (kernel 2), trace variant 1, refill 48, 256M paths in flight: 801 Mray/s
-    //   persistent megakernel (kernel 0), variant 0, refill 16:                 615 Mray/s
+    //   wavefront (kernel 2), trace variant 2, refill 64/56/48, sorted queues: 1071 Mray/s
+    //   persistent megakernel (kernel 0), variant 0, refill 16:                615 Mray/s
     int kernel = 2;
     int full_counters = 1;
     int variant = -1;       // -1: the kernel's default build
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
-    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 48 wavefront)
-    uint32_t refill_shadow = 0; // wavefront shadow trace; 0: same as refill
-    uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: same as refill
+    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 56 wavefront)
+    uint32_t refill_shadow = 0; // wavefront shadow trace; 0: refill if set, else 48
+    uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: refill if set, else 64
     uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
     int wf_sort = 1;                // wavefront: sort large shadow / secondary queues for coherence
     uint32_t wf_sort_min = 1u << 20; // ... of at least this many rays
@@ -367,7 +367,10 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     }
     // leaf-ordered triangle records {A,id},{B-A},{C-A}: e1/e2 computed exactly as
     // intersectRayTriangle does each time (kdtree.cpp:222-223), so bit-identical.
-    std::vector<float4> recs((size_t)cr::REC_STRIDE * (d->n_refs + cr::REC_PAD), make_float4(0.f, 0.f, 0.f, 0.f));
+    // load_rec addresses records with a 32-bit byte offset
+    if ((uint64_t)16 * cr::REC_STRIDE * (uint64_t)d->n_refs > 0xFFFFFFFFull)
+        return fail(c, CR_E_INVALID, "more than 89 M leaf references (triangle records exceed 4 GiB)");
+    std::vector<float4> recs((size_t)cr::REC_STRIDE * d->n_refs, make_float4(0.f, 0.f, 0.f, 0.f));
     for (uint32_t r = 0; r < d->n_refs; r++) {
         const uint32_t t = d->refs[r];
         if (t >= nt) return fail(c, CR_E_INVALID, "leaf ref out of range");

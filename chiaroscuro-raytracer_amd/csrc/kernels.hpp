@@ -8,7 +8,7 @@ namespace cr {
 enum { MODE_BLEND = 0, MODE_TILES = 1 };
 // float4 per triangle record.  3 (48 B, 1.5 lines per test on average) beat 4
 // (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
-enum { REC_STRIDE = 3, REC_PAD = 2 }; // REC_PAD zero records follow the last leaf's (PF 2 leaf loop)
+enum { REC_STRIDE = 3 };
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one
 // texel past the row/image end for coords == 1.0 (src/mesh.cpp:23-30) and three

@@ -83,11 +83,12 @@ template <bool SC> __device__ __forceinline__ uint2 load_node(const DevScene &S,
     return S.nodes[node];
 }
 
-// PF: 0 = plain leaf loop; 1 = software-pipelined (triangle j+1's loads issued
-// before j is tested); 2 = the same unrolled by two with unconditional loads
-// (REC_PAD zero records after the last leaf), so the two record sets keep their
-// registers instead of being copied every triangle.
-template <int R, bool FULL, int PF, bool FD, bool SC = false>
+// PF: software-pipelined leaf loop (triangle j+1's loads issued before j is
+// tested).  Measured and dropped: the same unrolled by two with unconditional
+// loads (no register rotation copies, but count-1 leaves fetch a second record:
+// -2.3%), and compiler-scheduled, pipelined scalar loads for uniform leaves
+// (address_space(4): -2.5% against the asm s_load + wait below).
+template <int R, bool FULL, bool PF, bool FD, bool SC = false>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c) {
@@ -165,17 +166,6 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         for (uint32_t j = 0; j < count; j++) {
             tally_tri(first + j);
             if (!test(sload_rec(base + (size_t)REC_STRIDE * j))) break;
-        }
-    } else if (PF == 2) {
-        TriRec ra = load_rec(S, first), rb;
-        for (uint32_t j = 0; j < count; j += 2) {
-            rb = load_rec(S, first + j + 1); // may be the pad record
-            tally_tri(first + j);
-            if (!test(ra)) break;
-            if (j + 1 >= count) break;
-            ra = load_rec(S, first + j + 2);
-            tally_tri(first + j + 1);
-            if (!test(rb)) break;
         }
     } else {
         TriRec nx;

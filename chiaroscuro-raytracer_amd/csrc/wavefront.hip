@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // Persistent: every lane runs one query at a time through trav_round; when
 // `A.refill` lanes of a wave have finished (or none is busy) they take the
 // next rays of the queue (one atomicAdd per wave).
-template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, int PF = 1>
+template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
+            const uint32_t r = trav_round<R, FULL, true, FD, SC>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
                                                                  exclude, T, c);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
@@ -366,12 +366,9 @@ struct WfVariant {
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd;
 };
-#define CR_WF(R, W, SC, FD, PF)                                                                                \
-    {wf_trace<false, false, R, W, SC, FD, PF>, wf_trace<true, false, R, W, SC, FD, PF>, R, W}
-static const WfVariant kWf[] = {CR_WF(4, 8, false, false, 1), CR_WF(8, 8, false, false, 1),
-                                CR_WF(8, 8, true, false, 1),  CR_WF(8, 6, false, false, 1),
-                                CR_WF(8, 6, true, false, 1),  CR_WF(8, 8, true, true, 1),
-                                CR_WF(8, 8, true, false, 2)};
+#define CR_WF(R, W, SC, FD) {wf_trace<false, false, R, W, SC, FD>, wf_trace<true, false, R, W, SC, FD>, R, W}
+static const WfVariant kWf[] = {CR_WF(4, 8, false, false), CR_WF(8, 8, false, false), CR_WF(8, 8, true, false),
+                                CR_WF(8, 6, false, false),  CR_WF(8, 6, true, false),  CR_WF(8, 8, true, true)};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
