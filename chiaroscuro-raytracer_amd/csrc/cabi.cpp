@@ -162,7 +162,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     HIPCHK(hipSetDevice(c->device));
     cr::RenderArgs A{};
     fill_args(c, A, cam, p, out, mode);
-    HIPCHK(hipMemsetAsync(c->d_counters, 0, 16 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     if (c->kernel == 0 || c->kernel == 2) {
         const bool wf = c->kernel == 2;
         uint32_t blk, blocks;
@@ -276,11 +276,13 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
         HIPCHK(hipEventRecord(c->ev1, st));
     }
-    unsigned long long h[16];
+    unsigned long long h[cr::CTR_SLOTS];
     HIPCHK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
-    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13], h[14]};
+    c->last = cr_counters{h[0], h[1],  h[2],  h[3],  h[4],  h[5],  h[6],  h[7], h[8],
+                          h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16],
+                          h[17], h[18], h[19], h[20], h[21]};
     return CR_OK;
 }
 
@@ -309,7 +311,7 @@ cr_ctx *cr_create(int device) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_counters, cr::CTR_SLOTS * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_work, 16 * sizeof(uint32_t)) != hipSuccess) {
         c->err = "device init failed";
         c->device = -1;
@@ -531,7 +533,7 @@ static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, cons
     if (e == hipSuccess) e = hipMemcpy(d_dir, dir, fbytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && shadow) e = hipMemcpy(d_dist, dist, n * sizeof(float), hipMemcpyHostToDevice);
     if (e == hipSuccess && shadow) e = hipMemcpy(d_light, light, n * sizeof(uint32_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long));
     Q.orig = d_orig; Q.dir = d_dir; Q.dist = d_dist; Q.light = d_light;
     Q.hit = d_hit; Q.tri = d_tri; Q.bary = d_bary; Q.dist_out = d_do;
     Q.counters = c->d_counters;
@@ -541,11 +543,13 @@ static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, cons
     if (e == hipSuccess && !shadow && tri) e = hipMemcpy(tri, d_tri, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
     if (e == hipSuccess && !shadow && bary) e = hipMemcpy(bary, d_bary, 2 * n * sizeof(float), hipMemcpyDeviceToHost);
     if (e == hipSuccess && !shadow && dist_out) e = hipMemcpy(dist_out, d_do, n * sizeof(float), hipMemcpyDeviceToHost);
-    unsigned long long h[16] = {};
+    unsigned long long h[cr::CTR_SLOTS] = {};
     if (e == hipSuccess) e = hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost);
     hipFree(buf);
     if (e != hipSuccess) return hip_fail(c, e, "intersect");
-    c->last = cr_counters{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9], h[10], h[11], h[12], h[13], h[14]};
+    c->last = cr_counters{h[0], h[1],  h[2],  h[3],  h[4],  h[5],  h[6],  h[7], h[8],
+                          h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16],
+                          h[17], h[18], h[19], h[20], h[21]};
     return CR_OK;
 }
 

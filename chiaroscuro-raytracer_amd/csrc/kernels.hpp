@@ -9,6 +9,7 @@ enum { MODE_BLEND = 0, MODE_TILES = 1 };
 // float4 per triangle record.  3 (48 B, 1.5 lines per test on average) beat 4
 // (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
 enum { REC_STRIDE = 3 };
+enum { CTR_N = 22, CTR_SLOTS = 32 }; // Ctr fields (cr_counters order); device counter buffer entries
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one
 // texel past the row/image end for coords == 1.0 (src/mesh.cpp:23-30) and three

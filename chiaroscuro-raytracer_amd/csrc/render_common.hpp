@@ -12,6 +12,8 @@ struct Ctr {
     uint32_t closest = 0, shadow = 0, inner = 0, leaf = 0, tritest = 0, hit = 0, texhit = 0, paths = 0, pixels = 0;
     uint32_t wave_desc = 0, wave_tri = 0, wave_round = 0, wave_query = 0; // diagnostics, see chiaro_hip.h
     uint32_t wave_desc_uniform = 0, wave_tri_uniform = 0;
+    uint32_t wave_desc_lines = 0, wave_tri_lines = 0;
+    uint32_t leaf_rounds = 0, leaf_distinct = 0, leaf_records = 0, leaf_fit21 = 0, leaf_fit56 = 0;
 };
 __device__ __forceinline__ uint32_t wave_count(bool pred) { return (uint32_t)__popcll(__ballot(pred)); }
 // True in exactly one active lane (the lowest): `if (wave_leader()) n++` counts
@@ -22,11 +24,13 @@ __device__ __forceinline__ bool wave_leader() {
 
 // Call with the whole wave converged.
 __device__ __forceinline__ void flush_counters(unsigned long long *ctrs, const Ctr &c, uint32_t uniform = 0u) {
-    const uint32_t v[15] = {c.closest, c.shadow,  c.inner,    c.leaf,     c.tritest,   c.hit,       c.texhit,
-                            c.paths,   c.pixels, c.wave_desc, c.wave_tri, c.wave_round, c.wave_query,
-                            c.wave_desc_uniform, c.wave_tri_uniform};
+    const uint32_t v[CTR_N] = {c.closest,   c.shadow,    c.inner,      c.leaf,       c.tritest,
+                               c.hit,       c.texhit,    c.paths,      c.pixels,     c.wave_desc,
+                               c.wave_tri,  c.wave_round, c.wave_query, c.wave_desc_uniform, c.wave_tri_uniform,
+                               c.wave_desc_lines, c.wave_tri_lines, c.leaf_rounds, c.leaf_distinct,
+                               c.leaf_records,    c.leaf_fit21,     c.leaf_fit56};
 #pragma unroll
-    for (int i = 0; i < 15; i++) {
+    for (int i = 0; i < CTR_N; i++) {
         unsigned long long s = v[i];
         if (!(uniform & (1u << i))) {
 #pragma unroll

@@ -21,6 +21,18 @@ __device__ __forceinline__ bool wave_uniform(uint32_t x) {
     return __ballot(x == (uint32_t)__builtin_amdgcn_readfirstlane(x)) == __ballot(1);
 }
 
+// Distinct values of key over the active lanes (FULL-build diagnostics).
+__device__ __forceinline__ uint32_t wave_distinct(uint32_t key) {
+    uint64_t m = __ballot(1);
+    uint32_t n = 0;
+    while (m) {
+        const uint32_t k = (uint32_t)__shfl((int)key, __ffsll((long long)m) - 1, 64);
+        m &= ~__ballot(key == k);
+        n++;
+    }
+    return n;
+}
+
 // Traversal registers of a query in flight.  r = per-axis rcp_for_div(d) for
 // the exact short split-distance division (FD builds, device_math.hpp).
 struct Trav {
@@ -98,9 +110,11 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         if (FULL) {
             c.inner++;
             const bool uni = wave_uniform(T.node);
+            const uint32_t lines = wave_distinct(T.node >> 4); // 8-B nodes
             if (wave_leader()) {
                 c.wave_desc++;
                 c.wave_desc_uniform += uni;
+                c.wave_desc_lines += lines;
             }
         }
         const uint32_t a = nd.y & 3u;
@@ -155,12 +169,32 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
     auto tally_tri = [&](uint32_t ref) {
         if (FULL) {
             const bool uni = wave_uniform(ref);
+            const uint32_t lines = wave_distinct(ref * (16u * REC_STRIDE) >> 7);
             if (wave_leader()) {
                 c.wave_tri++;
                 c.wave_tri_uniform += uni;
+                c.wave_tri_lines += lines;
             }
         }
     };
+    if (FULL && !wave_uniform(first)) { // what staging the wave's leaves in LDS would take
+        uint64_t m = __ballot(count > 0);
+        uint32_t nd = 0, nr = 0;
+        while (m) {
+            const int l = __ffsll((long long)m) - 1;
+            const uint32_t f = (uint32_t)__shfl((int)first, l, 64), n = (uint32_t)__shfl((int)count, l, 64);
+            m &= ~__ballot(first == f && count > 0);
+            nd++;
+            nr += n;
+        }
+        if (wave_leader()) {
+            c.leaf_rounds++;
+            c.leaf_distinct += nd;
+            c.leaf_records += nr;
+            c.leaf_fit21 += nr <= 21;
+            c.leaf_fit56 += nr <= 56;
+        }
+    }
     if (SC && wave_uniform(first)) { // every lane at the same leaf: scalar loads
         const float4 *base = S.recs + (size_t)REC_STRIDE * __builtin_amdgcn_readfirstlane(first);
         for (uint32_t j = 0; j < count; j++) {

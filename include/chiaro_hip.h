@@ -135,6 +135,20 @@ typedef struct {
      * every active lane (a scalar load would serve the whole wave) */
     uint64_t wave_desc_uniform;
     uint64_t wave_tri_uniform;
+    /* of wave_desc / wave_tri: distinct 128-B cache lines the iteration's node /
+     * first record load touches, summed (the cost unit of the vector memory
+     * address path) */
+    uint64_t wave_desc_lines;
+    uint64_t wave_tri_lines;
+    /* leaf rounds whose leaf is not wave-uniform: how many, the distinct leaves
+     * and the triangle records they hold (summed), and how many of those rounds
+     * hold at most 21 / 56 records (what a per-wave LDS staging area of 1 / 2.6
+     * KiB would take) */
+    uint64_t leaf_rounds;
+    uint64_t leaf_distinct;
+    uint64_t leaf_records;
+    uint64_t leaf_fit21;
+    uint64_t leaf_fit56;
 } cr_counters;
 
 cr_ctx *cr_create(int device);

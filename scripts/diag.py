@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--kernel", type=int, default=2)
     ap.add_argument("--variant", type=int, default=-1)
     ap.add_argument("--refill", type=int, default=0)
+    ap.add_argument("--k", type=int, default=0, help="path depth override (1: camera + first shadow rays only)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -36,7 +37,7 @@ def main():
     dev.set_option("kernel", args.kernel)
     dev.set_option("variant", args.variant)
     dev.set_option("refill", args.refill)
-    p = ca.render_params(i["xres"], i["yres"], args.spp, i["k"], i["seed"])
+    p = ca.render_params(i["xres"], i["yres"], args.spp, args.k or i["k"], i["seed"])
     dev.render_device(cam, p, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     c = dev.counters()
@@ -54,6 +55,13 @@ def main():
         "leaves_per_query_lane": round(c["leaf"] / rays, 1),
         "uniform_desc": round(c["wave_desc_uniform"] / max(c["wave_desc"], 1), 3),
         "uniform_tri": round(c["wave_tri_uniform"] / max(c["wave_tri"], 1), 3),
+        "lines_per_desc": round(c["wave_desc_lines"] / max(c["wave_desc"], 1), 2),
+        "lines_per_tri": round(c["wave_tri_lines"] / max(c["wave_tri"], 1), 2),
+        "nonuniform_leaf_rounds": round(c["leaf_rounds"] / max(c["wave_round"], 1), 3),
+        "distinct_leaves_per_round": round(c["leaf_distinct"] / max(c["leaf_rounds"], 1), 2),
+        "records_per_round": round(c["leaf_records"] / max(c["leaf_rounds"], 1), 1),
+        "rounds_fit21": round(c["leaf_fit21"] / max(c["leaf_rounds"], 1), 3),
+        "rounds_fit56": round(c["leaf_fit56"] / max(c["leaf_rounds"], 1), 3),
     })
     print(json.dumps(out))
 
