@@ -82,6 +82,17 @@ class ChiaroSceneInfo(C.Structure):
                 ("obj_path", C.c_char * 1024), ("render_path", C.c_char * 1024)]
 
 
+class CrTonemapParams(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("m", "s", "kl", "f", "defog", "gamma")]
+
+
+def tonemap_params(exposure, defog=0.0, knee_low=0.0, knee_high=5.0, gamma=2.2) -> CrTonemapParams:
+    """cr_tonemap_setup: normalizeImage's host scalars (src/rayTracer.cpp:196-205)."""
+    t = CrTonemapParams()
+    libs()[0].cr_tonemap_setup(exposure, defog, knee_low, knee_high, gamma, C.byref(t))
+    return t
+
+
 # --------------------------------------------------------------- loading --
 _hip = None
 _host = None
@@ -89,7 +100,8 @@ _host = None
 # Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
                "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_intersect",
-               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_set_option", "cr_synchronize")
+               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_set_option", "cr_synchronize",
+               "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
                 "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
@@ -137,6 +149,10 @@ def libs():
     _sig(hip, "cr_last_kernel_ms", C.c_float, [P])
     _sig(hip, "cr_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
     _sig(hip, "cr_synchronize", C.c_int, [P])
+    _sig(hip, "cr_tonemap_setup", None, [C.c_float] * 5 + [C.POINTER(CrTonemapParams)])
+    _sig(hip, "cr_tonemap_device", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32, P, P, P])
+    _sig(hip, "cr_tonemap", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32,
+                                      C.POINTER(C.c_uint8)])
 
     _sig(host, "chiaro_last_error", C.c_char_p, [])
     _sig(host, "chiaro_scene_create", P, [C.c_int, C.POINTER(C.c_char_p)])
@@ -351,6 +367,12 @@ class Device:
                                                   C.c_void_p(d_frame_ptr), C.c_void_p(stream)),
                   "cr_blend_tiles_device")
 
+    def tonemap_device(self, t: CrTonemapParams, xres: int, yres: int, d_rgb_ptr: int, d_bytes_ptr: int,
+                       stream: int = 0):
+        """normalizeImage's per-pixel transform on device buffers (rows flipped)."""
+        self._chk(libs()[0].cr_tonemap_device(self._c, C.byref(t), xres, yres, C.c_void_p(d_rgb_ptr),
+                                              C.c_void_p(d_bytes_ptr), C.c_void_p(stream)), "cr_tonemap_device")
+
     @staticmethod
     def tiles_for_rank(p: CrRenderParams, rank: int) -> int:
         return int(libs()[0].cr_tiles_for_rank(C.byref(p), int(rank)))
@@ -437,7 +459,8 @@ class RayTracer:
         return np.ctypeslib.as_array(d, shape=(self.yres, self.xres, 3)).copy()
 
     def normalizeImage(self, exposure=3.4028234663852886e38, defog=0.0, kneeLow=0.0, kneeHigh=5.0, gamma=2.2):
-        libs()[1].chiaro_raytracer_normalize(self._h, exposure, defog, kneeLow, kneeHigh, gamma)
+        if libs()[1].chiaro_raytracer_normalize(self._h, exposure, defog, kneeLow, kneeHigh, gamma):
+            raise RuntimeError("normalizeImage: " + _host_err())
 
     def exportImage(self, filename: str):
         if libs()[1].chiaro_raytracer_export(self._h, str(filename).encode()):

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -367,6 +368,20 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
             nodes[i] = make_uint2(sb, n.axis | (n.child_or_first << 2));
         }
     }
+    // fat node records: a node's own record followed by both children's
+    if ((uint64_t)32 * d->n_nodes > 0xFFFFFFFFull) return fail(c, CR_E_INVALID, "more than 134 M kd nodes");
+    std::vector<uint4> fat((size_t)2 * d->n_nodes, make_uint4(0u, 0u, 0u, 0u));
+    for (uint32_t i = 0; i < d->n_nodes; i++) {
+        const uint2 n = nodes[i];
+        fat[2 * (size_t)i].x = n.x;
+        fat[2 * (size_t)i].y = n.y;
+        if ((n.y & 3u) != 3u) {
+            const uint32_t ch = n.y >> 2;
+            fat[2 * (size_t)i].z = nodes[ch].x;
+            fat[2 * (size_t)i].w = nodes[ch].y;
+            fat[2 * (size_t)i + 1] = make_uint4(nodes[ch + 1].x, nodes[ch + 1].y, 0u, 0u);
+        }
+    }
     // leaf-ordered triangle records {A,id},{B-A},{C-A}: e1/e2 computed exactly as
     // intersectRayTriangle does each time (kdtree.cpp:222-223), so bit-identical.
     // load_rec addresses records with a 32-bit byte offset
@@ -425,7 +440,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         texs[i] = make_uint4((uint32_t)t.width, (uint32_t)t.height, (uint32_t)t.components, (uint32_t)off);
     }
     int rc;
-    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, tri, &c->S.tri)) ||
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
         (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels))) {
@@ -503,6 +518,64 @@ int cr_blend_tiles_device(cr_ctx *c, const cr_render_params *p, const float *d_g
     int e = cr::launch_blend(B, (hipStream_t)stream);
     if (e) return hip_fail(c, (hipError_t)e, "blend kernel launch");
     return CR_OK;
+}
+
+// rayTracer.cpp:172-205: host scalars of normalizeImage, glibc powf / logf as the reference
+static inline float tm_knee(double x, double f) { return logf(x * f + 1) / f; }
+static float tm_find_knee_f(float x, float y) {
+    float f0 = 0, f1 = 1;
+    while (tm_knee(x, f1) > y) {
+        f0 = f1;
+        f1 = f1 * 2;
+    }
+    for (int i = 0; i < 30; ++i) {
+        const float f2 = (f0 + f1) / 2;
+        if (tm_knee(x, f2) < y) f1 = f2;
+        else f0 = f2;
+    }
+    return (f0 + f1) / 2;
+}
+
+void cr_tonemap_setup(float exposure, float defog, float kneeLow, float kneeHigh, float gamma, cr_tonemap_params *t) {
+    if (!t) return;
+    t->m = powf(2.f, exposure + 2.47393f);
+    t->s = 255.f * powf(2.f, -3.5f * gamma);
+    t->kl = powf(2.f, kneeLow);
+    t->f = tm_find_knee_f(powf(2.f, kneeHigh), powf(2.f, 3.5) - t->kl);
+    t->defog = defog;
+    t->gamma = gamma;
+}
+
+int cr_tonemap_device(cr_ctx *c, const cr_tonemap_params *t, uint32_t xres, uint32_t yres, const float *d_rgb,
+                      uint8_t *d_bytes, void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!t || !d_rgb || !d_bytes) return fail(c, CR_E_INVALID, "bad tonemap args");
+    if ((uint64_t)xres * yres > (1ull << 31)) return fail(c, CR_E_INVALID, "image too large");
+    HIPCHK(hipSetDevice(c->device));
+    const cr::TonemapArgs T{d_rgb, d_bytes, xres, yres, t->m, t->s, t->kl, t->f, t->defog, t->gamma};
+    const int e = cr::launch_tonemap(T, (hipStream_t)stream);
+    if (e) return hip_fail(c, (hipError_t)e, "tonemap kernel launch");
+    return CR_OK;
+}
+
+int cr_tonemap(cr_ctx *c, const cr_tonemap_params *t, uint32_t xres, uint32_t yres, uint8_t *bytes_out) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!bytes_out) return fail(c, CR_E_INVALID, "null output");
+    const size_t n = (size_t)3 * xres * yres;
+    if (!c->d_accum || c->accum_elems != n) return fail(c, CR_E_INVALID, "no rendered frame of this size");
+    HIPCHK(hipSetDevice(c->device));
+    void *d_bytes = nullptr;
+    if (hipMalloc(&d_bytes, n ? n : 1) != hipSuccess) return fail(c, CR_E_OOM, "tonemap buffer");
+    int rc = cr_tonemap_device(c, t, xres, yres, c->d_accum, (uint8_t *)d_bytes, c->stream);
+    if (rc == CR_OK) {
+        const hipError_t e = hipMemcpyAsync(bytes_out, d_bytes, n, hipMemcpyDeviceToHost, c->stream);
+        const hipError_t e2 = e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
+        if (e2 != hipSuccess) rc = hip_fail(c, e2, "tonemap copy");
+    }
+    hipFree(d_bytes);
+    return rc;
 }
 
 static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, const float *dir, const float *dist,

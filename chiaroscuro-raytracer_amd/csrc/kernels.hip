@@ -238,6 +238,28 @@ __global__ void __launch_bounds__(256) blend_tiles_kernel(BlendArgs B) {
     o[2] = nw.z;
 }
 
+// Tonemap, one byte per thread (reads coalesced, writes row-contiguous).
+// knee (rayTracer.cpp:172): logf((float)(x*f + 1)) / f in double, returned as
+// float; logf and powf are evaluated in double and rounded once (glibc's logf /
+// powf are double-evaluated too; the two agree except where the value lies
+// within their error of a float rounding boundary -- tests/test_gpu_tonemap.py).
+__global__ void __launch_bounds__(256) tonemap_kernel(TonemapArgs T) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n = 3ull * T.xres * T.yres;
+    if (e >= n) return;
+    const uint32_t p = (uint32_t)(e / 3), ch = (uint32_t)(e - 3ull * p);
+    const uint32_t y = p / T.xres, x = p - y * T.xres;
+    float v = std_max(0.f, T.rgb[e] - T.defog);
+    v *= T.m;
+    if (v > T.kl) {
+        const float lg = (float)log((double)(float)((double)(v - T.kl) * (double)T.f + 1.0));
+        v = T.kl + (float)((double)lg / (double)T.f);
+    }
+    const float w = (float)pow((double)v, (double)T.gamma) * T.s;
+    const float c = (w > 0.f ? w : 0.f) < 255.f ? (w > 0.f ? w : 0.f) : 255.f; // glm::clamp
+    T.out[3ull * ((uint64_t)(T.yres - 1 - y) * T.xres + x) + ch] = (uint8_t)c;
+}
+
 // ---------------------------------------------------------------- launch --
 int launch_render(const RenderArgs &A, int kernel, uint32_t block, uint32_t waves_per_cu, int num_cus,
                   hipStream_t st) {
@@ -267,6 +289,13 @@ int launch_blend(const BlendArgs &B, hipStream_t st) {
     const uint32_t n = B.xres * B.yres;
     if (n == 0) return 0;
     hipLaunchKernelGGL(blend_tiles_kernel, dim3((n + 255) / 256), dim3(256), 0, st, B);
+    return (int)hipGetLastError();
+}
+
+int launch_tonemap(const TonemapArgs &T, hipStream_t st) {
+    const uint64_t n = 3ull * T.xres * T.yres;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(tonemap_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, T);
     return (int)hipGetLastError();
 }
 

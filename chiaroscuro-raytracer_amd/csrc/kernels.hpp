@@ -18,6 +18,7 @@ __host__ __device__ inline uint64_t tex_pad(int w, int nc) { return (uint64_t)(w
 
 struct DevScene {
     const uint2 *nodes;   // {split bits | first ref, axis | child<<2 ; leaf: 3 | count<<2}
+    const uint4 *fat;     // 2 per node: {self, child 0}, {child 1, 0, 0} (two-level descent)
     // REC_STRIDE float4 per leaf reference, AoS: {A, tri id bits}, {e1 = B-A, 0},
     // {e2 = C-A, 0} -- bitwise what the reference computes per test.  (A 40-B SoA
     // split measured 15% slower: three cache lines per test instead of one or two.)
@@ -143,9 +144,18 @@ struct BlendArgs {
     uint32_t xres, yres, tile, tiles_x, nranks, max_tiles, layer;
 };
 
+// RayTracer::normalizeImage's per-pixel transform (src/rayTracer.cpp:207-221)
+struct TonemapArgs {
+    const float *rgb; // [yres][xres][3], row 0 = top
+    uint8_t *out;     // [yres][xres][3], rows flipped as the reference's data
+    uint32_t xres, yres;
+    float m, s, kl, f, defog, gamma;
+};
+
 int launch_render(const RenderArgs &A, int kernel, uint32_t block, uint32_t waves_per_cu, int num_cus,
                   hipStream_t st);
 int launch_intersect(const QueryArgs &Q, hipStream_t st);
 int launch_blend(const BlendArgs &B, hipStream_t st);
+int launch_tonemap(const TonemapArgs &T, hipStream_t st);
 
 } // namespace cr

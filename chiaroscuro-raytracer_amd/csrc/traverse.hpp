@@ -76,6 +76,7 @@ __device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool s
 typedef unsigned int cr_v2u __attribute__((ext_vector_type(2)));
 typedef float cr_v4f __attribute__((ext_vector_type(4)));
 typedef float cr_v8f __attribute__((ext_vector_type(8)));
+typedef unsigned int cr_v8u __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ uint2 sload_node(const uint2 *p) {
     cr_v2u r;
     asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
@@ -95,22 +96,38 @@ template <bool SC> __device__ __forceinline__ uint2 load_node(const DevScene &S,
     return S.nodes[node];
 }
 
+// Fat node records (DevScene::fat): 32 B per node, {self, child 0, child 1}, so
+// one dependent load serves two descent levels.
+__device__ __forceinline__ void sload_fat(const uint4 *p, uint4 &a, uint4 &b) {
+    cr_v8u r;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
+    a = make_uint4(r[0], r[1], r[2], r[3]);
+    b = make_uint4(r[4], r[5], r[6], r[7]);
+}
+template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, uint32_t node, uint4 &a, uint4 &b) {
+    if (SC && wave_uniform(node)) return sload_fat(S.fat + 2u * __builtin_amdgcn_readfirstlane(node), a, b);
+    const uint4 *p = (const uint4 *)((const char *)S.fat + node * 32u);
+    a = p[0];
+    b = p[1];
+}
+
 // PF: software-pipelined leaf loop (triangle j+1's loads issued before j is
 // tested).  Measured and dropped: the same unrolled by two with unconditional
 // loads (no register rotation copies, but count-1 leaves fetch a second record:
 // -2.3%), and compiler-scheduled, pipelined scalar loads for uniform leaves
 // (address_space(4): -2.5% against the asm s_load + wait below).
-template <int R, bool FULL, bool PF, bool FD, bool SC = false>
+template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c) {
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
-    uint2 nd = load_node<SC>(S, T.node);
-    while ((nd.y & 3u) != 3u) {
+    // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
+    // descend into (child + k), the far child pushed when both are crossed
+    auto step = [&](uint2 nd) -> uint32_t {
         if (FULL) {
             c.inner++;
             const bool uni = wave_uniform(T.node);
-            const uint32_t lines = wave_distinct(T.node >> 4); // 8-B nodes
+            const uint32_t lines = wave_distinct(T.node >> (FAT ? 2 : 4)); // 32-B / 8-B node records
             if (wave_leader()) {
                 c.wave_desc++;
                 c.wave_desc_uniform += uni;
@@ -123,10 +140,11 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         const float tsplit = FD ? div_by_rcp(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
         const uint32_t below = (oa < split) || (oa == split && da <= 0);
         const uint32_t child = nd.y >> 2;
+        uint32_t k;
         if (tsplit >= T.tmax || tsplit < 0) {
-            T.node = child + (1u - below);
+            k = 1u - below;
         } else if (tsplit <= T.tmin) {
-            T.node = child + below;
+            k = below;
         } else {
             const uint2 e = make_uint2(child + below, __float_as_uint(T.tmax));
             const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
@@ -134,10 +152,31 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             else T.nl++;
             ring[slot] = e;
             T.sp++;
-            T.node = child + (1u - below);
             T.tmax = tsplit;
+            k = 1u - below;
         }
+        T.node = child + k;
+        return k;
+    };
+    uint2 nd;
+    if (FAT) { // two levels per dependent load: a node's record carries its children's
+        uint4 f0, f1;
+        load_fat<SC>(S, T.node, f0, f1);
+        nd = make_uint2(f0.x, f0.y);
+        while ((nd.y & 3u) != 3u) {
+            const uint32_t k = step(nd);
+            nd = k ? make_uint2(f1.x, f1.y) : make_uint2(f0.z, f0.w);
+            if ((nd.y & 3u) == 3u) break;
+            step(nd);
+            load_fat<SC>(S, T.node, f0, f1);
+            nd = make_uint2(f0.x, f0.y);
+        }
+    } else {
         nd = load_node<SC>(S, T.node);
+        while ((nd.y & 3u) != 3u) {
+            step(nd);
+            nd = load_node<SC>(S, T.node);
+        }
     }
     if (FULL) {
         c.leaf++;
@@ -200,6 +239,18 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         for (uint32_t j = 0; j < count; j++) {
             tally_tri(first + j);
             if (!test(sload_rec(base + (size_t)REC_STRIDE * j))) break;
+        }
+    } else if (PF == 2) { // pipelined, unrolled by two: the record sets alternate roles, no copies
+        TriRec ra, rb;
+        if (count) ra = load_rec(S, first);
+        for (uint32_t j = 0; j < count; j += 2) {
+            if (j + 1 < count) rb = load_rec(S, first + j + 1);
+            tally_tri(first + j);
+            if (!test(ra)) break;
+            if (j + 1 >= count) break;
+            if (j + 2 < count) ra = load_rec(S, first + j + 2);
+            tally_tri(first + j + 1);
+            if (!test(rb)) break;
         }
     } else {
         TriRec nx;

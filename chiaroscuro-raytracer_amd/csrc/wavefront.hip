@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // Persistent: every lane runs one query at a time through trav_round; when
 // `A.refill` lanes of a wave have finished (or none is busy) they take the
 // next rays of the queue (one atomicAdd per wave).
-template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false>
+template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, true, FD, SC>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
                                                                  exclude, T, c);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
@@ -366,9 +366,13 @@ struct WfVariant {
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd;
 };
-#define CR_WF(R, W, SC, FD) {wf_trace<false, false, R, W, SC, FD>, wf_trace<true, false, R, W, SC, FD>, R, W}
-static const WfVariant kWf[] = {CR_WF(4, 8, false, false), CR_WF(8, 8, false, false), CR_WF(8, 8, true, false),
-                                CR_WF(8, 6, false, false),  CR_WF(8, 6, true, false),  CR_WF(8, 8, true, true)};
+#define CR_WF(R, W, SC, FD, FAT)                                                                               \
+    {wf_trace<false, false, R, W, SC, FD, FAT>, wf_trace<true, false, R, W, SC, FD, FAT>, R, W}
+static const WfVariant kWf[] = {
+    CR_WF(4, 8, false, false, false), CR_WF(8, 8, false, false, false), CR_WF(8, 8, true, false, false),
+    CR_WF(8, 6, false, false, false), CR_WF(8, 6, true, false, false),  CR_WF(8, 8, true, true, false),
+    CR_WF(8, 8, true, false, true),   CR_WF(8, 8, false, false, true),
+    {wf_trace<false, false, 8, 8, true, false, false, 2>, wf_trace<true, false, 8, 8, true, false, false, 2>, 8, 8}};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }

@@ -269,8 +269,12 @@ int chiaro_raytracer_counters(const chiaro_raytracer *r, cr_counters *out) {
 }
 int chiaro_raytracer_normalize(chiaro_raytracer *r, float exposure, float defog, float kl, float kh, float gamma) {
     if (!r) return CR_E_INVALID;
-    r->r->normalizeImage(exposure, defog, kl, kh, gamma);
-    return CR_OK;
+    return guard(
+        [&]() -> int {
+            r->r->normalizeImage(exposure, defog, kl, kh, gamma);
+            return CR_OK;
+        },
+        CR_E_HIP);
 }
 int chiaro_raytracer_export(chiaro_raytracer *r, const char *filename) {
     if (!r || !filename) return CR_E_INVALID;

@@ -123,48 +123,16 @@ void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) {
 
 uint8_t *RayTracer::getData() { return data.data(); }
 
-// rayTracer.cpp:173-195
-static inline float knee(double x, double f) { return logf(x * f + 1) / f; }
-static float findKneeF(float x, float y) {
-    float f0 = 0;
-    float f1 = 1;
-    while (knee(x, f1) > y) {
-        f0 = f1;
-        f1 = f1 * 2;
-    }
-    for (int i = 0; i < 30; ++i) {
-        float f2 = (f0 + f1) / 2;
-        float y2 = knee(x, f2);
-        if (y2 < y)
-            f1 = f2;
-        else
-            f0 = f2;
-    }
-    return (f0 + f1) / 2;
-}
-
-// rayTracer.cpp:198-223 (exrdisplay-style), host post-process
+// rayTracer.cpp:196-222 (exrdisplay-style): the scalar setup on the host, the
+// per-pixel transform on the GPU over the device accumulator of the last layer
+// (cr_tonemap; bytes differ from the reference's glibc powf / logf only where a
+// value lies within their error of a rounding boundary).
 void RayTracer::normalizeImage(float exposure, float defog, float kneeLow, float kneeHigh, float gamma) {
     if (exposure == FLT_MAX) exposure = scene.exposure;
-    const float m = powf(2.f, exposure + 2.47393f);
-    const float s = 255.f * powf(2.f, -3.5f * gamma);
-    const float kl = powf(2.f, kneeLow);
-    const float f = findKneeF(powf(2.f, kneeHigh), powf(2.f, 3.5) - kl);
-    auto transform = [=](float x) {
-        x = std_max(0.f, x - defog);
-        x *= m;
-        if (x > kl) x = kl + knee(x - kl, f);
-        const float v = powf(x, gamma) * s;
-        return (v > 0.f ? v : 0.f) < 255.f ? (v > 0.f ? v : 0.f) : 255.f; // glm::clamp
-    };
-    for (unsigned y = 0; y < scene.yres; y++)
-        for (unsigned x = 0; x < scene.xres; x++) {
-            size_t i = 3 * ((size_t)(scene.yres - y - 1) * scene.xres + x);
-            const float *p = &pixels[3 * ((size_t)y * scene.xres + x)];
-            data[i++] = (uint8_t)transform(p[0]);
-            data[i++] = (uint8_t)transform(p[1]);
-            data[i++] = (uint8_t)transform(p[2]);
-        }
+    cr_tonemap_params t;
+    cr_tonemap_setup(exposure, defog, kneeLow, kneeHigh, gamma, &t);
+    if (cr_tonemap(ctx_, &t, scene.xres, scene.yres, data.data()) != CR_OK)
+        throw std::runtime_error(std::string("chiaro: tonemap failed: ") + cr_last_error(ctx_));
 }
 
 namespace {

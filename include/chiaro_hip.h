@@ -25,6 +25,8 @@
  *                        the same loop split over ranks by 32x32 tiles (no
  *                        reference counterpart: the reference's only split is the
  *                        OpenMP row loop, src/rayTracer.cpp:55).
+ *   cr_tonemap_setup / cr_tonemap / cr_tonemap_device
+ *                        RayTracer::normalizeImage (src/rayTracer.cpp:172-222)
  *   cr_intersect         KDTree::intersectRay       (src/kdtree.cpp:210-216)
  *   cr_intersect_shadow  KDTree::intersectShadowRay (src/kdtree.cpp:283-290)
  *
@@ -165,6 +167,25 @@ int cr_render(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, floa
 /* Same, blending into the caller-owned device buffer d_frame [yres][xres][3]
  * (only this rank's tiles are touched) on `stream` (hipStream_t, NULL = null stream). */
 int cr_render_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *d_frame, void *stream);
+
+/* Tonemap (RayTracer::normalizeImage, src/rayTracer.cpp:196-222).  The scalar
+ * setup -- m = 2^(exposure+2.47393), s = 255*2^(-3.5*gamma), kl = 2^kneeLow and
+ * the knee factor f = findKneeF(2^kneeHigh, 2^3.5 - kl) (:172-194) -- is host
+ * arithmetic, done once by cr_tonemap_setup exactly as the reference does it.
+ * The per-pixel transform runs on the device, one byte per thread:
+ *   x = max(0, v - defog) * m;  x > kl: x = kl + log(1 + (x-kl)*f)/f;
+ *   byte = (uint8) clamp(x^gamma * s, 0, 255)
+ * with the rows flipped as the reference writes `data` ((yres-1-y)*xres + x). */
+typedef struct cr_tonemap_params {
+    float m, s, kl, f, defog, gamma;
+} cr_tonemap_params;
+void cr_tonemap_setup(float exposure, float defog, float kneeLow, float kneeHigh, float gamma, cr_tonemap_params *out);
+/* d_rgb [yres][xres][3] fp32 (row 0 = top) -> d_bytes [yres][xres][3] uint8,
+ * both device buffers, on `stream`. */
+int cr_tonemap_device(cr_ctx *ctx, const cr_tonemap_params *t, uint32_t xres, uint32_t yres, const float *d_rgb,
+                      uint8_t *d_bytes, void *stream);
+/* The ctx's accumulator (the frame of the last cr_render) -> host bytes. */
+int cr_tonemap(cr_ctx *ctx, const cr_tonemap_params *t, uint32_t xres, uint32_t yres, uint8_t *bytes_out);
 
 /* Batch means (no blend) of this rank's tiles into compact d_tiles
  * [cr_tiles_for_rank][tile][tile][3]. */

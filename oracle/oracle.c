@@ -779,3 +779,41 @@ float or_light_surface(const float p[9]) {
     v3 A = V3(p[0], p[1], p[2]), B = V3(p[3], p[4], p[5]), Cc = V3(p[6], p[7], p[8]);
     return 0.5f * length3(cross(sub(B, A), sub(Cc, A)));
 }
+
+/* ---------------------------------------------- tonemap (normalizeImage) -- */
+/* rayTracer.cpp:172-194: knee and findKneeF (glibc logf on a float argument:
+ * the double x*f + 1 is converted to float at the call, the quotient is double) */
+static inline float tm_knee(double x, double f) { return logf((float)(x * f + 1)) / f; }
+static float tm_find_knee_f(float x, float y) {
+    float f0 = 0, f1 = 1;
+    while (tm_knee(x, f1) > y) {
+        f0 = f1;
+        f1 = f1 * 2;
+    }
+    for (int i = 0; i < 30; ++i) {
+        float f2 = (f0 + f1) / 2;
+        if (tm_knee(x, f2) < y) f1 = f2;
+        else f0 = f2;
+    }
+    return (f0 + f1) / 2;
+}
+/* rayTracer.cpp:196-222: rgb [yres][xres][3] (row 0 = top) -> out with the rows
+ * flipped as the reference's data; glibc powf / logf throughout. */
+void or_tonemap(const float *rgb, uint32_t xres, uint32_t yres, float exposure, float defog, float kneeLow,
+                float kneeHigh, float gamma, uint8_t *out) {
+    const float m = powf(2.f, exposure + 2.47393f);
+    const float s = 255.f * powf(2.f, -3.5f * gamma);
+    const float kl = powf(2.f, kneeLow);
+    const float f = tm_find_knee_f(powf(2.f, kneeHigh), powf(2.f, 3.5f) - kl); /* C++ powf(2.f, 3.5) */
+    for (uint32_t y = 0; y < yres; y++)
+        for (uint32_t x = 0; x < xres; x++)
+            for (int ch = 0; ch < 3; ch++) {
+                float v = rgb[3 * ((size_t)y * xres + x) + ch];
+                v = std_max(0.f, v - defog);
+                v *= m;
+                if (v > kl) v = kl + tm_knee(v - kl, f);
+                const float w = powf(v, gamma) * s;
+                const float c = (w > 0.f ? w : 0.f) < 255.f ? (w > 0.f ? w : 0.f) : 255.f; /* glm::clamp */
+                out[3 * ((size_t)(yres - y - 1) * xres + x) + ch] = (uint8_t)c;
+            }
+}

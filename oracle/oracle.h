@@ -100,6 +100,9 @@ float or_glm_dot(const float a[3], const float b[3]);
 float or_glm_distance(const float a[3], const float b[3]);
 void or_material_normal(const float n[9], float out[3]);
 float or_light_surface(const float p[9]);
+/* rayTracer.cpp:172-222 normalizeImage (glibc powf / logf), rows flipped */
+void or_tonemap(const float *rgb, uint32_t xres, uint32_t yres, float exposure, float defog, float kneeLow,
+                float kneeHigh, float gamma, uint8_t *out);
 
 /* trig mode: 0 = shared correctly-rounded sincos (bit-exact with the HIP path),
  * 1 = glibc sinf/cosf exactly as src/brdf.cpp:52-53 calls them. */

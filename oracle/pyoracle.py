@@ -65,6 +65,8 @@ def lib():
             "or_glm_distance": (C.c_float, [FP, FP]),
             "or_material_normal": (None, [FP, FP]),
             "or_light_surface": (C.c_float, [FP]),
+            "or_tonemap": (None, [FP, C.c_uint32, C.c_uint32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
+                                  C.POINTER(C.c_uint8)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -190,6 +192,15 @@ def sincos(x):
 def rng_draws(seed, layer, pixel, sample, n):
     out = np.zeros(n, np.uint32)
     lib().or_rng_draws(seed, layer, pixel, sample, n, _p(out, C.c_uint32))
+    return out
+
+
+def tonemap(rgb, exposure, defog=0.0, knee_low=0.0, knee_high=5.0, gamma=2.2):
+    """rayTracer.cpp:196-222 on a [yres][xres][3] fp32 frame -> uint8 (rows flipped)."""
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    out = np.zeros(rgb.shape, np.uint8)
+    lib().or_tonemap(_p(rgb), rgb.shape[1], rgb.shape[0], exposure, defog, knee_low, knee_high, gamma,
+                     out.ctypes.data_as(C.POINTER(C.c_uint8)))
     return out
 
 
