@@ -120,7 +120,9 @@ def main():
     fr = DistributedFrame(dev, xres, yres, rank, world, tile, dist)
     tiles = fr.tiles
 
-    totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0}
+    totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0,
+              "trace_ms": [0.0, 0.0], "trace_launches": [0, 0]}
+    wavefront = args.kernel in (-1, 2)
 
     def step(layer, record):
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
@@ -131,6 +133,11 @@ def main():
             totals["kernel_ms"] += dev.last_kernel_ms()
             totals["px"] += c["pixels"]
             totals["launches"] += 1
+            if wavefront:
+                ts = dev.trace_stats()
+                for i, kind in enumerate(("closest", "shadow")):
+                    totals["trace_ms"][i] += ts[kind]["ms"]
+                    totals["trace_launches"][i] += ts[kind]["launches"]
 
     # Timed launches count only rays; the node/leaf/triangle counters of SURVEY §8d
     # (algorithmic bytes) come from one extra, untimed launch of the counting
@@ -175,6 +182,7 @@ def main():
     else:
         dev.render_tiles_device(cam, pc, tiles.data_ptr(), stream)
     cc = dev.counters()
+    cts = dev.trace_stats() if wavefront else None
     totals["bytes"] = ca.algorithmic_bytes(cc, cc["pixels"])
     totals["tritest"] = cc["tritest"]
     totals["count_rays"] = cc["closest"] + cc["shadow"]
@@ -182,19 +190,19 @@ def main():
     if rank == 0:
         value = rays_all / elapsed / 1e6
         kms = totals["kernel_ms"] / max(totals["launches"], 1)
-        bytes_per_launch = totals["bytes"]  # counting pass: one launch, same size as a timed one
-        achieved = bytes_per_launch / (kms / 1e3) / 1e9 if kms > 0 else 0.0
-        # measured fabric bytes of one render pass, from the committed rocprofv3 PMC
-        # summary of this same configuration (scripts/prof_summary.py); null if none
-        traffic = None
+        pass_bytes = totals["bytes"]  # counting pass: one render pass, same size as a timed one
+        pass_gbs = pass_bytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+        # measured fabric bytes from the committed rocprofv3 PMC summary of this same
+        # configuration (scripts/prof_summary.py); null if none
+        pj = None
         pmc = ROOT / "profiles" / ("pmc_%s.json" % args.config)
         if pmc.exists():
             try:
                 pj = json.loads(pmc.read_text())
-                if pj.get("spp") == spp and pj.get("n_gpus") == world:
-                    traffic = pj.get("hbm_bytes_per_launch")
+                if not (pj.get("spp") == spp and pj.get("n_gpus") == world):
+                    pj = None
             except Exception:
-                traffic = None
+                pj = None
         kernel_name = {0: "persistent megakernel", 1: "thread per pixel", 2: "wavefront"}[
             args.kernel if args.kernel >= 0 else 2]
         cpu = None
@@ -202,6 +210,45 @@ def main():
             cpu = cpu_baseline(model.triangles(), model.textures(), info, info["leaf_size"], cam.as_array(), xres,
                                yres, spp, k, seed,
                                args.cpu_budget)
+        pass_view = {"kernels": "render pass (%s): all kernels of one layer" % kernel_name, "ms": round(kms, 3),
+                     "algorithmic_bytes": int(pass_bytes), "achieved": round(pass_gbs, 2),
+                     "traffic": pj.get("hbm_bytes_per_launch") if pj else None}
+        if wavefront:
+            # dominant kernel: the trace kernel instantiation with the most device time.  Its
+            # algorithmic bytes (8 per inner node, 8 per leaf, 40 per triangle test)
+            # come from the counting pass, its launch time from HIP events around every launch
+            # of the timed passes (on the render stream).
+            i = 0 if totals["trace_ms"][0] >= totals["trace_ms"][1] else 1
+            kind = ("closest", "shadow")[i]
+            launches = max(totals["trace_launches"][i], 1)
+            avg_ms = totals["trace_ms"][i] / launches
+            per_pass_launches = totals["trace_launches"][i] / max(totals["launches"], 1)
+            t = cts[kind]
+            kbytes = (8 * t["inner"] + 8 * t["leaf"] + 40 * t["tritest"]) / max(per_pass_launches, 1)
+            achieved = kbytes / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+            tr = (pj or {}).get("trace", {}).get(kind)
+            other = ("closest", "shadow")[1 - i]
+            to = cts[other]
+            o_launch = max(totals["trace_launches"][1 - i], 1)
+            o_ms = totals["trace_ms"][1 - i] / o_launch
+            o_bytes = (8 * to["inner"] + 8 * to["leaf"] + 40 * to["tritest"]) / max(
+                totals["trace_launches"][1 - i] / max(totals["launches"], 1), 1)
+            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 5),
+                        "traffic": tr["fabric_bytes_per_launch"] if tr else None,
+                        "kernel": "wf_trace<%s> (%s-ray kd traversal, wavefront.hip)" % (kind, kind),
+                        "avg_launch_ms": round(avg_ms, 3), "launches": launches,
+                        "algorithmic_bytes_per_launch": int(kbytes),
+                        "rocprof_avg_launch_ms": round(tr["avg_ns"] / 1e6, 3) if tr else None,
+                        "other_trace": {"kernel": "wf_trace<%s>" % other, "avg_launch_ms": round(o_ms, 3),
+                                        "algorithmic_bytes_per_launch": int(o_bytes),
+                                        "achieved": round(o_bytes / (o_ms / 1e3) / 1e9, 2) if o_ms > 0 else 0.0},
+                        "pass": pass_view}
+        else:
+            roofline = {"bound": "hbm", "achieved": round(pass_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(pass_gbs / HBM_PEAK_GBS, 5), "traffic": pass_view["traffic"],
+                        "kernel": pass_view["kernels"], "kernel_ms": round(kms, 3),
+                        "algorithmic_bytes_per_launch": int(pass_bytes)}
         label = {"sponza": "sponza_standin (Sponza-Crytek stand-in, ~261k tris) 1920x1080",
                  "sponza_4k": "sponza_standin (Sponza-Crytek stand-in) 3840x2160",
                  "nanobox": "nanobox_standin (textured nanosuit-in-a-box stand-in, ~20k tris) 1920x1080",
@@ -222,13 +269,7 @@ def main():
             "config": {"workload": label, "spp_per_step": spp, "k": k, "tile": tile,
                        "parallelism": "tile-split x%d" % world, "rays": int(rays_all),
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         # unit = one render pass (one layer): the wavefront's camera, K x (closest
-                         # trace, shade, shadow trace, bounce) and sum kernels, HIP events around
-                         # them on their stream; the two trace kernels are ~95% of it
-                         "kernel": "render pass (%s)" % kernel_name, "kernel_ms": round(kms, 3),
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+            "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -82,6 +82,11 @@ class ChiaroSceneInfo(C.Structure):
                 ("obj_path", C.c_char * 1024), ("render_path", C.c_char * 1024)]
 
 
+class CrTraceStats(C.Structure):
+    _fields_ = [("launches", C.c_uint64 * 2), ("ms", C.c_double * 2), ("inner", C.c_uint64 * 2),
+                ("leaf", C.c_uint64 * 2), ("tritest", C.c_uint64 * 2)]
+
+
 class CrTonemapParams(C.Structure):
     _fields_ = [(n, C.c_float) for n in ("m", "s", "kl", "f", "defog", "gamma")]
 
@@ -100,7 +105,7 @@ _host = None
 # Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
                "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_intersect",
-               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_set_option", "cr_synchronize",
+               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize",
                "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
@@ -147,6 +152,7 @@ def libs():
     _sig(hip, "cr_intersect_shadow", C.c_int, [P, C.c_uint32, FP, FP, FP, UP, UP])
     _sig(hip, "cr_get_counters", C.c_int, [P, C.POINTER(CrCounters)])
     _sig(hip, "cr_last_kernel_ms", C.c_float, [P])
+    _sig(hip, "cr_get_trace_stats", C.c_int, [P, C.POINTER(CrTraceStats)])
     _sig(hip, "cr_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
     _sig(hip, "cr_synchronize", C.c_int, [P])
     _sig(hip, "cr_tonemap_setup", None, [C.c_float] * 5 + [C.POINTER(CrTonemapParams)])
@@ -405,6 +411,15 @@ class Device:
 
     def last_kernel_ms(self) -> float:
         return float(libs()[0].cr_last_kernel_ms(self._c))
+
+    def trace_stats(self) -> dict:
+        """cr_get_trace_stats: per trace-kernel instantiation ("closest", "shadow") of the
+        last wavefront render -- launches, summed event ms, inner / leaf / tritest."""
+        t = CrTraceStats()
+        self._chk(libs()[0].cr_get_trace_stats(self._c, C.byref(t)), "cr_get_trace_stats")
+        return {name: {"launches": int(t.launches[i]), "ms": float(t.ms[i]), "inner": int(t.inner[i]),
+                       "leaf": int(t.leaf[i]), "tritest": int(t.tritest[i])}
+                for i, name in enumerate(("closest", "shadow"))}
 
     def set_option(self, key: str, value: int):
         self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")

@@ -35,6 +35,8 @@ struct cr_ctx {
     void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
     size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
     cr_counters last{};
+    cr::TraceEvents tev;     // wavefront trace launches of the last render (cr_get_trace_stats)
+    cr_trace_stats last_trace{};
     // options
     // Defaults from sweeps on MI355X, sponza stand-in 1080p x 128 spp:
     //   wavefront (kernel 2), trace variant 2, refill 64/56/48, sorted queues: 1071 Mray/s
@@ -247,6 +249,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 return r;
             A.pathbuf = (float4 *)c->d_pathbuf;
         }
+        c->tev.n = 0;
         HIPCHK(hipEventRecord(c->ev0, st));
         for (uint32_t s0 = 0; s0 < p->spp; s0 += (uint32_t)chunk) {
             A.s0 = s0;
@@ -259,7 +262,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                     W.w0 = w0;
                     W.P = std::min(P, A.n_work - w0);
                     HIPCHK(hipMemsetAsync(W.cnt, 0, cr::WF_CNT * sizeof(uint32_t), st));
-                    e = cr::launch_wavefront_chunk(A, W, c->num_cus, st);
+                    e = cr::launch_wavefront_chunk(A, W, c->num_cus, st, &c->tev);
                 }
                 W.P = P;
             } else {
@@ -284,6 +287,21 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     c->last = cr_counters{h[0], h[1],  h[2],  h[3],  h[4],  h[5],  h[6],  h[7], h[8],
                           h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16],
                           h[17], h[18], h[19], h[20], h[21]};
+    c->last_trace = cr_trace_stats{};
+    if (c->kernel == 2) {
+        for (int i = 0; i < c->tev.n; i++) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, c->tev.ev[2 * i], c->tev.ev[2 * i + 1]));
+            const int k = c->tev.kind[i];
+            c->last_trace.launches[k]++;
+            c->last_trace.ms[k] += ms;
+        }
+        for (int k = 0; k < 2; k++) {
+            c->last_trace.inner[k] = h[cr::CTR_TRACE + 3 * k];
+            c->last_trace.leaf[k] = h[cr::CTR_TRACE + 3 * k + 1];
+            c->last_trace.tritest[k] = h[cr::CTR_TRACE + 3 * k + 2];
+        }
+    }
     return CR_OK;
 }
 
@@ -334,6 +352,9 @@ void cr_destroy(cr_ctx *c) {
         if (c->d_counters) hipFree(c->d_counters);
         if (c->d_work) hipFree(c->d_work);
         if (c->ev0) hipEventDestroy(c->ev0);
+        for (int i = 0; i < 2 * c->tev.cap; i++) hipEventDestroy(c->tev.ev[i]);
+        delete[] c->tev.ev;
+        delete[] c->tev.kind;
         if (c->ev1) hipEventDestroy(c->ev1);
         if (c->stream) hipStreamDestroy(c->stream);
     }
@@ -644,6 +665,12 @@ int cr_get_counters(cr_ctx *c, cr_counters *out) {
 }
 
 float cr_last_kernel_ms(cr_ctx *c) { return c ? c->last_ms : 0.f; }
+
+int cr_get_trace_stats(cr_ctx *c, cr_trace_stats *out) {
+    if (!c || !out) return CR_E_INVALID;
+    *out = c->last_trace;
+    return CR_OK;
+}
 
 int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!c || !key) return CR_E_INVALID;

@@ -10,6 +10,9 @@ enum { MODE_BLEND = 0, MODE_TILES = 1 };
 // (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
 enum { REC_STRIDE = 3 };
 enum { CTR_N = 22, CTR_SLOTS = 32 }; // Ctr fields (cr_counters order); device counter buffer entries
+// Counting builds of the wavefront trace kernels also tally inner / leaf / tritest per
+// instantiation: slots CTR_TRACE + 3 * kind + {0, 1, 2}, kind 0 = closest, 1 = shadow.
+enum { CTR_TRACE = 24 };
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one
 // texel past the row/image end for coords == 1.0 (src/mesh.cpp:23-30) and three
@@ -120,8 +123,16 @@ struct WfArgs {
 inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 1 + 2 + WF_STATE + 2 * K) * 16 + 8 + 16; } // + sort
 int num_wf_variants();
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
+// HIP events bracketing every trace launch (start, stop), recorded on the launch
+// stream; kind[i] = 0 closest / 1 shadow for pair i.  Grown by the launcher.
+struct TraceEvents {
+    hipEvent_t *ev = nullptr; // [2 * cap]
+    int *kind = nullptr;      // [cap]
+    int cap = 0, n = 0;
+};
 // One chunk: camera generation + K x (closest, shade, shadow, bounce).
-int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st);
+int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st,
+                           TraceEvents *te = nullptr);
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
                hipStream_t st);
 size_t wf_sort_tmp_bytes(uint32_t n, int key_bits);

@@ -230,6 +230,17 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
     else c.closest = issued;
     flush_counters(A.counters, c, 0u);
+    if (FULL) { // per-instantiation split of the §8d work counters (bench roofline)
+        unsigned long long *base = A.counters + CTR_TRACE + 3 * (SHADOW ? 1 : 0);
+        const uint32_t v[3] = {c.inner, c.leaf, c.tritest};
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            unsigned long long x = v[i];
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+            if ((threadIdx.x & 63) == 0 && x) atomicAdd(&base[i], x);
+        }
+    }
 }
 
 // ----------------------------------------------------------------- shade --
@@ -402,7 +413,36 @@ static const uint32_t *order_queue(const WfArgs &W, const uint32_t *dcount, hipS
     return vals[sel];
 }
 
-int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st) {
+// Records a (start, stop) event pair around one trace launch when te is given.
+static int trace_event(TraceEvents *te, hipStream_t st, int kind, bool start) {
+    if (!te) return 0;
+    if (start) {
+        if (te->n == te->cap) {
+            const int cap = te->cap ? 2 * te->cap : 64;
+            hipEvent_t *ev = new hipEvent_t[2 * (size_t)cap];
+            int *kd = new int[cap];
+            for (int i = 0; i < 2 * te->cap; i++) ev[i] = te->ev[i];
+            for (int i = 0; i < te->cap; i++) kd[i] = te->kind[i];
+            for (int i = 2 * te->cap; i < 2 * cap; i++)
+                if (int e = (int)hipEventCreate(&ev[i])) {
+                    for (int j = 2 * te->cap; j < i; j++) hipEventDestroy(ev[j]);
+                    delete[] ev;
+                    delete[] kd;
+                    return e;
+                }
+            delete[] te->ev;
+            delete[] te->kind;
+            te->ev = ev;
+            te->kind = kd;
+            te->cap = cap;
+        }
+        te->kind[te->n] = kind;
+        return (int)hipEventRecord(te->ev[2 * te->n], st);
+    }
+    return (int)hipEventRecord(te->ev[2 * te->n++ + 1], st);
+}
+
+int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st, TraceEvents *te) {
     WfArgs W = W0;
     const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks;
@@ -414,10 +454,14 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     W.order = nullptr; // generation-1 closest rays: path order is already coherent (camera rays)
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
+        if ((err = trace_event(te, st, 0, true))) break;
         hipLaunchKernelGGL(v.closest, dim3(blocks), dim3(blk), lds, st, A, W, g);
+        if ((err = trace_event(te, st, 0, false))) break;
         hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, st, A, W, g);
         W.order = order_queue(W, W.cnt + 64 + g, st, err);
+        if (err || (err = trace_event(te, st, 1, true))) break;
         hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
+        if ((err = trace_event(te, st, 1, false))) break;
         hipLaunchKernelGGL(wf_bounce, dim3(sgrid), dim3(256), 0, st, A, W, g);
         if (g < (uint32_t)A.K) W.order = order_queue(W, W.cnt + g + 1, st, err);
     }

@@ -207,6 +207,18 @@ int cr_intersect_shadow(cr_ctx *ctx, uint32_t n, const float *orig, const float 
 int cr_get_counters(cr_ctx *ctx, cr_counters *out);
 /* Device time (ms) of the last render kernel, HIP events on its own stream. */
 float cr_last_kernel_ms(cr_ctx *ctx);
+/* Per-kernel view of the last wavefront render ("kernel" 2) for the roofline:
+ * the trace kernel's two instantiations, [0] closest-hit (KDTree::intersectRay,
+ * src/kdtree.cpp:210-281) and [1] shadow (intersectShadowRay, :283-344) -- their
+ * launch counts, summed device time (a HIP event pair around every launch, on
+ * the render stream) and, after a counting render ("counters" 1), their
+ * inner-node / leaf / triangle-test tallies (zero after a lean render). */
+typedef struct cr_trace_stats {
+    uint64_t launches[2];
+    double ms[2];
+    uint64_t inner[2], leaf[2], tritest[2];
+} cr_trace_stats;
+int cr_get_trace_stats(cr_ctx *ctx, cr_trace_stats *out);
 /* Kernel variant / tuning knobs: "kernel" (0 = persistent wave-regeneration,
  * 1 = one-thread-per-pixel), "variant" (persistent-kernel build, 0 = default),
  * "refill" (1..64: idle lanes of a wave that trigger a path-state step in the

@@ -76,10 +76,19 @@ def main():
     out = {"render_pass": dict(per_pass), "kernels": summary, "passes_profiled": passes}
     (prof / ("%s_pmc.json" % tag)).write_text(json.dumps(out, indent=1, sort_keys=True))
     spp = int(sys.argv[sys.argv.index("--spp") + 1]) if "--spp" in sys.argv else 128
+    # the trace kernel's lean instantiations (bench.py roofline): fabric bytes per launch
+    trace = {}
+    for n, e in summary.items():
+        m = re.search(r"wf_trace<(true|false), false,", n)
+        if m and "fabric_bytes_total" in e:
+            trace["shadow" if m.group(1) == "true" else "closest"] = {
+                "kernel": n, "calls": e["calls"], "avg_ns": e["avg_ns"],
+                "fabric_bytes_per_launch": e["fabric_bytes_total"] / e["calls"]}
     (prof / ("pmc_%s.json" % config)).write_text(json.dumps({
         "source": "profiles/%s_pmc.json" % tag, "spp": spp, "n_gpus": 1,
         "hbm_bytes_per_launch": per_pass["fabric_bytes"],
-        "unit": "one render pass (all timed kernels of one layer)",
+        "trace": trace,
+        "unit": "one render pass (all timed kernels of one layer); trace: per launch of that kernel",
         "note": "2*FETCH_SIZE+WRITE_SIZE (KiB) summed over the pass's dispatches; includes Infinity-Cache hits "
                 "(upper bound on HBM bytes)",
     }, indent=1))
