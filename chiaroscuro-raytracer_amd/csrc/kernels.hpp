@@ -118,13 +118,15 @@ struct WfArgs {
     int world_keys;      // g > 0: world-space origin keys for queues whose rays start at hits of
                          // generation >= g (shadow queue g, closest queue g + 1); 0: pixel keys only
     uint32_t world_bits; // bits per axis of the origin's Morton code
+    uint32_t tail_min;   // a closest queue shorter than this hands the rest of the chunk to wf_tail (0: never)
 };
 // rays 2x2 float4, hit 1, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs
 inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 1 + 2 + WF_STATE + 2 * K) * 16 + 8 + 16; } // + sort
 int num_wf_variants();
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
+void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks);
 // HIP events bracketing every trace launch (start, stop), recorded on the launch
-// stream; kind[i] = 0 closest / 1 shadow for pair i.  Grown by the launcher.
+// stream; kind[i] = 0 closest / 1 shadow / 2 tail for pair i.  Grown by the launcher.
 struct TraceEvents {
     hipEvent_t *ev = nullptr; // [2 * cap]
     int *kind = nullptr;      // [cap]

@@ -243,15 +243,89 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     }
 }
 
+// ------------------------------------------------------ per-path bodies --
+// Shared by the per-generation kernels (wf_shade / wf_bounce) and the tail
+// kernel (wf_tail), so both execute the same arithmetic on the same state.
+
+// RayTracer::sendRay up to the shadow query (rayTracer.cpp:80-99) for a closest
+// hit of path p: hit shading, emission, NEE light sample.  Writes the path state
+// (slot 3's w -- the shadow-queue slot -- is left to the caller).  Returns the
+// shadow ray in `sh` when the scene has lights.
+struct ShadowRay {
+    f3 o, d;
+    float dist;
+    uint32_t light;
+};
+__device__ __forceinline__ bool shade_path(const RenderArgs &A, const WfArgs &W, uint32_t p, f3 ro, uint4 h,
+                                           bool &textured, ShadowRay &sh) {
+    const DevScene &S = A.S;
+    const uint32_t k = __float_as_uint(PS(W, 0, p).w);
+    const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
+    textured = hs.textured;
+    Rng rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
+    f3 contrib = mk(0.f, 0.f, 0.f), next = add(hs.p, muls(hs.normal, 0.001f));
+    bool nee = false;
+    if (S.nlights) {
+        const Nee e = sample_light(S, hs.p, hs.normal, hs.fcol, rng);
+        contrib = e.contrib;
+        next = e.origin;
+        sh.o = e.origin;
+        sh.d = e.dir;
+        sh.dist = e.distance;
+        sh.light = e.light;
+        nee = true;
+    }
+    PS(W, 0, p) = pk(hs.direct, k);
+    PS(W, 1, p) = pk(hs.fcol, rng.key);
+    PS(W, 2, p) = pk(hs.normal, rng.ctr);
+    PS(W, 4, p) = pk(next, 0u);
+    PS(W, 3, p) = pk(contrib, NO_SLOT);
+    return nee;
+}
+
+// NEE result, then the k == K cut, BRDF sample and Russian roulette
+// (rayTracer.cpp:100-134) of path p.  visible: the shadow ray found no occluder
+// (false when there was no NEE).  Returns true when the path continues with the
+// closest ray (org, wi) of its next bounce; otherwise the path is finished.
+__device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W, uint32_t p, bool visible, f3 &org,
+                                            f3 &wi) {
+    const float4 s0 = PS(W, 0, p), s1 = PS(W, 1, p), s2 = PS(W, 2, p), s3 = PS(W, 3, p);
+    const uint32_t k = __float_as_uint(s0.w);
+    f3 direct = ld3(s0);
+    const f3 fcol = ld3(s1), normal = ld3(s2);
+    Rng rng{__float_as_uint(s1.w), __float_as_uint(s2.w)};
+    if (visible) direct = add(direct, ld3(s3));
+    if ((int)k == A.K) {
+        finish_path(A, W, p, k, direct);
+        return false;
+    }
+    const float sx = rng_uniform(rng, -1.f, 1.f);
+    const float sy = rng_uniform(rng, -1.f, 1.f);
+    float pdf;
+    sample_wi(normal, sx, sy, wi, pdf);
+    const float Kmax = std_max(std_max(fcol.x, fcol.y), fcol.z);
+    if (pdf == 0.f || rng_uniform(rng, 0.f, 1.f) > Kmax) {
+        finish_path(A, W, p, k, direct);
+        return false;
+    }
+    const float cosine = fabsf(dot(normal, wi));
+    const f3 w = divs(muls(fcol, cosine), pdf * Kmax);
+    W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(direct, 0u);
+    W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
+    PS(W, 0, p) = pk(direct, k + 1);
+    PS(W, 2, p).w = __uint_as_float(rng.ctr);
+    org = ld3(PS(W, 4, p));
+    return true;
+}
+
 // ----------------------------------------------------------------- shade --
-// RayTracer::sendRay up to the shadow query (rayTracer.cpp:80-99) for every
-// closest ray of generation g; misses finish their path with the background.
+// Every closest ray of generation g: misses finish their path with the
+// background, hits are shaded and append their NEE ray to the shadow queue.
 __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
     __shared__ uint32_t app[5];
     if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
     __syncthreads();
-    const DevScene &S = A.S;
     const uint32_t n = *cnt_closest(W, g);
     const float4 *rays = W.ray[g & 1];
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
@@ -266,43 +340,21 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
         const uint32_t p = __float_as_uint(r0.w);
         const bool hit = in && h.w != 0u;
         bool textured = false, nee = false;
-        f3 sorg = mk(0.f, 0.f, 0.f), sdir = mk(0.f, 0.f, 0.f);
-        float sdist = 0.f;
-        uint32_t slight = 0;
+        ShadowRay sh = {mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, 0u};
         if (in && !hit) {
             if (p != NO_PATH) finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
         } else if (hit) {
-            const uint32_t k = __float_as_uint(PS(W, 0, p).w);
-            const HitShade hs = shade_hit(S, ld3(r0), h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
-            textured = hs.textured;
-            Rng rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
-            f3 contrib = mk(0.f, 0.f, 0.f), next = add(hs.p, muls(hs.normal, 0.001f));
-            if (S.nlights) {
-                const Nee e = sample_light(S, hs.p, hs.normal, hs.fcol, rng);
-                contrib = e.contrib;
-                next = e.origin;
-                sorg = e.origin;
-                sdir = e.dir;
-                sdist = e.distance;
-                slight = e.light;
-                nee = true;
-            }
-            PS(W, 0, p) = pk(hs.direct, k);
-            PS(W, 1, p) = pk(hs.fcol, rng.key);
-            PS(W, 2, p) = pk(hs.normal, rng.ctr);
-            PS(W, 4, p) = pk(next, 0u);
-            if (!nee) PS(W, 3, p) = pk(contrib, NO_SLOT);
-            else PS(W, 3, p) = pk(contrib, 0u); // slot set below
+            nee = shade_path(A, W, p, ld3(r0), h, textured, sh);
         }
         const uint32_t j = block_append(cnt_shadow(W, g), nee, app);
         if (nee) {
             PS(W, 3, p).w = __uint_as_float(j);
-            W.sray[2 * (size_t)j] = pk(sorg, p);
-            W.sray[2 * (size_t)j + 1] = make_float4(sdir.x, sdir.y, sdir.z, sdist);
-            W.sexcl[j] = slight;
+            W.sray[2 * (size_t)j] = pk(sh.o, p);
+            W.sray[2 * (size_t)j + 1] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
+            W.sexcl[j] = sh.light;
             if (W.sort) {
-                W.key[0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sorg, sdir)
-                                                                            : sort_key(A, W, p, sdir);
+                W.key[0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
+                                                                            : sort_key(A, W, p, sh.d);
                 W.perm[0][j] = j;
             }
         }
@@ -313,9 +365,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
 }
 
 // ---------------------------------------------------------------- bounce --
-// NEE result, then the k == K cut, BRDF sample and Russian roulette
-// (rayTracer.cpp:100-134): either the next closest ray of generation g + 1 or
-// the end of the path.
+// Either the next closest ray of generation g + 1 or the end of the path.
 __global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ uint32_t app[5];
     const uint32_t n = *cnt_closest(W, g);
@@ -324,39 +374,13 @@ __global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         bool live = i < n && W.hit[min(i, n - 1)].w != 0u;
-        uint32_t p = 0, k = 0;
+        uint32_t p = 0;
         bool cont = false;
         f3 wi = mk(0.f, 0.f, 0.f), org = mk(0.f, 0.f, 0.f);
         if (live) {
             p = __float_as_uint(rays[2 * (size_t)i].w);
-            const float4 s0 = PS(W, 0, p), s1 = PS(W, 1, p), s2 = PS(W, 2, p), s3 = PS(W, 3, p);
-            k = __float_as_uint(s0.w);
-            f3 direct = ld3(s0);
-            const f3 fcol = ld3(s1), normal = ld3(s2);
-            Rng rng{__float_as_uint(s1.w), __float_as_uint(s2.w)};
-            const uint32_t slot = __float_as_uint(s3.w);
-            if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(s3));
-            if ((int)k == A.K) {
-                finish_path(A, W, p, k, direct);
-            } else {
-                const float sx = rng_uniform(rng, -1.f, 1.f);
-                const float sy = rng_uniform(rng, -1.f, 1.f);
-                float pdf;
-                sample_wi(normal, sx, sy, wi, pdf);
-                const float Kmax = std_max(std_max(fcol.x, fcol.y), fcol.z);
-                if (pdf == 0.f || rng_uniform(rng, 0.f, 1.f) > Kmax) {
-                    finish_path(A, W, p, k, direct);
-                } else {
-                    const float cosine = fabsf(dot(normal, wi));
-                    const f3 w = divs(muls(fcol, cosine), pdf * Kmax);
-                    W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(direct, 0u);
-                    W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
-                    PS(W, 0, p) = pk(direct, k + 1);
-                    PS(W, 2, p).w = __uint_as_float(rng.ctr);
-                    org = ld3(PS(W, 4, p));
-                    cont = true;
-                }
-            }
+            const uint32_t slot = __float_as_uint(PS(W, 3, p).w);
+            cont = bounce_path(A, W, p, slot != NO_SLOT && W.occ[slot] == 0u, org, wi);
         }
         const uint32_t j = block_append(cnt_closest(W, g + 1), cont, app);
         if (cont) {
@@ -369,6 +393,109 @@ __global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_
             }
         }
     }
+}
+
+// ------------------------------------------------------------------ tail --
+// The last generations in ONE launch: every path left in the closest queue of
+// generation g0 runs to its end on one lane -- closest query, shade, shadow
+// query, bounce, next closest query ... -- with the same per-path bodies as
+// the per-generation kernels.  Small late generations are bound by their
+// longest query (a per-launch latency floor of ~1.3 ms on the sponza stand-in);
+// here the paths' chains overlap instead of paying that floor per generation
+// and kind.  Lanes refill from the queue (one atomicAdd per wave) when `refill`
+// of them are idle or none is busy; a lane with a finished query advances its
+// path at once.
+template <bool FULL, int R, int MINW>
+__global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uint32_t g0) {
+    extern __shared__ uint2 ring_lds[];
+    __shared__ unsigned long long tl[T_N];
+    if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
+    __syncthreads();
+    const DevScene &S = A.S;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t n = *cnt_closest(W, g0);
+    uint32_t *work = work_closest(W, g0);
+    const float4 *rays = W.ray[g0 & 1];
+    Ctr c = {};
+    uint32_t state = ST_NEED_WORK, p = 0, exclude = 0, nclosest = 0, nshadow = 0;
+    f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
+    Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
+    // start the next closest query of path p from (o, d); a root-box miss is a MISS at once
+    auto start_closest = [&]() {
+        nclosest++;
+        state = trav_begin(S, o, d, false, 0.f, T) ? ST_CLOSEST : ST_MISS;
+    };
+    for (;;) {
+        const uint64_t need_m = __ballot(state == ST_NEED_WORK);
+        const uint64_t busy_m = __ballot(state == ST_CLOSEST || state == ST_SHADOW);
+        if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= A.refill)) {
+            const uint32_t leader = (uint32_t)__ffsll((long long)need_m) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(work, (uint32_t)__popcll(need_m));
+            base = __shfl(base, (int)leader, 64);
+            if (state == ST_NEED_WORK) {
+                const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(need_m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need_m, 0u));
+                if (idx >= n) {
+                    state = ST_DONE;
+                } else {
+                    const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
+                    o = ld3(r0);
+                    d = ld3(r1);
+                    p = __float_as_uint(r0.w);
+                    if (p != NO_PATH) start_closest(); // dead camera ray of a partial tile: no query
+                }
+            }
+        }
+        // advance every lane whose query has a result, until it has a new query or is idle
+        while (state >= ST_HIT) {
+            if (state == ST_MISS) {
+                finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
+                state = ST_NEED_WORK;
+            } else if (state == ST_HIT) {
+                bool textured = false;
+                ShadowRay sh;
+                tally(tl, T_HIT, true);
+                const bool nee = shade_path(A, W, p, o, make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
+                                                                 __float_as_uint(d.y), 1u),
+                                            textured, sh);
+                tally(tl, T_TEXHIT, textured);
+                if (nee) {
+                    o = sh.o;
+                    d = sh.d;
+                    exclude = sh.light;
+                    nshadow++;
+                    state = trav_begin(S, o, d, true, sh.dist, T) ? ST_SHADOW : ST_VISIBLE;
+                } else {
+                    state = ST_OCCLUDED; // no NEE term: bounce without the contribution
+                }
+            } else { // ST_VISIBLE / ST_OCCLUDED: the bounce
+                f3 org, wi;
+                if (bounce_path(A, W, p, state == ST_VISIBLE, org, wi)) {
+                    o = org;
+                    d = wi;
+                    start_closest();
+                } else {
+                    state = ST_NEED_WORK;
+                }
+            }
+        }
+        const bool busy = state == ST_CLOSEST || state == ST_SHADOW;
+        if (!__any(busy)) {
+            if (!__any(state != ST_DONE)) break;
+            continue;
+        }
+        if (busy) {
+            const bool shadow = state == ST_SHADOW;
+            const uint32_t r = trav_round<R, FULL, 1, false, true, false>(S, ring_lds, W.gstack, W.gstride, gid, o, d,
+                                                                        shadow, exclude, T, c);
+            if (r != (shadow ? ST_SHADOW : ST_CLOSEST)) state = r;
+        }
+    }
+    c.closest = nclosest;
+    c.shadow = nshadow;
+    flush_counters(A.counters, c, 0u);
+    flush_tallies(A, tl);
 }
 
 // --------------------------------------------------------------- launch --
@@ -394,15 +521,19 @@ void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &bloc
     blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)v.waves_per_simd; // 4 SIMDs, 4 waves/block
 }
 
-// Sorts the queue whose keys the previous kernel wrote; returns the permutation
-// for the trace kernel (nullptr: trace in queue order).
-static const uint32_t *order_queue(const WfArgs &W, const uint32_t *dcount, hipStream_t st, int &err) {
-    if (!W.sort) return nullptr;
+// Length of a queue (device counter -> host; waits for the stream).
+static uint32_t queue_len(const uint32_t *dcount, hipStream_t st, int &err) {
     uint32_t n = 0;
     if ((err = (int)hipMemcpyAsync(&n, dcount, sizeof(n), hipMemcpyDeviceToHost, st)) ||
         (err = (int)hipStreamSynchronize(st)))
-        return nullptr;
-    if (n < W.sort_min) return nullptr;
+        return 0;
+    return n;
+}
+
+// Sorts the queue of n rays whose keys the previous kernel wrote; returns the
+// permutation for the trace kernel (nullptr: trace in queue order).
+static const uint32_t *order_queue(const WfArgs &W, uint32_t n, hipStream_t st, int &err) {
+    if (!W.sort || err || n < W.sort_min) return nullptr;
     uint32_t *keys[2] = {W.key[0], W.key[1]}, *vals[2] = {W.perm[0], W.perm[1]};
     size_t tb = W.sort_tmp_bytes;
     const int sel = sort_queue(keys, vals, n, W.key_bits, W.sort_tmp, tb, st);
@@ -442,28 +573,53 @@ static int trace_event(TraceEvents *te, hipStream_t st, int kind, bool start) {
     return (int)hipEventRecord(te->ev[2 * te->n++ + 1], st);
 }
 
+// Tail kernel builds: lean and counting; 4 waves/SIMD (the path bodies need more
+// registers than the trace kernels' 64).
+enum { TAIL_MINW = 4 };
+void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks) {
+    block = 256;
+    blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * TAIL_MINW;
+}
+
 int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st, TraceEvents *te) {
     WfArgs W = W0;
     const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
-    uint32_t blk, blocks;
+    uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
-    if (W.gstride < blk * blocks) return (int)hipErrorInvalidValue;
+    wf_tail_geometry(num_cus, tblk, tblocks);
+    if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds = (size_t)v.ring * blk * sizeof(uint2);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
     int err = 0;
     W.order = nullptr; // generation-1 closest rays: path order is already coherent (camera rays)
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
+    // closest queue of generation g holds n rays; below W.tail_min the rest of the
+    // chunk runs in one wf_tail launch
+    uint32_t n = W.P;
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
+        if (n < W.tail_min) {
+            const size_t tlds = (size_t)8 * tblk * sizeof(uint2);
+            if ((err = trace_event(te, st, 2, true))) break;
+            if (A.full_counters)
+                hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+            else
+                hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+            err = trace_event(te, st, 2, false);
+            break;
+        }
         if ((err = trace_event(te, st, 0, true))) break;
         hipLaunchKernelGGL(v.closest, dim3(blocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, 0, false))) break;
         hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, st, A, W, g);
-        W.order = order_queue(W, W.cnt + 64 + g, st, err);
+        W.order = W.sort ? order_queue(W, queue_len(W.cnt + 64 + g, st, err), st, err) : nullptr;
         if (err || (err = trace_event(te, st, 1, true))) break;
         hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, 1, false))) break;
         hipLaunchKernelGGL(wf_bounce, dim3(sgrid), dim3(256), 0, st, A, W, g);
-        if (g < (uint32_t)A.K) W.order = order_queue(W, W.cnt + g + 1, st, err);
+        if (g < (uint32_t)A.K) {
+            n = (W.sort || W.tail_min) ? queue_len(W.cnt + g + 1, st, err) : W.P;
+            W.order = n >= W.tail_min ? order_queue(W, n, st, err) : nullptr;
+        }
     }
     return err ? err : (int)hipGetLastError();
 }

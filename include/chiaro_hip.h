@@ -209,14 +209,16 @@ int cr_get_counters(cr_ctx *ctx, cr_counters *out);
 float cr_last_kernel_ms(cr_ctx *ctx);
 /* Per-kernel view of the last wavefront render ("kernel" 2) for the roofline:
  * the trace kernel's two instantiations, [0] closest-hit (KDTree::intersectRay,
- * src/kdtree.cpp:210-281) and [1] shadow (intersectShadowRay, :283-344) -- their
- * launch counts, summed device time (a HIP event pair around every launch, on
- * the render stream) and, after a counting render ("counters" 1), their
- * inner-node / leaf / triangle-test tallies (zero after a lean render). */
+ * src/kdtree.cpp:210-281) and [1] shadow (intersectShadowRay, :283-344), and
+ * [2] the tail kernel that runs the last, small generations -- launch counts,
+ * summed device time (a HIP event pair around every launch, on the render
+ * stream) and, for [0] and [1] after a counting render ("counters" 1), the
+ * inner-node / leaf / triangle-test tallies of those launches (zero after a
+ * lean render; [2] is not split by query kind and stays zero). */
 typedef struct cr_trace_stats {
-    uint64_t launches[2];
-    double ms[2];
-    uint64_t inner[2], leaf[2], tritest[2];
+    uint64_t launches[3];
+    double ms[3];
+    uint64_t inner[3], leaf[3], tritest[3];
 } cr_trace_stats;
 int cr_get_trace_stats(cr_ctx *ctx, cr_trace_stats *out);
 /* Kernel variant / tuning knobs: "kernel" (0 = persistent wave-regeneration,

@@ -38,7 +38,9 @@ def main():
             else:
                 k = n.split("(")[0].split("::")[-1]
             acc[k] = acc.get(k, 0.0) + ms
-        print(json.dumps({"pass_ms": round(tot, 1), "counting": counting,
+        wall = (max(int(r["End_Timestamp"]) for r in p) - int(p[0]["Start_Timestamp"])) / 1e6
+        print(json.dumps({"pass_ms": round(tot, 1), "wall_ms": round(wall, 1), "gaps_ms": round(wall - tot, 1),
+                          "counting": counting,
                           "phases_ms": {k: round(v, 1) for k, v in acc.items()}}))
 
 

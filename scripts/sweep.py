@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--grid", action="append", default=[], help="option=v1,v2,...")
+    ap.add_argument("--nranks", type=int, default=1, help="render rank 0's tiles of an N-way tile split")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -40,6 +41,9 @@ def main():
     xres, yres, k, seed = info["xres"], info["yres"], info["k"], info["seed"]
     cam = ca.camera(info["VP"], info["LA"], info["UP"], info["yview"], xres, yres)
     frame = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda")
+    if args.nranks > 1:
+        p0 = ca.render_params(xres, yres, args.spp, k, seed, layer=1, rank=0, nranks=args.nranks)
+        frame = torch.zeros((ca.Device.tiles_for_rank(p0, 0), 32, 32, 3), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     dev.set_option("counters", 0)
     keys, values = [], []
@@ -54,8 +58,11 @@ def main():
         for cfg in configs:
             for key, v in zip(keys, cfg):
                 dev.set_option(key, v)
-            p = ca.render_params(xres, yres, args.spp, k, seed, layer=1)
-            dev.render_device(cam, p, frame.data_ptr(), stream)
+            p = ca.render_params(xres, yres, args.spp, k, seed, layer=1, rank=0, nranks=args.nranks)
+            if args.nranks > 1:
+                dev.render_tiles_device(cam, p, frame.data_ptr(), stream)
+            else:
+                dev.render_device(cam, p, frame.data_ptr(), stream)
             torch.cuda.synchronize()
             c = dev.counters()
             if ref is None:

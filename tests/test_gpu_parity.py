@@ -69,6 +69,30 @@ def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
+@pytest.mark.parametrize("tail_min", [1 << 30, 12000, 3000])
+def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min):
+    """wf_tail (the last generations of a chunk in one launch, per-path bodies
+    shared with wf_shade / wf_bounce): from generation 1 (every queue is below
+    1 << 30) and from later generations, counting and lean builds."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4)), (cornell, (64, 64, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_tail_min", tail_min)
+        try:
+            g, gc, o, oc = _render_both(ca, pair, x, y, s)
+            pair.dev.set_option("counters", 0)
+            g_lean = pair.dev.render(pair.camera(ca, x, y), ca.render_params(x, y, s, 6, 0xC41A05C0))
+            ts = pair.dev.trace_stats()
+        finally:
+            pair.dev.set_option("counters", 1)
+            pair.dev.set_option("wf_tail_min", 1 << 20)
+        assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
+        assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
+        assert {k: gc[k] for k in ORACLE_KEYS} == oc
+        assert ts["tail"]["launches"] == 1
+        if tail_min == 1 << 30:
+            assert ts["closest"]["launches"] == 0 and ts["shadow"]["launches"] == 0
+
+
 @pytest.mark.parametrize("kernel", [0, 1, 2])
 def test_nanobox_textured_bitexact(ca, nanobox, kernel):
     """C3 stand-in: RGB / RGBA / 1-channel textures, wrapped UVs, UV == 1 seams,
