@@ -66,6 +66,10 @@ __device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool s
 //   [slot][thread] (blockDim.x threads), deeper ones spill to gstk
 //   [depth][gstride].  On pop the interval is [current tmax, entry.tmax]: the
 //   current tmax equals the push-time tsplit (stack invariant).
+// (A wave-level mailbox -- per wave in LDS, the lanes for which a triangle was
+// a geometric miss in their current query, so a uniform leaf skips it when all
+// active lanes know it -- is exact too and measured 3% slower: the LDS lookup
+// serialises behind every scalar record load.)
 // (Speculative descent -- lanes that reached their leaf early descending toward
 // the next one, Aila & Laine's postponed leaves -- is exact here too but
 // measured slower: the merged descent loop costs more than the idle lanes.)

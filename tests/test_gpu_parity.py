@@ -55,7 +55,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
     wave-uniform nodes / leaves) renders the same bits."""
@@ -103,13 +103,27 @@ def test_nanobox_textured_bitexact(ca, nanobox, kernel):
     assert oc["texhit"] > oc["hit"] // 2 and o.mean() > 0.01
 
 
+LEAN_KEYS = ("closest", "shadow", "hit", "texhit", "paths", "pixels")
+
+
 def _render_both(ca, pair, xres, yres, spp, k=6, seed=0xC41A05C0, layer=1, kernel=None, accum=None):
+    """Counting build (all counters, compared with the oracle by the callers) AND
+    the lean build the timed renders use (its own trace variant; per-query
+    counters only), which must give the same bits."""
     cam = pair.camera(ca, xres, yres)
     p = ca.render_params(xres, yres, spp, k, seed, layer=layer)
     if kernel is not None:
         pair.dev.set_option("kernel", kernel)
     g = pair.dev.render(cam, p, None if accum is None else accum[0].copy())
     gc = pair.dev.counters()
+    pair.dev.set_option("counters", 0)
+    try:
+        g_lean = pair.dev.render(cam, p, None if accum is None else accum[0].copy())
+        lc = pair.dev.counters()
+    finally:
+        pair.dev.set_option("counters", 1)
+    assert_bitwise(g_lean, g, "lean vs counting build %dx%dx%d" % (xres, yres, spp))
+    assert {key: lc[key] for key in LEAN_KEYS} == {key: gc[key] for key in LEAN_KEYS}
     o, oc = pair.oracle.render(cam.as_array(), xres, yres, spp, k, seed, layer=layer,
                                pixels=None if accum is None else accum[1].copy())
     return g, gc, o, oc
