@@ -487,7 +487,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
         }
         if (busy) {
             const bool shadow = state == ST_SHADOW;
-            const uint32_t r = trav_round<R, FULL, 1, false, true, false>(S, ring_lds, W.gstack, W.gstride, gid, o, d,
+            const uint32_t r = trav_round<R, FULL, 1, false, true, true>(S, ring_lds, W.gstack, W.gstride, gid, o, d,
                                                                         shadow, exclude, T, c);
             if (r != (shadow ? ST_SHADOW : ST_CLOSEST)) state = r;
         }

@@ -5,6 +5,7 @@ counting launch (FULL build) is marked "counting" and is not a timed pass.
 """
 import csv
 import json
+import re
 import sys
 
 
@@ -26,9 +27,12 @@ def main():
             if "wf_trace<false" in n:
                 g += 1
                 k = "g%d closest" % g
-                counting |= "false, true," in n
+                counting |= re.search(r"wf_trace<false, true,", n) is not None
             elif "wf_trace<true" in n:
                 k = "g%d shadow" % g
+            elif "wf_tail" in n:
+                k = "tail (g%d..)" % (g + 1)
+                counting |= "wf_tail<true" in n
             elif "rocprim" in n:
                 k = "sort"
             elif "wf_shade" in n or "wf_bounce" in n:
