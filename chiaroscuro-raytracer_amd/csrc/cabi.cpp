@@ -21,6 +21,7 @@ struct cr_ctx {
     std::string err;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    cr::WfStreams wfs{nullptr, nullptr, nullptr}; // wavefront side stream + fork / join events
     float last_ms = 0.f;
     // scene
     bool has_scene = false;
@@ -185,7 +186,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(1, (1ull << 31) / std::max<uint32_t>(A.n_items, 1)));
         chunk = std::min<uint64_t>(chunk, p->spp);
         const bool chunked = chunk < p->spp;
-        if (int r = grow(c, &c->d_gstack, c->gstack_bytes, cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
+        // wavefront: a second stack-overflow area for the closest trace that runs beside a shadow trace
+        if (int r = grow(c, &c->d_gstack, c->gstack_bytes,
+                         (wf ? 2 : 1) * cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
             return r;
         if (int r = grow(c, &c->d_samples, c->samples_bytes, per_sample * chunk)) return r;
         if (chunked)
@@ -196,12 +199,12 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         cr::WfArgs W{};
         if (wf) {
             // path slots per wavefront chunk, and the queues / state carved from one buffer
-            // ... at most ~40% of the currently free HBM (the buffer is reused, so only a
+            // ... at most ~45% of the currently free HBM (the buffer is reused, so only a
             // growth needs the headroom)
             uint64_t P = std::min<uint64_t>((uint64_t)A.n_items * chunk, c->wf_paths);
             size_t freeb = 0, totalb = 0;
             if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-                const uint64_t cap = (uint64_t)((freeb + c->wf_bytes) * 0.4) / cr::wf_bytes_per_path(p->k);
+                const uint64_t cap = (uint64_t)((freeb + c->wf_bytes) * 0.45) / cr::wf_bytes_per_path(p->k);
                 P = std::max<uint64_t>(std::min<uint64_t>(P, cap), std::min<uint64_t>(P, 1u << 20));
             }
             const size_t f4 = 16 * (size_t)P;
@@ -213,8 +216,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             const uint64_t nworld = (1ull << (3 * c->wf_world_bits)) * c->wf_dir_res * c->wf_dir_res;
             while (c->wf_world_keys && key_bits < 32 && (1ull << key_bits) < nworld) key_bits++;
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits) : 0;
-            const size_t need = (4 + 1 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 8 * (size_t)P +
-                                (c->wf_sort ? 16 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
+            const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 8 * (size_t)P +
+                                (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
                                 8192;
             if (int r = grow(c, &c->d_wf, c->wf_bytes, need)) return r;
             char *b = (char *)c->d_wf;
@@ -225,7 +228,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             };
             W.ray[0] = (float4 *)take(2 * f4);
             W.ray[1] = (float4 *)take(2 * f4);
-            W.hit = (uint4 *)take(f4);
+            W.hit[0] = (uint4 *)take(f4);
+            W.hit[1] = (uint4 *)take(f4);
             W.sray = (float4 *)take(2 * f4);
             W.ps = (float4 *)take(cr::WF_STATE * f4);
             W.dw = (float4 *)take(2 * (size_t)p->k * f4);
@@ -241,14 +245,16 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             W.world_bits = c->wf_world_bits;
             W.tail_min = c->wf_tail_min;
             if (c->wf_sort) {
-                for (int i = 0; i < 2; i++) {
-                    W.key[i] = (uint32_t *)take(4 * (size_t)P);
-                    W.perm[i] = (uint32_t *)take(4 * (size_t)P);
-                }
+                for (int q = 0; q < 2; q++)
+                    for (int i = 0; i < 2; i++) {
+                        W.key[q][i] = (uint32_t *)take(4 * (size_t)P);
+                        W.perm[q][i] = (uint32_t *)take(4 * (size_t)P);
+                    }
                 W.sort_tmp = take(sort_tmp);
                 W.sort_tmp_bytes = sort_tmp;
             }
             W.gstack = A.gstack;
+            W.gstack2 = A.gstack + (size_t)c->stack_depth * A.gstride;
             W.gstride = A.gstride;
             W.P = (uint32_t)P;
         } else {
@@ -269,7 +275,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                     W.w0 = w0;
                     W.P = std::min(P, A.n_work - w0);
                     HIPCHK(hipMemsetAsync(W.cnt, 0, cr::WF_CNT * sizeof(uint32_t), st));
-                    e = cr::launch_wavefront_chunk(A, W, c->num_cus, st, &c->tev);
+                    e = cr::launch_wavefront_chunk(A, W, c->num_cus, st, c->wfs, &c->tev);
                 }
                 W.P = P;
             } else {
@@ -336,6 +342,9 @@ cr_ctx *cr_create(int device) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->wfs.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->wfs.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->wfs.join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->d_counters, cr::CTR_SLOTS * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_work, 16 * sizeof(uint32_t)) != hipSuccess) {
@@ -364,6 +373,9 @@ void cr_destroy(cr_ctx *c) {
         delete[] c->tev.kind;
         if (c->ev1) hipEventDestroy(c->ev1);
         if (c->stream) hipStreamDestroy(c->stream);
+        if (c->wfs.side) hipStreamDestroy(c->wfs.side);
+        if (c->wfs.fork) hipEventDestroy(c->wfs.fork);
+        if (c->wfs.join) hipEventDestroy(c->wfs.join);
     }
     delete c;
 }

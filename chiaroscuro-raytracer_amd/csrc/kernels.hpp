@@ -94,7 +94,7 @@ struct WfArgs {
     uint32_t P;       // path slots of this chunk
     uint32_t w0;      // first work item of the chunk
     float4 *ray[2];   // closest rays, by generation parity: [2P] {o, path}, {d, 0}
-    uint4 *hit;       // [P] closest result of ray i: {tri, bx bits, by bits, 1} / {0, 0, 0, 0}
+    uint4 *hit[2];    // [P] closest result of ray i of generation g in hit[g & 1]: {tri, bx, by bits, 1} / 0
     float4 *sray;     // [2P] shadow rays {o, path}, {d, limit}
     uint32_t *sexcl;  // [P] light triangle the shadow ray ignores
     uint32_t *occ;    // [P] shadow result of shadow ray j
@@ -102,11 +102,13 @@ struct WfArgs {
     float4 *ps;       // [WF_STATE][P] path state
     float4 *dw;       // [2K][P] (direct, w) per bounce
     uint2 *gstack;    // trace kernels' stack overflow [depth][gstride]
+    uint2 *gstack2;   // ... of a closest trace running beside a shadow trace
     uint32_t gstride; // threads of the trace grid
-    // queue ordering (raysort.hip): shade / bounce write a sort key and the slot
-    // per appended ray into key[0] / perm[0]; the host sorts them and hands the
-    // trace kernel the permutation (`order`, null = queue order)
-    uint32_t *key[2], *perm[2];
+    // queue ordering (raysort.hip): wf_shade writes a sort key and the slot per
+    // appended ray into key[q][0] / perm[q][0] (q = 0 shadow queue, 1 closest
+    // queue); the host sorts them (double buffers [q][0..1]) and hands the trace
+    // kernel the permutation (`order`, null = queue order)
+    uint32_t *key[2][2], *perm[2][2];
     const uint32_t *order;
     void *sort_tmp;
     size_t sort_tmp_bytes;
@@ -120,8 +122,13 @@ struct WfArgs {
     uint32_t world_bits; // bits per axis of the origin's Morton code
     uint32_t tail_min;   // a closest queue shorter than this hands the rest of the chunk to wf_tail (0: never)
 };
-// rays 2x2 float4, hit 1, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs
-inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 1 + 2 + WF_STATE + 2 * K) * 16 + 8 + 16; } // + sort
+// rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms
+inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32; }
+// Second stream and fork / join events of a render (shadow trace g beside closest trace g + 1).
+struct WfStreams {
+    hipStream_t side;
+    hipEvent_t fork, join;
+};
 int num_wf_variants();
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
 void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks);
@@ -132,8 +139,8 @@ struct TraceEvents {
     int *kind = nullptr;      // [cap]
     int cap = 0, n = 0;
 };
-// One chunk: camera generation + K x (closest, shade, shadow, bounce).
-int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st,
+// One chunk: camera, closest 1, then per generation shade, shadow || next closest, resolve.
+int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st, const WfStreams &ss,
                            TraceEvents *te = nullptr);
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
                hipStream_t st);

@@ -7,14 +7,17 @@
 // split by phase into kernels that exchange work through queues in HBM:
 //
 //   wf_camera                 one closest ray per path of the chunk
+//   wf_trace<closest>(1)
 //   for g = 1..K:
-//     wf_trace<closest>(g)    resumable traversal only: small register file,
-//                             high occupancy, lanes refill from the queue
 //     wf_shade(g)             hit reconstruction, emission, NEE light sample
-//                             -> shadow-ray queue (rayTracer.cpp:80-99)
-//     wf_trace<shadow>(g)
-//     wf_bounce(g)            NEE result, RR, BRDF sample -> next closest queue,
-//                             or finish the path (back-to-front fold)
+//                             -> shadow queue g, then BRDF sample + RR -> closest
+//                             queue g + 1 (rayTracer.cpp:80-134: none of these
+//                             draws depends on the shadow result)
+//     wf_trace<shadow>(g)  ||  wf_trace<closest>(g + 1)    two streams: each
+//                             launch's tail (its longest queries) overlaps the other
+//     wf_resolve(g)           NEE result -> the bounce's direct term; paths that
+//                             ended at bounce g are folded into samples[w]
+//   (a closest queue below wf_tail_min: the rest of the chunk runs in wf_tail)
 //
 // Paths keep their (pixel, sample) RNG keys and draw order, and every path
 // writes its radiance to samples[w]; sum_samples adds them per pixel in sample
@@ -199,13 +202,13 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         d = ld3(r1);
                         if (SHADOW) exclude = W.sexcl[idx];
                         if (!SHADOW && __float_as_uint(r0.w) == NO_PATH) {
-                            W.hit[idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
+                            W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
                         } else if (issued++, trav_begin(S, o, d, SHADOW, r1.w, T)) {
                             state = busy_st;
                         } else if (SHADOW) {
                             W.occ[idx] = 0u; // culled: visible (kdtree.cpp:285-287)
                         } else {
-                            W.hit[idx] = make_uint4(0u, 0u, 0u, 0u);
+                            W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u);
                         }
                     }
                 }
@@ -220,7 +223,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                                                                  exclude, T, c);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
-                else W.hit[idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
+                else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
                                                            __float_as_uint(d.y), 1u)
                                               : make_uint4(0u, 0u, 0u, 0u);
                 state = ST_NEED_WORK;
@@ -318,9 +321,56 @@ __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W
     return true;
 }
 
+// Everything of RayTracer::sendRay at a closest hit of bounce k = g that does not
+// need the shadow result (rayTracer.cpp:80-134): hit shading, emission, the NEE
+// light sample and -- for k < K -- the BRDF sample and Russian roulette, in the
+// reference's draw order.  The NEE term stays pending for wf_resolve:
+// dw[2(k-1)] = {direct, shadow slot (set by the caller)}, PS3 = {contrib, ended}.
+// A continuing path gets W_k in dw[2(k-1)+1] and its next closest ray (org, wi).
+__device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t k, f3 ro, uint4 h,
+                                           bool &textured, ShadowRay &sh, bool &cont, f3 &org, f3 &wi) {
+    const DevScene &S = A.S;
+    const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
+    textured = hs.textured;
+    Rng rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
+    f3 contrib = mk(0.f, 0.f, 0.f), next = add(hs.p, muls(hs.normal, 0.001f));
+    bool nee = false;
+    if (S.nlights) {
+        const Nee e = sample_light(S, hs.p, hs.normal, hs.fcol, rng);
+        contrib = e.contrib;
+        next = e.origin;
+        sh.o = e.origin;
+        sh.d = e.dir;
+        sh.dist = e.distance;
+        sh.light = e.light;
+        nee = true;
+    }
+    cont = false;
+    if ((int)k != A.K) {
+        const float sx = rng_uniform(rng, -1.f, 1.f);
+        const float sy = rng_uniform(rng, -1.f, 1.f);
+        float pdf;
+        sample_wi(hs.normal, sx, sy, wi, pdf);
+        const float Kmax = std_max(std_max(hs.fcol.x, hs.fcol.y), hs.fcol.z);
+        if (!(pdf == 0.f || rng_uniform(rng, 0.f, 1.f) > Kmax)) {
+            const float cosine = fabsf(dot(hs.normal, wi));
+            const f3 w = divs(muls(hs.fcol, cosine), pdf * Kmax);
+            W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
+            PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), k + 1);
+            PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
+            org = next;
+            cont = true;
+        }
+    }
+    W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(hs.direct, NO_SLOT);
+    PS(W, 3, p) = pk(contrib, cont ? 0u : 1u);
+    return nee;
+}
+
 // ----------------------------------------------------------------- shade --
 // Every closest ray of generation g: misses finish their path with the
-// background, hits are shaded and append their NEE ray to the shadow queue.
+// background; hits run shade_next and append their NEE ray to shadow queue g and
+// their next ray to closest queue g + 1.
 __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
     __shared__ uint32_t app[5];
@@ -328,34 +378,47 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
     __syncthreads();
     const uint32_t n = *cnt_closest(W, g);
     const float4 *rays = W.ray[g & 1];
+    const uint4 *hits = W.hit[g & 1];
+    float4 *next_rays = W.ray[(g + 1) & 1];
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         const bool in = i < n;
         uint4 h = make_uint4(0u, 0u, 0u, 0u);
         float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (in) {
-            h = W.hit[i];
+            h = hits[i];
             r0 = rays[2 * (size_t)i];
         }
         const uint32_t p = __float_as_uint(r0.w);
         const bool hit = in && h.w != 0u;
-        bool textured = false, nee = false;
+        bool textured = false, nee = false, cont = false;
         ShadowRay sh = {mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, 0u};
+        f3 org = mk(0.f, 0.f, 0.f), wi = mk(0.f, 0.f, 0.f);
         if (in && !hit) {
-            if (p != NO_PATH) finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
+            if (p != NO_PATH) finish_path(A, W, p, g, mk(A.bg[0], A.bg[1], A.bg[2]));
         } else if (hit) {
-            nee = shade_path(A, W, p, ld3(r0), h, textured, sh);
+            nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi);
         }
         const uint32_t j = block_append(cnt_shadow(W, g), nee, app);
         if (nee) {
-            PS(W, 3, p).w = __uint_as_float(j);
+            W.dw[(size_t)(2 * (g - 1)) * W.P + p].w = __uint_as_float(j);
             W.sray[2 * (size_t)j] = pk(sh.o, p);
             W.sray[2 * (size_t)j + 1] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
             W.sexcl[j] = sh.light;
             if (W.sort) {
-                W.key[0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
-                                                                            : sort_key(A, W, p, sh.d);
-                W.perm[0][j] = j;
+                W.key[0][0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
+                                                                               : sort_key(A, W, p, sh.d);
+                W.perm[0][0][j] = j;
+            }
+        }
+        const uint32_t jc = block_append(cnt_closest(W, g + 1), cont, app);
+        if (cont) {
+            next_rays[2 * (size_t)jc] = pk(org, p);
+            next_rays[2 * (size_t)jc + 1] = pk(wi, 0u);
+            if (W.sort) {
+                W.key[1][0][jc] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
+                                                                                : sort_key(A, W, p, wi);
+                W.perm[1][0][jc] = jc;
             }
         }
         tally(tl, T_HIT, hit);
@@ -364,34 +427,24 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
     flush_tallies(A, tl);
 }
 
-// ---------------------------------------------------------------- bounce --
-// Either the next closest ray of generation g + 1 or the end of the path.
-__global__ void __launch_bounds__(256) wf_bounce(RenderArgs A, WfArgs W, uint32_t g) {
-    __shared__ uint32_t app[5];
+// --------------------------------------------------------------- resolve --
+// After the shadow trace of generation g: the bounce's direct term
+// D_k = direct + (visible ? contrib : 0) (rayTracer.cpp:96-99), and the
+// back-to-front fold of every path that ended at this bounce.
+__global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32_t g) {
     const uint32_t n = *cnt_closest(W, g);
     const float4 *rays = W.ray[g & 1];
-    float4 *next_rays = W.ray[(g + 1) & 1];
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-        const uint32_t i = base + threadIdx.x;
-        bool live = i < n && W.hit[min(i, n - 1)].w != 0u;
-        uint32_t p = 0;
-        bool cont = false;
-        f3 wi = mk(0.f, 0.f, 0.f), org = mk(0.f, 0.f, 0.f);
-        if (live) {
-            p = __float_as_uint(rays[2 * (size_t)i].w);
-            const uint32_t slot = __float_as_uint(PS(W, 3, p).w);
-            cont = bounce_path(A, W, p, slot != NO_SLOT && W.occ[slot] == 0u, org, wi);
-        }
-        const uint32_t j = block_append(cnt_closest(W, g + 1), cont, app);
-        if (cont) {
-            next_rays[2 * (size_t)j] = pk(org, p);
-            next_rays[2 * (size_t)j + 1] = pk(wi, 0u);
-            if (W.sort) {
-                W.key[0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
-                                                                            : sort_key(A, W, p, wi);
-                W.perm[0][j] = j;
-            }
-        }
+    const uint4 *hits = W.hit[g & 1];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (hits[i].w == 0u) continue;
+        const uint32_t p = __float_as_uint(rays[2 * (size_t)i].w);
+        float4 &dk = W.dw[(size_t)(2 * (g - 1)) * W.P + p];
+        const float4 d4 = dk, s3 = PS(W, 3, p);
+        const uint32_t slot = __float_as_uint(d4.w);
+        f3 direct = ld3(d4);
+        if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(s3));
+        if (__float_as_uint(s3.w)) finish_path(A, W, p, g, direct);
+        else dk = pk(direct, 0u);
     }
 }
 
@@ -530,11 +583,12 @@ static uint32_t queue_len(const uint32_t *dcount, hipStream_t st, int &err) {
     return n;
 }
 
-// Sorts the queue of n rays whose keys the previous kernel wrote; returns the
-// permutation for the trace kernel (nullptr: trace in queue order).
-static const uint32_t *order_queue(const WfArgs &W, uint32_t n, hipStream_t st, int &err) {
+// Sorts the queue of n rays whose keys wf_shade wrote into key / perm set `set`
+// (0 shadow, 1 closest); returns the permutation for the trace kernel (nullptr:
+// trace in queue order).
+static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStream_t st, int &err) {
     if (!W.sort || err || n < W.sort_min) return nullptr;
-    uint32_t *keys[2] = {W.key[0], W.key[1]}, *vals[2] = {W.perm[0], W.perm[1]};
+    uint32_t *keys[2] = {W.key[set][0], W.key[set][1]}, *vals[2] = {W.perm[set][0], W.perm[set][1]};
     size_t tb = W.sort_tmp_bytes;
     const int sel = sort_queue(keys, vals, n, W.key_bits, W.sort_tmp, tb, st);
     if (sel < 0) {
@@ -581,7 +635,8 @@ void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks) {
     blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * TAIL_MINW;
 }
 
-int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st, TraceEvents *te) {
+int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st, const WfStreams &ss,
+                           TraceEvents *te) {
     WfArgs W = W0;
     const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
@@ -591,34 +646,61 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     const size_t lds = (size_t)v.ring * blk * sizeof(uint2);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
     int err = 0;
-    W.order = nullptr; // generation-1 closest rays: path order is already coherent (camera rays)
+    // the rest of the chunk from closest queue g on, in one launch
+    auto tail = [&](uint32_t g) {
+        const size_t tlds = (size_t)8 * tblk * sizeof(uint2);
+        W.order = nullptr;
+        if ((err = trace_event(te, st, 2, true))) return;
+        if (A.full_counters)
+            hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+        else
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+        err = trace_event(te, st, 2, false);
+    };
+    // closest trace of generation g on stream s; its stack overflow rows are the
+    // second half of gstack when it runs beside a shadow trace
+    auto closest = [&](uint32_t g, hipStream_t s, const uint32_t *order, uint2 *gstack) {
+        WfArgs Wc = W;
+        Wc.order = order;
+        Wc.gstack = gstack;
+        if ((err = trace_event(te, s, 0, true))) return;
+        hipLaunchKernelGGL(v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
+        err = trace_event(te, s, 0, false);
+    };
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
-    // closest queue of generation g holds n rays; below W.tail_min the rest of the
-    // chunk runs in one wf_tail launch
-    uint32_t n = W.P;
+    if (W.P < W.tail_min) {
+        tail(1);
+        return err ? err : (int)hipGetLastError();
+    }
+    closest(1, st, nullptr, W.gstack); // camera rays: path order is already coherent
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
-        if (n < W.tail_min) {
-            const size_t tlds = (size_t)8 * tblk * sizeof(uint2);
-            if ((err = trace_event(te, st, 2, true))) break;
-            if (A.full_counters)
-                hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
-            else
-                hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
-            err = trace_event(te, st, 2, false);
-            break;
-        }
-        if ((err = trace_event(te, st, 0, true))) break;
-        hipLaunchKernelGGL(v.closest, dim3(blocks), dim3(blk), lds, st, A, W, g);
-        if ((err = trace_event(te, st, 0, false))) break;
         hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, st, A, W, g);
-        W.order = W.sort ? order_queue(W, queue_len(W.cnt + 64 + g, st, err), st, err) : nullptr;
-        if (err || (err = trace_event(te, st, 1, true))) break;
+        uint32_t cnt[2] = {0u, 0u}; // shadow queue g, closest queue g + 1
+        if ((err = (int)hipMemcpyAsync(&cnt[0], W.cnt + 64 + g, 4, hipMemcpyDeviceToHost, st)) ||
+            (err = (int)hipMemcpyAsync(&cnt[1], W.cnt + g + 1, 4, hipMemcpyDeviceToHost, st)) ||
+            (err = (int)hipStreamSynchronize(st)))
+            break;
+        const uint32_t nc = g < (uint32_t)A.K ? cnt[1] : 0u;
+        const bool next = nc >= W.tail_min && nc > 0; // closest g + 1 as its own launch, beside shadow g
+        const uint32_t *order_s = order_queue(W, 0, cnt[0], st, err);
+        const uint32_t *order_c = next ? order_queue(W, 1, nc, st, err) : nullptr;
+        if (err) break;
+        if (next) {
+            if ((err = (int)hipEventRecord(ss.fork, st)) || (err = (int)hipStreamWaitEvent(ss.side, ss.fork, 0))) break;
+            closest(g + 1, ss.side, order_c, W.gstack2);
+            if (err) break;
+        }
+        W.order = order_s;
+        if ((err = trace_event(te, st, 1, true))) break;
         hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, 1, false))) break;
-        hipLaunchKernelGGL(wf_bounce, dim3(sgrid), dim3(256), 0, st, A, W, g);
-        if (g < (uint32_t)A.K) {
-            n = (W.sort || W.tail_min) ? queue_len(W.cnt + g + 1, st, err) : W.P;
-            W.order = n >= W.tail_min ? order_queue(W, n, st, err) : nullptr;
+        hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        if (next) {
+            if ((err = (int)hipEventRecord(ss.join, ss.side)) || (err = (int)hipStreamWaitEvent(st, ss.join, 0)))
+                break;
+        } else {
+            if (nc > 0) tail(g + 1);
+            break;
         }
     }
     return err ? err : (int)hipGetLastError();
