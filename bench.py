@@ -121,7 +121,7 @@ def main():
     tiles = fr.tiles
 
     totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0,
-              "trace_ms": [0.0, 0.0], "trace_launches": [0, 0]}
+              "trace_ms": [0.0] * 4, "trace_launches": [0] * 4}
     wavefront = args.kernel in (-1, 2)
 
     def step(layer, record):
@@ -135,7 +135,7 @@ def main():
             totals["launches"] += 1
             if wavefront:
                 ts = dev.trace_stats()
-                for i, kind in enumerate(("closest", "shadow")):
+                for i, kind in enumerate(ca.TRACE_KINDS):
                     totals["trace_ms"][i] += ts[kind]["ms"]
                     totals["trace_launches"][i] += ts[kind]["launches"]
 
@@ -214,35 +214,35 @@ def main():
                      "algorithmic_bytes": int(pass_bytes), "achieved": round(pass_gbs, 2),
                      "traffic": pj.get("hbm_bytes_per_launch") if pj else None}
         if wavefront:
-            # dominant kernel: the trace kernel instantiation with the most device time.  Its
-            # algorithmic bytes (8 per inner node, 8 per leaf, 40 per triangle test)
-            # come from the counting pass, its launch time from HIP events around every launch
-            # of the timed passes (on the render stream).
-            i = 0 if totals["trace_ms"][0] >= totals["trace_ms"][1] else 1
-            kind = ("closest", "shadow")[i]
-            launches = max(totals["trace_launches"][i], 1)
-            avg_ms = totals["trace_ms"][i] / launches
-            per_pass_launches = totals["trace_launches"][i] / max(totals["launches"], 1)
-            t = cts[kind]
-            kbytes = (8 * t["inner"] + 8 * t["leaf"] + 40 * t["tritest"]) / max(per_pass_launches, 1)
-            achieved = kbytes / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
-            tr = (pj or {}).get("trace", {}).get(kind)
-            other = ("closest", "shadow")[1 - i]
-            to = cts[other]
-            o_launch = max(totals["trace_launches"][1 - i], 1)
-            o_ms = totals["trace_ms"][1 - i] / o_launch
-            o_bytes = (8 * to["inner"] + 8 * to["leaf"] + 40 * to["tritest"]) / max(
-                totals["trace_launches"][1 - i] / max(totals["launches"], 1), 1)
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 5),
+            # Dominant kernel: the camera-ray trace (wf_trace, generation-1 closest queries), the
+            # largest launch of a pass and the only trace that never runs beside another one.
+            # Algorithmic bytes (8 per inner node, 8 per leaf, 40 per triangle test)
+            # per kind from the counting pass; launch times from HIP event pairs around every
+            # launch of the timed passes, on the launch's stream.
+            def kind_view(kind):
+                i = ca.TRACE_KINDS.index(kind)
+                launches = totals["trace_launches"][i]
+                if not launches:
+                    return None
+                avg_ms = totals["trace_ms"][i] / launches
+                per_pass = launches / max(totals["launches"], 1)
+                t = cts[kind]
+                kb = (8 * t["inner"] + 8 * t["leaf"] + 40 * t["tritest"]) / max(per_pass, 1e-9)
+                tr = (pj or {}).get("trace", {}).get(kind)
+                return {"kernel": "wf_trace<%s>" % kind, "avg_launch_ms": round(avg_ms, 3), "launches": launches,
+                        "algorithmic_bytes_per_launch": int(kb),
+                        "achieved": round(kb / (avg_ms / 1e3) / 1e9, 2) if avg_ms > 0 else 0.0,
                         "traffic": tr["fabric_bytes_per_launch"] if tr else None,
-                        "kernel": "wf_trace<%s> (%s-ray kd traversal, wavefront.hip)" % (kind, kind),
-                        "avg_launch_ms": round(avg_ms, 3), "launches": launches,
-                        "algorithmic_bytes_per_launch": int(kbytes),
-                        "rocprof_avg_launch_ms": round(tr["avg_ns"] / 1e6, 3) if tr else None,
-                        "other_trace": {"kernel": "wf_trace<%s>" % other, "avg_launch_ms": round(o_ms, 3),
-                                        "algorithmic_bytes_per_launch": int(o_bytes),
-                                        "achieved": round(o_bytes / (o_ms / 1e3) / 1e9, 2) if o_ms > 0 else 0.0},
+                        "rocprof_avg_launch_ms": round(tr["avg_ns"] / 1e6, 3) if tr else None}
+            views = {k: kind_view(k) for k in ("camera", "closest", "shadow")}
+            dom = views["camera"] or views["closest"]
+            roofline = {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(dom["achieved"] / HBM_PEAK_GBS, 5), "traffic": dom["traffic"],
+                        "kernel": dom["kernel"] + " (camera-ray kd traversal, wavefront.hip)",
+                        "avg_launch_ms": dom["avg_launch_ms"], "launches": dom["launches"],
+                        "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
+                        "rocprof_avg_launch_ms": dom["rocprof_avg_launch_ms"],
+                        "other_traces": {k: v for k, v in views.items() if v is not None and v is not dom},
                         "pass": pass_view}
         else:
             roofline = {"bound": "hbm", "achieved": round(pass_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

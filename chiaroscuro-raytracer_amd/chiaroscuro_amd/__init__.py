@@ -82,9 +82,12 @@ class ChiaroSceneInfo(C.Structure):
                 ("obj_path", C.c_char * 1024), ("render_path", C.c_char * 1024)]
 
 
+TRACE_KINDS = ("camera", "closest", "shadow", "tail")  # cr_trace_stats order
+
+
 class CrTraceStats(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 3), ("ms", C.c_double * 3), ("inner", C.c_uint64 * 3),
-                ("leaf", C.c_uint64 * 3), ("tritest", C.c_uint64 * 3)]
+    _fields_ = [("launches", C.c_uint64 * 4), ("ms", C.c_double * 4), ("inner", C.c_uint64 * 4),
+                ("leaf", C.c_uint64 * 4), ("tritest", C.c_uint64 * 4)]
 
 
 class CrTonemapParams(C.Structure):
@@ -413,13 +416,13 @@ class Device:
         return float(libs()[0].cr_last_kernel_ms(self._c))
 
     def trace_stats(self) -> dict:
-        """cr_get_trace_stats: per trace-kernel instantiation ("closest", "shadow", "tail") of the
+        """cr_get_trace_stats: per trace-launch kind (TRACE_KINDS) of the
         last wavefront render -- launches, summed event ms, inner / leaf / tritest."""
         t = CrTraceStats()
         self._chk(libs()[0].cr_get_trace_stats(self._c, C.byref(t)), "cr_get_trace_stats")
         return {name: {"launches": int(t.launches[i]), "ms": float(t.ms[i]), "inner": int(t.inner[i]),
                        "leaf": int(t.leaf[i]), "tritest": int(t.tritest[i])}
-                for i, name in enumerate(("closest", "shadow", "tail"))}
+                for i, name in enumerate(TRACE_KINDS)}
 
     def set_option(self, key: str, value: int):
         self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")

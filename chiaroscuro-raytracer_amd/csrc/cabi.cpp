@@ -309,7 +309,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             c->last_trace.launches[k]++;
             c->last_trace.ms[k] += ms;
         }
-        for (int k = 0; k < 2; k++) { // the tail kernel's work is not split by kind
+        for (int k = 0; k < cr::TK_TAIL; k++) { // the tail kernel's work is not split by kind
             c->last_trace.inner[k] = h[cr::CTR_TRACE + 3 * k];
             c->last_trace.leaf[k] = h[cr::CTR_TRACE + 3 * k + 1];
             c->last_trace.tritest[k] = h[cr::CTR_TRACE + 3 * k + 2];

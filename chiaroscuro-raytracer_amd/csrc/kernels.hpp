@@ -9,9 +9,12 @@ enum { MODE_BLEND = 0, MODE_TILES = 1 };
 // float4 per triangle record.  3 (48 B, 1.5 lines per test on average) beat 4
 // (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
 enum { REC_STRIDE = 3 };
-enum { CTR_N = 22, CTR_SLOTS = 32 }; // Ctr fields (cr_counters order); device counter buffer entries
-// Counting builds of the wavefront trace kernels also tally inner / leaf / tritest per
-// instantiation: slots CTR_TRACE + 3 * kind + {0, 1, 2}, kind 0 = closest, 1 = shadow.
+enum { CTR_N = 22, CTR_SLOTS = 40 }; // Ctr fields (cr_counters order); device counter buffer entries
+// Wavefront trace launches by kind (cr_trace_stats order): camera rays (generation-1
+// closest trace), closest traces of later generations, shadow traces, the tail kernel.
+enum { TK_CAMERA = 0, TK_CLOSEST = 1, TK_SHADOW = 2, TK_TAIL = 3, TK_N = 4 };
+// Counting builds of the trace kernels also tally inner / leaf / tritest per kind
+// (not the tail): slots CTR_TRACE + 3 * kind + {0, 1, 2}.
 enum { CTR_TRACE = 24 };
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one
@@ -133,7 +136,7 @@ int num_wf_variants();
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
 void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks);
 // HIP events bracketing every trace launch (start, stop), recorded on the launch
-// stream; kind[i] = 0 closest / 1 shadow / 2 tail for pair i.  Grown by the launcher.
+// stream; kind[i] = TK_* of pair i.  Grown by the launcher.
 struct TraceEvents {
     hipEvent_t *ev = nullptr; // [2 * cap]
     int *kind = nullptr;      // [cap]

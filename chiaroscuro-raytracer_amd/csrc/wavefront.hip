@@ -166,7 +166,11 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // Persistent: every lane runs one query at a time through trav_round; when
 // `A.refill` lanes of a wave have finished (or none is busy) they take the
 // next rays of the queue (one atomicAdd per wave).
-template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1>
+// CAM: the generation-1 closest trace (camera rays) as its own instantiation, the
+// same code: it is the largest launch of a pass and never runs beside another
+// trace, so profiles and the bench roofline see it separately.
+template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
+          bool CAM = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
@@ -234,7 +238,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     else c.closest = issued;
     flush_counters(A.counters, c, 0u);
     if (FULL) { // per-instantiation split of the §8d work counters (bench roofline)
-        unsigned long long *base = A.counters + CTR_TRACE + 3 * (SHADOW ? 1 : 0);
+        unsigned long long *base = A.counters + CTR_TRACE + 3 * (SHADOW ? TK_SHADOW : (CAM ? TK_CAMERA : TK_CLOSEST));
         const uint32_t v[3] = {c.inner, c.leaf, c.tritest};
 #pragma unroll
         for (int i = 0; i < 3; i++) {
@@ -553,18 +557,21 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
 
 // --------------------------------------------------------------- launch --
 struct WfVariant {
+    void (*camera)(RenderArgs, WfArgs, uint32_t);
     void (*closest)(RenderArgs, WfArgs, uint32_t);
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd;
 };
-#define CR_WF(R, W, SC, FD, FAT)                                                                               \
-    {wf_trace<false, false, R, W, SC, FD, FAT>, wf_trace<true, false, R, W, SC, FD, FAT>, R, W}
+#define CR_WF_PF(R, W, SC, FD, FAT, PF)                                                                        \
+    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true>, wf_trace<false, false, R, W, SC, FD, FAT, PF>,           \
+     wf_trace<true, false, R, W, SC, FD, FAT, PF>, R, W}
+#define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
 static const WfVariant kWf[] = {
     CR_WF(4, 8, false, false, false), CR_WF(8, 8, false, false, false), CR_WF(8, 8, true, false, false),
     CR_WF(8, 6, false, false, false), CR_WF(8, 6, true, false, false),  CR_WF(8, 8, true, true, false),
-    CR_WF(8, 8, true, false, true),   CR_WF(8, 8, false, false, true),
-    {wf_trace<false, false, 8, 8, true, false, false, 2>, wf_trace<true, false, 8, 8, true, false, false, 2>, 8, 8}};
-static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4};
+    CR_WF(8, 8, true, false, true),   CR_WF(8, 8, false, false, true),  CR_WF_PF(8, 8, true, false, false, 2)};
+static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
+                                   wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
 
@@ -650,12 +657,12 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     auto tail = [&](uint32_t g) {
         const size_t tlds = (size_t)8 * tblk * sizeof(uint2);
         W.order = nullptr;
-        if ((err = trace_event(te, st, 2, true))) return;
+        if ((err = trace_event(te, st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
         else
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
-        err = trace_event(te, st, 2, false);
+        err = trace_event(te, st, TK_TAIL, false);
     };
     // closest trace of generation g on stream s; its stack overflow rows are the
     // second half of gstack when it runs beside a shadow trace
@@ -663,9 +670,10 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         WfArgs Wc = W;
         Wc.order = order;
         Wc.gstack = gstack;
-        if ((err = trace_event(te, s, 0, true))) return;
-        hipLaunchKernelGGL(v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
-        err = trace_event(te, s, 0, false);
+        const int kind = g == 1 ? TK_CAMERA : TK_CLOSEST;
+        if ((err = trace_event(te, s, kind, true))) return;
+        hipLaunchKernelGGL(g == 1 ? v.camera : v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
+        err = trace_event(te, s, kind, false);
     };
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
     if (W.P < W.tail_min) {
@@ -691,9 +699,9 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
             if (err) break;
         }
         W.order = order_s;
-        if ((err = trace_event(te, st, 1, true))) break;
+        if ((err = trace_event(te, st, TK_SHADOW, true))) break;
         hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
-        if ((err = trace_event(te, st, 1, false))) break;
+        if ((err = trace_event(te, st, TK_SHADOW, false))) break;
         hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
         if (next) {
             if ((err = (int)hipEventRecord(ss.join, ss.side)) || (err = (int)hipStreamWaitEvent(st, ss.join, 0)))

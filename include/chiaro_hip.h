@@ -207,18 +207,19 @@ int cr_intersect_shadow(cr_ctx *ctx, uint32_t n, const float *orig, const float 
 int cr_get_counters(cr_ctx *ctx, cr_counters *out);
 /* Device time (ms) of the last render kernel, HIP events on its own stream. */
 float cr_last_kernel_ms(cr_ctx *ctx);
-/* Per-kernel view of the last wavefront render ("kernel" 2) for the roofline:
- * the trace kernel's two instantiations, [0] closest-hit (KDTree::intersectRay,
- * src/kdtree.cpp:210-281) and [1] shadow (intersectShadowRay, :283-344), and
- * [2] the tail kernel that runs the last, small generations -- launch counts,
- * summed device time (a HIP event pair around every launch, on the render
- * stream) and, for [0] and [1] after a counting render ("counters" 1), the
- * inner-node / leaf / triangle-test tallies of those launches (zero after a
- * lean render; [2] is not split by query kind and stays zero). */
+/* Per-kernel view of the last wavefront render ("kernel" 2) for the roofline.
+ * Kinds: [0] the camera-ray trace (generation-1 closest-hit queries,
+ * KDTree::intersectRay, src/kdtree.cpp:210-281), [1] the closest-hit traces of
+ * later generations, [2] the shadow traces (intersectShadowRay, :283-344), [3]
+ * the tail kernel that runs the last, small generations.  Per kind: launch
+ * count, summed device time (a HIP event pair around every launch, on its
+ * stream; [1] and [2] partly run side by side, so their times overlap) and, for
+ * [0]-[2] after a counting render ("counters" 1), the inner-node / leaf /
+ * triangle-test tallies of those launches (zero after a lean render and for [3]). */
 typedef struct cr_trace_stats {
-    uint64_t launches[3];
-    double ms[3];
-    uint64_t inner[3], leaf[3], tritest[3];
+    uint64_t launches[4];
+    double ms[4];
+    uint64_t inner[4], leaf[4], tritest[4];
 } cr_trace_stats;
 int cr_get_trace_stats(cr_ctx *ctx, cr_trace_stats *out);
 /* Kernel variant / tuning knobs: "kernel" (0 = persistent wave-regeneration,

@@ -1,6 +1,8 @@
 """Per-phase time of each wavefront render pass from a rocprofv3 kernel trace.
     python scripts/pass_breakdown.py gpurun_out/prof_r01/trace/trace_kernel_trace.csv
-A pass starts at wf_camera; trace launches are numbered by generation.  The
+A pass starts at wf_camera; trace launches are numbered by generation (closest and
+shadow separately: shadow g runs beside closest g + 1).  pass_ms sums kernel
+times, busy_ms is the union of their intervals, overlap_ms the difference.  The
 counting launch (FULL build) is marked "counting" and is not a timed pass.
 """
 import csv
@@ -19,7 +21,7 @@ def main():
         if cur is not None:
             cur.append(r)
     for p in passes:
-        g, acc, tot, counting = 0, {}, 0.0, False
+        g, gs, acc, tot, counting = 0, 0, {}, 0.0, False
         for r in p:
             n = r["Kernel_Name"]
             ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
@@ -29,21 +31,32 @@ def main():
                 k = "g%d closest" % g
                 counting |= re.search(r"wf_trace<false, true,", n) is not None
             elif "wf_trace<true" in n:
-                k = "g%d shadow" % g
+                gs += 1
+                k = "g%d shadow" % gs
             elif "wf_tail" in n:
-                k = "tail (g%d..)" % (g + 1)
+                k = "tail (g%d..)" % (gs + 1)
                 counting |= "wf_tail<true" in n
             elif "rocprim" in n:
                 k = "sort"
-            elif "wf_shade" in n or "wf_bounce" in n:
-                k = "shade+bounce"
+            elif "wf_shade" in n or "wf_bounce" in n or "wf_resolve" in n:
+                k = "shade+resolve"
             elif "__amd_rocclr" in n:
                 k = "copies/fills"
             else:
                 k = n.split("(")[0].split("::")[-1]
             acc[k] = acc.get(k, 0.0) + ms
         wall = (max(int(r["End_Timestamp"]) for r in p) - int(p[0]["Start_Timestamp"])) / 1e6
-        print(json.dumps({"pass_ms": round(tot, 1), "wall_ms": round(wall, 1), "gaps_ms": round(wall - tot, 1),
+        busy, end = 0, None  # union of the kernel intervals (kernels on two streams overlap)
+        for a, b in sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in p):
+            if end is None or a > end:
+                busy += b - a
+                end = b
+            elif b > end:
+                busy += b - end
+                end = b
+        busy /= 1e6
+        print(json.dumps({"pass_ms": round(tot, 1), "wall_ms": round(wall, 1), "busy_ms": round(busy, 1),
+                          "overlap_ms": round(tot - busy, 1), "gaps_ms": round(wall - busy, 1),
                           "counting": counting,
                           "phases_ms": {k: round(v, 1) for k, v in acc.items()}}))
 

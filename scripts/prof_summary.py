@@ -79,9 +79,13 @@ def main():
     # the trace kernel's lean instantiations (bench.py roofline): fabric bytes per launch
     trace = {}
     for n, e in summary.items():
-        m = re.search(r"wf_trace<(true|false), false,", n)
-        if m and "fabric_bytes_total" in e:
-            trace["shadow" if m.group(1) == "true" else "closest"] = {
+        m = re.search(r"wf_trace<([^>]*)>", n)
+        if not m or "fabric_bytes_total" not in e:
+            continue
+        targs = [a.strip() for a in m.group(1).split(",")]  # SHADOW, FULL, R, MINW, SC, FD, FAT, PF, CAM
+        if targs[1] == "false":  # lean builds (the timed ones)
+            kind = "shadow" if targs[0] == "true" else ("camera" if targs[-1] == "true" else "closest")
+            trace[kind] = {
                 "kernel": n, "calls": e["calls"], "avg_ns": e["avg_ns"],
                 "fabric_bytes_per_launch": e["fabric_bytes_total"] / e["calls"]}
     (prof / ("pmc_%s.json" % config)).write_text(json.dumps({

@@ -90,7 +90,9 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
         assert ts["tail"]["launches"] == 1
         if tail_min == 1 << 30:
-            assert ts["closest"]["launches"] == 0 and ts["shadow"]["launches"] == 0
+            assert all(ts[kind]["launches"] == 0 for kind in ("camera", "closest", "shadow"))
+        else:
+            assert ts["camera"]["launches"] == 1
 
 
 @pytest.mark.parametrize("kernel", [0, 1, 2])
