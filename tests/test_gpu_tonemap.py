@@ -62,3 +62,71 @@ def test_raytracer_normalize_image_on_rendered_frame(ca, po, scenes):
         _compare(rt.getData(), po.tonemap(rt.pixels, *prm), "nanobox %s" % (prm,))
     rt.normalizeImage()  # exposure = the scene's (.rtc), as the reference's default
     _compare(rt.getData(), po.tonemap(rt.pixels, i["exposure"]), "nanobox scene exposure")
+
+
+def _read_exr(path):
+    """Minimal reader of the scanline, uncompressed, FLOAT B,G,R file exportImage writes."""
+    b = open(path, "rb").read()
+    assert b[:4] == (20000630).to_bytes(4, "little")
+    pos, attrs = 8, {}
+    while b[pos] != 0:
+        name_end = b.index(b"\0", pos)
+        name = b[pos:name_end].decode()
+        type_end = b.index(b"\0", name_end + 1)
+        size = int.from_bytes(b[type_end + 1:type_end + 5], "little")
+        attrs[name] = b[type_end + 5:type_end + 5 + size]
+        pos = type_end + 5 + size
+    pos += 1
+    x0, y0, x1, y1 = np.frombuffer(attrs["dataWindow"], "<i4")
+    w, h = x1 - x0 + 1, y1 - y0 + 1
+    assert attrs["compression"] == b"\0"
+    offsets = np.frombuffer(b[pos:pos + 8 * h], "<u8")
+    img = np.zeros((h, w, 3), np.float32)
+    for y, off in enumerate(int(o) for o in offsets):
+        yy, sz = (int(v) for v in np.frombuffer(b[off:off + 8], "<i4"))
+        assert yy == y and sz == 12 * w
+        line = np.frombuffer(b[off + 8:off + 8 + sz], "<f4").reshape(3, w)  # B, G, R planes
+        img[y] = line[::-1].T
+    return img
+
+
+def _read_hdr(path):
+    """Radiance RGBE, flat scanlines, -Y H +X W -> [H][W][3] float32 (row 0 = top)."""
+    b = open(path, "rb").read()
+    hdr_end = b.index(b"\n\n") + 2
+    line_end = b.index(b"\n", hdr_end)
+    res = b[hdr_end:line_end].split()
+    assert res[0] == b"-Y" and res[2] == b"+X"
+    h, w = int(res[1]), int(res[3])
+    e = np.frombuffer(b[line_end + 1:], np.uint8).reshape(h, w, 4).astype(np.float64)
+    scale = np.where(e[..., 3:] > 0, np.ldexp(1.0, (e[..., 3:] - 136).astype(int)), 0.0)
+    return (e[..., :3] * scale).astype(np.float32)
+
+
+def test_export_formats_round_trip(ca, scenes, tmp_path):
+    """RayTracer.exportImage (rayTracer.cpp:225-279 with this build's writers, FreeImage
+    being absent): PFM and EXR hold the float pixels exactly, HDR within RGBE's 8-bit
+    mantissa, PNG and PPM the normalizeImage bytes (top row first)."""
+    from PIL import Image
+
+    sc = ca.Scene(scenes.config_rtc("nanobox"), "xres", "64", "yres", "36", "samples", "2")
+    m = ca.Model(sc)
+    rt = ca.RayTracer(m, sc)
+    i = sc.info
+    rt.rayTrace(i["VP"], i["LA"], i["UP"], i["yview"])
+    px = rt.pixels.copy()
+    rt.exportImage(str(tmp_path / "a.pfm"))
+    rt.exportImage(str(tmp_path / "a.exr"))
+    rt.exportImage(str(tmp_path / "a.hdr"))
+    rt.exportImage(str(tmp_path / "a.png"))
+    rt.exportImage(str(tmp_path / "a.ppm"))
+    data = rt.getData().reshape(36, 64, 3)[::-1]  # `data` rows are bottom-up
+    raw = open(tmp_path / "a.pfm", "rb").read().split(b"\n", 3)[3]
+    pfm = np.frombuffer(raw, "<f4").reshape(36, 64, 3)[::-1]
+    assert np.array_equal(pfm.view(np.uint32), px.view(np.uint32))
+    assert np.array_equal(_read_exr(tmp_path / "a.exr").view(np.uint32), px.view(np.uint32))
+    hdr = _read_hdr(tmp_path / "a.hdr")
+    peak = np.maximum(px.max(axis=2, keepdims=True), 1e-30)
+    assert np.all(np.abs(hdr - px) <= peak / 128.0 + 1e-30)
+    assert np.array_equal(np.asarray(Image.open(tmp_path / "a.png").convert("RGB")), data)
+    assert np.array_equal(np.asarray(Image.open(tmp_path / "a.ppm").convert("RGB")), data)
