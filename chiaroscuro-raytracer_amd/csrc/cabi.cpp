@@ -56,7 +56,9 @@ struct cr_ctx {
     // sweep (1080p x 128 spp, refill 56): no sort 807; (8x8 px, 8x8 dirs) 891; (16x16, 16x16) 912;
     // (16x16, 32x32 Morton) 930; (32x32, 32x32) 914 Mray/s
     uint32_t wf_sort_tile = 4;      // key: log2 pixel sub-tile edge
-    uint32_t wf_dir_res = 32;       // key: direction bins per octahedral axis
+    // direction bins per octahedral axis: 32 -> 64 575.6 -> 570.2 ms per pass, rank 0 of 8 79.6 -> 78.0
+    // (world bits 5 / 7 and 16 bins measured slower; 7 bits x 64 bins: 31-bit keys, 607 ms)
+    uint32_t wf_dir_res = 64;       // key: direction bins per octahedral axis
     int wf_world_keys = 2;          // key: world-space origins for queues starting at hits of gen >= 2
     uint32_t wf_world_bits = 6;     // key: Morton bits per axis of the origin
     // closest queues shorter than this finish in one wf_tail launch (0: never).  Sweep, sponza

@@ -50,7 +50,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         finally:
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_sort_tile", 4)
-            pair.dev.set_option("wf_dir_res", 32)
+            pair.dev.set_option("wf_dir_res", 64)
         assert_bitwise(g, o, "sorted wavefront %dx%dx%d" % (x, y, s))
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
