@@ -63,6 +63,11 @@ def main():
         "rounds_fit21": round(c["leaf_fit21"] / max(c["leaf_rounds"], 1), 3),
         "rounds_fit56": round(c["leaf_fit56"] / max(c["leaf_rounds"], 1), 3),
     })
+    ts = dev.trace_stats()  # wavefront: per-kind inner / leaf / tritest (counting build)
+    ncam = i["xres"] * i["yres"] * args.spp
+    if args.kernel == 2 and "camera" in ts:
+        out["camera_per_ray"] = {k: round(ts["camera"][k] / ncam, 1) for k in ("inner", "leaf", "tritest")}
+        out["trace_stats"] = ts
     print(json.dumps(out))
 
 

@@ -22,6 +22,10 @@ class Pair:
             self.dev = ca.Device(0)
             self.desc = self.kd.describe()
             self.dev.upload(self.desc)
+            # every wavefront generation as its own launches (the default hands queues
+            # below 1M rays -- all of a test-sized render -- to wf_tail; the tail test
+            # sets its own threshold)
+            self.dev.set_option("wf_tail_min", 0)
 
     def camera(self, ca, xres, yres):
         i = self.info

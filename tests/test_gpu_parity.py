@@ -84,7 +84,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min):
             ts = pair.dev.trace_stats()
         finally:
             pair.dev.set_option("counters", 1)
-            pair.dev.set_option("wf_tail_min", 1 << 20)
+            pair.dev.set_option("wf_tail_min", 0)
         assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
         assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
