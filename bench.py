@@ -235,6 +235,17 @@ def main():
                         "traffic": tr["fabric_bytes_per_launch"] if tr else None,
                         "rocprof_avg_launch_ms": round(tr["avg_ns"] / 1e6, 3) if tr else None}
             views = {k: kind_view(k) for k in ("camera", "closest", "shadow")}
+            # what bounds the trace kernels instead of HBM: instruction issue (committed
+            # scripts/pmc_issue.sh summary of this configuration, per lean trace kind)
+            issue = None
+            pi = ROOT / "profiles" / ("pmc_issue_%s.json" % args.config)
+            if pi.exists():
+                try:
+                    ij = json.loads(pi.read_text())
+                    if ij.get("spp") == spp:
+                        issue = ij.get("kinds")
+                except Exception:
+                    issue = None
             dom = views["camera"] or views["closest"]
             roofline = {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(dom["achieved"] / HBM_PEAK_GBS, 5), "traffic": dom["traffic"],
@@ -243,6 +254,7 @@ def main():
                         "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
                         "rocprof_avg_launch_ms": dom["rocprof_avg_launch_ms"],
                         "other_traces": {k: v for k, v in views.items() if v is not None and v is not dom},
+                        "issue": issue,
                         "pass": pass_view}
         else:
             roofline = {"bound": "hbm", "achieved": round(pass_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -40,7 +40,7 @@ struct cr_ctx {
     cr_trace_stats last_trace{};
     // options
     // Defaults from sweeps on MI355X, sponza stand-in 1080p x 128 spp:
-    //   wavefront (kernel 2), trace variant 6, refill 64/56/48, sorted queues, tail below 1M rays
+    //   wavefront (kernel 2), trace variant 9, refill 64/56/48, sorted queues, tail below 1M rays
     //   persistent megakernel (kernel 0), variant 0, refill 16:                615 Mray/s
     int kernel = 2;
     int full_counters = 1;
@@ -163,8 +163,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // wavefront trace builds (wavefront.hip kWf): 2 = LDS ring 8, 8 waves/SIMD, scalar loads for
     // wave-uniform nodes / leaves: 1003 vs 935 Mray/s for the same build without them (variant 1);
     // 6 = 2 + fat node records (a node and both children in 32 B: one dependent load per two
-    // descent levels): 595.0 vs 597.5 ms per 1080p x 128 spp pass, 83.0 vs 84.2 ms for rank 0 of 8
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 6 : 0);
+    // descent levels): 595.0 vs 597.5 ms per 1080p x 128 spp pass, 83.0 vs 84.2 ms for rank 0 of 8;
+    // 9 = 6 with branch-light descent steps and uniform-leaf tests (fewer scalar-unit exec-mask
+    // instructions): 563.8 vs 565.5 ms, rank 0 of 8 77.48 vs 77.64 ms (5 interleaved rounds)
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 9 : 0);
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {

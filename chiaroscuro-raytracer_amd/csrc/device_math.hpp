@@ -74,6 +74,18 @@ __device__ __forceinline__ float rcp_rn(float a) {
     return 1.f / a;
 }
 
+// rcp_rn for wave-wide use: the range test is one wave-uniform branch (the full
+// division runs for the whole wave only when some lane is out of range) instead
+// of a divergent if/else, which costs the scalar unit ~6 exec-mask instructions.
+__device__ __forceinline__ float rcp_rn_wave(float a) {
+    const float aa = fabsf(a);
+    const float y0 = __builtin_amdgcn_rcpf(a);
+    float r = __builtin_fmaf(__builtin_fmaf(-a, y0, 1.f), y0, y0);
+    const bool in = aa >= 0x1p-100f && aa <= 0x1p100f;
+    if (__ballot(!in)) r = in ? r : 1.f / a;
+    return r;
+}
+
 // ---------------------------------------------------------------- RNG --
 // Counter-based URBG (DESIGN.md "RNG"); identical to oracle/oracle.c rng_*.
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {

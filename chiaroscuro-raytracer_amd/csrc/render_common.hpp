@@ -93,6 +93,30 @@ __device__ __forceinline__ bool tri_test(f3 o, f3 d, const TriRec &r, float tmax
     return t >= 0.f && t < tmax;
 }
 
+// tri_test with the scalar unit in mind (BF trace builds): the early exits are
+// wave-uniform (taken when no active lane can still accept) and the lanes that
+// already failed compute on, masked by `ok`, so no exec-mask bookkeeping runs per
+// test.  Same values, same acceptance.
+__device__ __forceinline__ bool tri_test_wave(f3 o, f3 d, const TriRec &r, float tmax, float &ux, float &uy,
+                                              float &t) {
+    const f3 v0 = ld3(r.a), e1 = ld3(r.b), e2 = ld3(r.c);
+    const f3 p = cross(d, e2);
+    const float aa = dot(e1, p);
+    bool ok = !(aa < 1.19209290e-7F && aa > -1.19209290e-7F);
+    if (!__ballot(ok)) return false;
+    const float f = rcp_rn_wave(aa);
+    const f3 sv = sub(o, v0);
+    ux = f * dot(sv, p);
+    ok = ok && !(ux < 0.f || ux > 1.f);
+    if (!__ballot(ok)) return false;
+    const f3 q = cross(sv, e1);
+    uy = f * dot(d, q);
+    ok = ok && !(uy < 0.f || uy + ux > 1.f);
+    if (!__ballot(ok)) return false;
+    t = f * dot(e2, q);
+    return ok && t >= 0.f && t < tmax;
+}
+
 // tsplit = (split - oa) / da of a kd node (kdtree.cpp:266), correctly rounded.
 __device__ __forceinline__ float split_distance(float split, float oa, float da) { return (split - oa) / da; }
 

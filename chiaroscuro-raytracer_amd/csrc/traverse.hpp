@@ -120,7 +120,11 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // loads (no register rotation copies, but count-1 leaves fetch a second record:
 // -2.3%), and compiler-scheduled, pipelined scalar loads for uniform leaves
 // (address_space(4): -2.5% against the asm s_load + wait below).
-template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false>
+// BF: the decisions as selects instead of divergent branches (the trace kernels
+// are bound by the scalar unit's exec-mask bookkeeping, SURVEY §8d / DESIGN §3.3):
+// a descent step branches only around its stack push, and a uniform leaf's
+// triangle tests keep their result by select (tri_test_wave).
+template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c) {
@@ -145,7 +149,20 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         const uint32_t below = (oa < split) || (oa == split && da <= 0);
         const uint32_t child = nd.y >> 2;
         uint32_t k;
-        if (tsplit >= T.tmax || tsplit < 0) {
+        if (BF) {
+            const bool near_only = tsplit >= T.tmax || tsplit < 0;
+            const bool far_only = !near_only && tsplit <= T.tmin;
+            const bool push = !near_only && !far_only;
+            k = far_only ? below : 1u - below;
+            if (push) {
+                const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
+                if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
+                ring[slot] = make_uint2(child + below, __float_as_uint(T.tmax));
+            }
+            T.nl = push && T.nl < R ? T.nl + 1 : T.nl;
+            T.sp += push ? 1u : 0u;
+            T.tmax = push ? tsplit : T.tmax;
+        } else if (tsplit >= T.tmax || tsplit < 0) {
             k = 1u - below;
         } else if (tsplit <= T.tmin) {
             k = below;
@@ -238,7 +255,29 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             c.leaf_fit56 += nr <= 56;
         }
     }
-    if (SC && wave_uniform(first)) { // every lane at the same leaf: scalar loads
+    if (BF && SC && wave_uniform(first)) { // uniform leaf, results by select
+        const uint32_t uf = __builtin_amdgcn_readfirstlane(first), uc = __builtin_amdgcn_readfirstlane(count);
+        const float4 *base = S.recs + (size_t)REC_STRIDE * uf;
+        for (uint32_t j = 0; j < uc; j++) {
+            tally_tri(uf + j);
+            const TriRec r = sload_rec(base + (size_t)REC_STRIDE * j);
+            const uint32_t id = rec_id(r);
+            const bool live = !(shadow && (occluded || id == exclude));
+            if (FULL) c.tritest += live ? 1u : 0u;
+            float ux, uy, t;
+            const bool acc = live && tri_test_wave(o, d, r, T.tmax, ux, uy, t);
+            if (shadow) {
+                occluded = occluded || acc;
+                if (__ballot(!occluded) == 0) break; // every active lane occluded
+            } else {
+                bx = acc ? ux : bx;
+                by = acc ? uy : by;
+                T.tmax = acc ? t : T.tmax;
+                tri = acc ? id : tri;
+                found = found || acc;
+            }
+        }
+    } else if (SC && wave_uniform(first)) { // every lane at the same leaf: scalar loads
         const float4 *base = S.recs + (size_t)REC_STRIDE * __builtin_amdgcn_readfirstlane(first);
         for (uint32_t j = 0; j < count; j++) {
             tally_tri(first + j);

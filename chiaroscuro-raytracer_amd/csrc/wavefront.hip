@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // same code: it is the largest launch of a pass and never runs beside another
 // trace, so profiles and the bench roofline see it separately.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false>
+          bool CAM = false, bool BF = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
                                                                  exclude, T, c);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
@@ -562,14 +562,16 @@ struct WfVariant {
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd;
 };
-#define CR_WF_PF(R, W, SC, FD, FAT, PF)                                                                        \
-    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true>, wf_trace<false, false, R, W, SC, FD, FAT, PF>,           \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF>, R, W}
+#define CR_WF_BF(R, W, SC, FD, FAT, PF, BF)                                                                    \
+    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF>, wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF>, \
+     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF>, R, W}
+#define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
 #define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
 static const WfVariant kWf[] = {
     CR_WF(4, 8, false, false, false), CR_WF(8, 8, false, false, false), CR_WF(8, 8, true, false, false),
     CR_WF(8, 6, false, false, false), CR_WF(8, 6, true, false, false),  CR_WF(8, 8, true, true, false),
-    CR_WF(8, 8, true, false, true),   CR_WF(8, 8, false, false, true),  CR_WF_PF(8, 8, true, false, false, 2)};
+    CR_WF(8, 8, true, false, true),   CR_WF(8, 8, false, false, true),  CR_WF_PF(8, 8, true, false, false, 2),
+    CR_WF_BF(8, 8, true, false, true, 1, true)};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));

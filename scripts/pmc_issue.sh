@@ -1,0 +1,14 @@
+#!/bin/bash
+# Instruction-mix PMC pass over one bench configuration (issue-bound analysis of the
+# trace kernels): counts per instruction class, its own rocprofv3 --pmc run.
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc_issue
+mkdir -p $OUT
+ARGS=${@:-"--config sponza --steps 1 --warmup 0 --no-cpu-baseline"}
+timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/a -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/a.log 2>&1 || { echo "pass a failed"; exit 1; }
+echo "pass a ok"
+timeout -s KILL 300 rocprofv3 --pmc TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE -d $OUT/b -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/b.log 2>&1 || { echo "pass b failed"; exit 1; }
+echo "pass b ok"
+find $OUT -name "*.csv"

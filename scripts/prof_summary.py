@@ -82,9 +82,10 @@ def main():
         m = re.search(r"wf_trace<([^>]*)>", n)
         if not m or "fabric_bytes_total" not in e:
             continue
-        targs = [a.strip() for a in m.group(1).split(",")]  # SHADOW, FULL, R, MINW, SC, FD, FAT, PF, CAM
+        targs = [a.strip() for a in m.group(1).split(",")]  # SHADOW, FULL, R, MINW, SC, FD, FAT, PF, CAM[, BF]
         if targs[1] == "false":  # lean builds (the timed ones)
-            kind = "shadow" if targs[0] == "true" else ("camera" if targs[-1] == "true" else "closest")
+            cam = len(targs) > 8 and targs[8] == "true"
+            kind = "shadow" if targs[0] == "true" else ("camera" if cam else "closest")
             trace[kind] = {
                 "kernel": n, "calls": e["calls"], "avg_ns": e["avg_ns"],
                 "fabric_bytes_per_launch": e["fabric_bytes_total"] / e["calls"]}
