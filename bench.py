@@ -11,9 +11,23 @@ step   : one progressive layer of the whole frame of the config at its spp
          gather of the per-rank tile buffers to rank 0 (RCCL over xGMI) and the
          root-side unpermute + progressive blend, all inside the timed region.
 
-Prints ONE JSON line on rank 0 with the contract fields plus "roofline" (render
-kernel, algorithmic bytes per SURVEY §8d / HIP-event kernel time vs 8 TB/s HBM)
-and "cpu_baseline" (the oracle's OpenMP restatement on a bounded row sample).
+`--gpus N` (N > 1) without a torch.distributed environment starts the N rank
+processes itself (torch.distributed.run as a child process, before this process
+touches the GPU) and exits with their status; under torch.distributed.run the
+world size must equal N.
+
+Prints ONE JSON line on rank 0 with the contract fields plus
+  "roofline"      the dominant kernel (the camera-ray trace) against the ceiling
+                  that binds it: instruction issue (VALU / SALU wave-instructions
+                  per launch from the committed rocprofv3 PMC summary
+                  profiles/pmc_issue_<config>.json, divided by this run's live
+                  HIP-event launch time, against 1024 SIMDs x 2.4 GHz / 2 cycles
+                  and 256 scalar units x 2.4 GHz); the algorithmic-bytes view of
+                  SURVEY §8d against HBM and the L2 aggregate stays as a
+                  secondary field ("bytes"), with the fabric bytes measured;
+  "cpu_baseline"  the oracle's OpenMP restatement on a bounded row sample of the
+                  same frame, with every thread of this process's CPU share
+                  and with 1 thread, and the host's physical core count.
 """
 from __future__ import annotations
 
@@ -29,45 +43,137 @@ sys.path.insert(0, str(ROOT / "chiaroscuro-raytracer_amd"))
 os.environ.setdefault("CHIARO_QUIET", "1")
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 aggregate over 8 XCDs, ~34.5 TB/s
+CLK_GHZ = 2.4          # MI355X_MICROARCH.md: max shader clock
+# issue ceilings, wave-instructions per second (MI355X_MICROARCH.md: a wave64 VALU
+# instruction occupies a SIMD-32 for 2 cycles; one scalar ALU per CU, 1 per cycle)
+VALU_PEAK_GIPS = 256 * 4 * CLK_GHZ / 2
+SALU_PEAK_GIPS = 256 * CLK_GHZ
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def physical_cores():
+    """Physical cores of this host (lscpu: sockets x cores per socket), or None."""
+    import subprocess
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=30).stdout
+        f = {k.strip(): v.strip() for k, v in (ln.split(":", 1) for ln in out.splitlines() if ":" in ln)}
+        return int(f["Socket(s)"]) * int(f["Core(s) per socket"])
+    except Exception:
+        return None
+
+
+def cpu_threads():
+    """This process's CPU share: OMP_NUM_THREADS where the pool sets it (16 per GPU
+    on the MI355X boxes), else the CPUs this process may run on."""
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(pair_tris, textures, info, leaf, cam, xres, yres, spp, k, seed, budget_s):
-    """Oracle restatement (OpenMP over rows, dynamic schedule) on a row sample."""
+    """Oracle restatement (OpenMP over rows, dynamic schedule) on a row sample of
+    the same frame, with all threads of the CPU share and with 1 thread."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle as po
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     t0 = time.time()
     osc = po.OracleScene(pair_tris, leaf_size=leaf, textures=textures, build_threads=threads)
     log("cpu_baseline: oracle kd build %.1fs" % (time.time() - t0))
-    # calibrate on every 8th row at 1 spp, then size (rows, spp) to ~budget_s
-    step = 8
-    t0 = time.time()
-    osc.render(cam, xres, yres, 1, k, seed, y0=0, y1=yres, ystep=step, threads=threads)
-    dt = max(time.time() - t0, 1e-3)
-    rows = (yres + step - 1) // step
-    per_row_spp = dt / rows
-    work = budget_s / per_row_spp                   # affordable row-samples
-    s_spp = int(max(1, min(spp, work // yres)))     # whole frame if it fits, more spp if time allows
-    nrows = int(max(1, min(yres, work // s_spp)))
-    ystep = max(1, yres // nrows)
-    t0 = time.time()
-    _, c = osc.render(cam, xres, yres, s_spp, k, seed, y0=0, y1=yres, ystep=ystep, threads=threads)
-    dt = time.time() - t0
-    nr = (yres + ystep - 1) // ystep
-    rays = c["closest"] + c["shadow"]
-    return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": "oracle/liboracle.so (OpenMP rows, dynamic), %d of %d rows (every %d-th) x %d px x %d spp "
-                      "of the same frame/seed, %d rays in %.1f s" % (nr, yres, ystep, xres, s_spp, rays, dt)}
+
+    def timed(nthreads, budget):
+        # calibrate on every 8th row at 1 spp, then size (rows, spp) to ~budget
+        step = 8
+        t0 = time.time()
+        osc.render(cam, xres, yres, 1, k, seed, y0=0, y1=yres, ystep=step, threads=nthreads)
+        dt = max(time.time() - t0, 1e-3)
+        rows = (yres + step - 1) // step
+        work = budget / (dt / rows)                   # affordable row-samples
+        s_spp = int(max(1, min(spp, work // yres)))   # whole frame if it fits, more spp if time allows
+        nrows = int(max(1, min(yres, work // s_spp)))
+        ystep = max(1, yres // nrows)
+        t0 = time.time()
+        _, c = osc.render(cam, xres, yres, s_spp, k, seed, y0=0, y1=yres, ystep=ystep, threads=nthreads)
+        dt = time.time() - t0
+        rays = c["closest"] + c["shadow"]
+        nr = (yres + ystep - 1) // ystep
+        return rays / dt / 1e6, "%d of %d rows (every %d-th) x %d px x %d spp, %d rays in %.1f s" % (
+            nr, yres, ystep, xres, s_spp, rays, dt)
+
+    v_all, s_all = timed(threads, budget_s * 0.6)
+    v_1t, s_1t = timed(1, budget_s * 0.4)
+    phys = physical_cores()
+    return {"value": round(v_all, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "value_1t": round(v_1t, 4), "threads_all": threads, "physical_cores": phys,
+            "parallel_efficiency": round(v_all / (v_1t * threads), 3) if v_1t > 0 else None,
+            # linear in cores from the 1-thread rate: an upper bound for the whole host (the pool
+            # gives one GPU's job a 16-thread CPU share, so the other cores are not timed)
+            "projected_all_physical": round(v_1t * phys, 2) if phys else None,
+            "sample": "oracle/liboracle.so (OpenMP rows, dynamic) on the same frame/seed; %d threads: %s; "
+                      "1 thread: %s" % (threads, s_all, s_1t)}
+
+
+def issue_roofline(dom, iss, views, issue, pass_view):
+    """Roofline of the dominant trace kernel against the ceiling that binds it.
+
+    The trace kernels' working set (kd nodes + triangle records, ~65 MB for the
+    sponza stand-in) stays in L2 / Infinity Cache: the algorithmic bytes per launch
+     run at several times HBM peak while the measured fabric bytes are
+    ~1.5 % of them, so HBM does not bound them.  What does is instruction issue:
+    wave-instructions per launch (rocprofv3 SQ_INSTS_VALU / SQ_INSTS_SALU of this
+    kernel, profiles/pmc_issue_<config>.json) over this run's HIP-event launch time,
+    against the VALU issue peak (1024 SIMDs x 2.4 GHz / 2 cycles per wave64
+    instruction) and the scalar-unit peak (256 x 2.4 GHz).  The binding ceiling is
+    the one with the highest fraction; TA (vector address path) busy comes from
+    the profile only (no live counterpart)."""
+    t = dom["avg_launch_ms"] / 1e3
+    bytes_view = {"algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"], "achieved_gbs": dom["achieved"],
+                  "frac_of_hbm": round(dom["achieved"] / HBM_PEAK_GBS, 4),
+                  "frac_of_l2_aggregate": round(dom["achieved"] / L2_PEAK_GBS, 4),
+                  "fabric_bytes_per_launch": dom["traffic"]}
+    base = {"kernel": dom["kernel"] + " (camera-ray kd traversal, wavefront.hip)",
+            "avg_launch_ms": dom["avg_launch_ms"], "launches": dom["launches"],
+            "rocprof_avg_launch_ms": dom["rocprof_avg_launch_ms"], "bytes": bytes_view,
+            "other_traces": {k: v for k, v in views.items() if v is not None and v is not dom},
+            "issue": issue, "pass": pass_view}
+    if not iss or t <= 0:
+        return {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dom["achieved"] / HBM_PEAK_GBS, 5), "traffic": dom["traffic"],
+                "note": "no instruction-issue profile of this configuration: algorithmic bytes vs HBM", **base}
+    valu = iss["valu_insts_per_launch"] / t / 1e9
+    salu = iss["salu_insts_per_launch"] / t / 1e9
+    ceil = {"valu": {"achieved": round(valu, 2), "peak": VALU_PEAK_GIPS, "frac": round(valu / VALU_PEAK_GIPS, 4),
+                     "insts_per_launch": iss["valu_insts_per_launch"]},
+            "salu": {"achieved": round(salu, 2), "peak": SALU_PEAK_GIPS, "frac": round(salu / SALU_PEAK_GIPS, 4),
+                     "insts_per_launch": iss["salu_insts_per_launch"]},
+            "ta_busy_profiled": iss.get("ta_busy"),
+            "hbm_bytes": {"frac": bytes_view["frac_of_hbm"], "note": "algorithmic bytes, cache resident"}}
+    bound = max(("valu", "salu"), key=lambda k: ceil[k]["frac"])
+    b = ceil[bound]
+    return {"bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": "Gwave-inst/s", "frac": b["frac"],
+            "traffic": dom["traffic"], "ceilings": ceil,
+            "profile": "profiles/pmc_issue_<config>.json kinds[camera] (%s)" % iss["kernel"], **base}
+
+
+def spawn_ranks(n: int) -> int:
+    """Start n rank processes of this script with torch.distributed.run (a child
+    process; this process has not touched the GPU) and return their exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    log("bench: starting %d ranks: %s" % (n, " ".join(cmd)))
+    return subprocess.call(cmd)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (= rank processes) of one node, default 1")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza", help="cornell | cornell_box | sponza | sponza_4k")
@@ -78,15 +184,18 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.gpus is not None and args.gpus != world:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
 
-    import numpy as np
     import torch
 
     import chiaroscuro_amd as ca
     from chiaroscuro_amd import scenes
     from chiaroscuro_amd.tiles import DistributedFrame
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -95,6 +204,9 @@ def main():
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+        if rank == 0:
+            log("bench: %d ranks, backend %s" % (dist.get_world_size(), dist.get_backend()))
     dev_index = local
     torch.cuda.set_device(dev_index)
 
@@ -163,15 +275,18 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per rank: wall time, device time of its render passes (HIP events), rays
+    mine = torch.tensor([elapsed, totals["kernel_ms"] / max(totals["launches"], 1), totals["rays"]],
+                        dtype=torch.float64, device="cuda")
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor([totals["rays"], totals["bytes"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(r)
-        rays_all = float(r[0].item())
+        per_rank = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+        per_rank = torch.stack(per_rank).cpu().tolist()
     else:
-        rays_all = float(totals["rays"])
+        per_rank = [mine.cpu().tolist()]
+    elapsed = max(r[0] for r in per_rank)   # the step ends with the slowest rank
+    rays_all = float(sum(r[2] for r in per_rank))
+    rank_render_ms = [round(r[1], 3) for r in per_rank]
 
     # counting pass (untimed): algorithmic bytes of one launch of this rank
     dev.set_option("counters", 1)
@@ -247,15 +362,8 @@ def main():
                 except Exception:
                     issue = None
             dom = views["camera"] or views["closest"]
-            roofline = {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(dom["achieved"] / HBM_PEAK_GBS, 5), "traffic": dom["traffic"],
-                        "kernel": dom["kernel"] + " (camera-ray kd traversal, wavefront.hip)",
-                        "avg_launch_ms": dom["avg_launch_ms"], "launches": dom["launches"],
-                        "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
-                        "rocprof_avg_launch_ms": dom["rocprof_avg_launch_ms"],
-                        "other_traces": {k: v for k, v in views.items() if v is not None and v is not dom},
-                        "issue": issue,
-                        "pass": pass_view}
+            dom_kind = "camera" if views["camera"] else "closest"
+            roofline = issue_roofline(dom, (issue or {}).get(dom_kind), views, issue, pass_view)
         else:
             roofline = {"bound": "hbm", "achieved": round(pass_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(pass_gbs / HBM_PEAK_GBS, 5), "traffic": pass_view["traffic"],
@@ -280,6 +388,7 @@ def main():
             "data": "synthetic scene (deterministic generator), seeded counter RNG",
             "config": {"workload": label, "spp_per_step": spp, "k": k, "tile": tile,
                        "parallelism": "tile-split x%d" % world, "rays": int(rays_all),
+                       "rank_render_ms": rank_render_ms,
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -51,25 +51,32 @@ class TileLayout:
 class DistributedFrame:
     """One rank's side of a layer: render my tiles, gather to rank 0, blend.
 
-    dev      chiaroscuro_amd.Device of this rank
+    dev      chiaroscuro_amd.Device of this rank (anything with render_device /
+             render_tiles_device / blend_tiles_device taking buffer addresses;
+             the gloo tests pass an oracle-backed stand-in with device="cpu")
     dist     torch.distributed (initialised), or None for a single rank
+    device   torch device of the frame / tile / gather buffers
     """
 
-    def __init__(self, dev, xres: int, yres: int, rank: int, nranks: int, tile: int = 32, dist=None):
+    def __init__(self, dev, xres: int, yres: int, rank: int, nranks: int, tile: int = 32, dist=None,
+                 device: str = "cuda"):
         import torch
+        if nranks > 1 and (dist is None or dist.get_world_size() != nranks or dist.get_rank() != rank):
+            raise ValueError("DistributedFrame: nranks %d / rank %d disagree with the process group" % (nranks, rank))
         self.dev, self.dist, self.rank = dev, dist, rank
         self.layout = TileLayout(xres, yres, nranks, tile)
         L = self.layout
-        self.frame = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda") if rank == 0 or nranks == 1 \
-            else None
-        self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda") \
-            if nranks > 1 else None
-        self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda") \
-            if nranks > 1 and rank == 0 else None
+        f32 = dict(dtype=torch.float32, device=device)
+        self.frame = torch.zeros((yres, xres, 3), **f32) if rank == 0 or nranks == 1 else None
+        self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), **f32) if nranks > 1 else None
+        self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), **f32) if nranks > 1 and rank == 0 else None
 
     def render_layer(self, cam, params, stream: int = 0):
         """params: chiaroscuro_amd.render_params(..., layer=L, rank, nranks, tile)."""
         L = self.layout
+        if (params.rank, params.nranks, params.tile or 32, params.xres, params.yres) != \
+                (self.rank, L.nranks, L.tile, L.xres, L.yres):
+            raise ValueError("render_layer: params do not match this frame's partition")
         if L.nranks == 1:
             self.dev.render_device(cam, params, self.frame.data_ptr(), stream)
             return

@@ -65,6 +65,10 @@ struct cr_ctx {
     // 1080p x 128 spp: 0 / 256K / 1M / 4M / 16M -> 594.7 / 591.6 / 590.2 / 592.9 / 626.5 ms;
     // rank 0 of an 8-way split: 0 / 64K / 256K / 1M / 4M -> 88.8 / 85.9 / 83.3 / 83.1 / 84.2 ms
     uint32_t wf_tail_min = 1u << 20;
+    // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a
+    // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
+    // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do
+    uint64_t sample_buf = cr::SAMPLE_BUF_BYTES;
 };
 
 namespace {
@@ -186,7 +190,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         // samples per chunk: the per-sample buffer stays within SAMPLE_BUF_BYTES
         // and the work index within 31 bits
         const uint64_t per_sample = (uint64_t)A.n_items * 12u;
-        uint64_t chunk = std::max<uint64_t>(1, cr::SAMPLE_BUF_BYTES / std::max<uint64_t>(per_sample, 1));
+        uint64_t chunk = std::max<uint64_t>(1, c->sample_buf / std::max<uint64_t>(per_sample, 1));
         chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(1, (1ull << 31) / std::max<uint32_t>(A.n_items, 1)));
         chunk = std::min<uint64_t>(chunk, p->spp);
         const bool chunked = chunk < p->spp;
@@ -715,6 +719,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_dir_res") && v >= 1 && v <= 256 && (v & (v - 1)) == 0)
         c->wf_dir_res = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
+    else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
     return CR_OK;
 }

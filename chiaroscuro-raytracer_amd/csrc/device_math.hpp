@@ -128,43 +128,67 @@ __device__ __forceinline__ uint32_t rng_index(Rng &r, uint32_t n) {
 }
 
 // ------------------------------------------------------------ sincos --
-// Same double-precision evaluation as oracle/oracle.c cr_sincosf.
-__device__ __forceinline__ void cr_sincosf(float xf, float &s, float &c) {
-    const double PIO2_1 = 1.57079632673412561417e+00, PIO2_1T = 6.07710050650619224932e-11;
-    const double TWO_OVER_PI = 6.36619772367581382433e-01;
-    double x = (double)xf;
-    double k = floor(x * TWO_OVER_PI + 0.5);
-    int q = (int)k;
-    double r = (x - k * PIO2_1) - k * PIO2_1T;
-    double r2 = r * r;
-    double ps = 1.0 / 355687428096000.0;
-    ps = -1.0 / 1307674368000.0 + r2 * ps;
-    ps = 1.0 / 6227020800.0 + r2 * ps;
-    ps = -1.0 / 39916800.0 + r2 * ps;
-    ps = 1.0 / 362880.0 + r2 * ps;
-    ps = -1.0 / 5040.0 + r2 * ps;
-    ps = 1.0 / 120.0 + r2 * ps;
-    ps = -1.0 / 6.0 + r2 * ps;
-    double sv = r + r * (r2 * ps);
-    double pc = 1.0 / 6402373705728000.0;
-    pc = -1.0 / 20922789888000.0 + r2 * pc;
-    pc = 1.0 / 87178291200.0 + r2 * pc;
-    pc = -1.0 / 479001600.0 + r2 * pc;
-    pc = 1.0 / 3628800.0 + r2 * pc;
-    pc = -1.0 / 40320.0 + r2 * pc;
-    pc = 1.0 / 720.0 + r2 * pc;
-    pc = -1.0 / 24.0 + r2 * pc;
-    pc = 1.0 / 2.0 + r2 * pc;
-    double cv = 1.0 - r2 * pc;
-    double S, C;
-    switch (q & 3) {
-    case 0: S = sv; C = cv; break;
-    case 1: S = cv; C = -sv; break;
-    case 2: S = -sv; C = -cv; break;
-    default: S = -cv; C = sv; break;
+// glibc's sinf / cosf, the functions src/brdf.cpp:52-53 calls (glibc 2.35,
+// x86-64 FMA ifunc; sysdeps/ieee754/flt-32 s_sinf.c / s_cosf.c / sincosf.h):
+// double-precision polynomials on the argument reduced by a 2^24-scaled 2/pi,
+// every a*b+c of the C source contracted to one fma as the -mfma build does.
+// The same op sequence is oracle/oracle.c glibc_sincosf, checked equal to the
+// host's libm sinf / cosf on every float with |x| < 120 (tests/test_oracle_golden.py
+// samples it; scripts/glibc_trig_check.c sweeps all 2.25e9) and run against libm on
+// the GPU over all of [0, 2pi] (tests/native/numerics_check.hip).
+// The coefficients are glibc's __sincosf_table[0] as libm holds it; table [1]
+// (quadrants 2, 3) is [0] with the cosine coefficients negated, which negates the
+// cosine polynomial exactly (round-to-nearest is sign-symmetric), so it is
+// applied as a sign on the result.
+namespace glibc_sincos {
+constexpr double HPI_INV = 0x1.45f306dc9c883p+23, HPI = 0x1.921fb54442d18p+0;
+constexpr double C0 = 0x1p0, C1 = -0x1.ffffffd0c621cp-2, C2 = 0x1.55553e1068f19p-5, C3 = -0x1.6c087e89a359dp-10,
+                 C4 = 0x1.99343027bf8c3p-16;
+constexpr double S1 = -0x1.555545995a603p-3, S2 = 0x1.1107605230bc4p-7, S3 = -0x1.994eb3774cf24p-13;
+} // namespace glibc_sincos
+__device__ __forceinline__ uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ffu; }
+// sincosf.h sinf_poly, n even (sine) and odd (cosine)
+__device__ __forceinline__ double glibc_sin_poly(double x, double x2) {
+    using namespace glibc_sincos;
+    const double x3 = x * x2;
+    const double s1 = __fma_rn(x2, S3, S2);
+    const double x7 = x3 * x2;
+    const double s = __fma_rn(x3, S1, x);
+    return __fma_rn(x7, s1, s);
+}
+__device__ __forceinline__ double glibc_cos_poly(double x2) {
+    using namespace glibc_sincos;
+    const double x4 = x2 * x2;
+    const double c2 = __fma_rn(x2, C4, C3);
+    const double c1 = __fma_rn(x2, C1, C0);
+    const double x6 = x4 * x2;
+    const double c = __fma_rn(x4, C2, c1);
+    return __fma_rn(x6, c2, c);
+}
+// s_sinf.c / s_cosf.c for |y| < 120 (theta of concentric() lies in [0, 2pi])
+__device__ __forceinline__ void cr_sincosf(float y, float &sn, float &cs) {
+    double x = (double)y;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) { // |y| < ~pi/4
+        if (abstop12(y) < abstop12(0x1p-12f)) {
+            sn = y;
+            cs = 1.0f;
+            return;
+        }
+        const double x2 = x * x;
+        sn = (float)glibc_sin_poly(x, x2);
+        cs = (float)glibc_cos_poly(x2);
+        return;
     }
-    s = (float)S;
-    c = (float)C;
+    // reduce_fast, !TOINT_INTRINSICS: the quadrant from the 2^24-scaled product
+    const double r = x * glibc_sincos::HPI_INV;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    x = __fma_rn(-(double)n, glibc_sincos::HPI, x);
+    const double xs = ((n & 3) == 1 || (n & 3) == 2) ? -x : x; // sign[n & 3] = {1, -1, -1, 1}
+    const double x2 = x * x;
+    const double ps = glibc_sin_poly(xs, x2), pc = (n & 2) ? -glibc_cos_poly(x2) : glibc_cos_poly(x2);
+    // odd quadrants swap the polynomials (sinf_poly(.., n) / (.., n ^ 1))
+    sn = (float)((n & 1) ? pc : ps);
+    cs = (float)((n & 1) ? ps : pc);
 }
 
 // --------------------------------------------------------------- BRDF --

@@ -91,7 +91,8 @@ int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t s
 // work items [w0, w0 + P) advance one bounce per generation through separate
 // kernels (camera, closest trace, shade, shadow trace, bounce) that exchange
 // rays through queues in HBM.
-enum : uint32_t { WF_CNT = 256 }; // counters: closest count [g], shadow count [64+g], work [128+g], [192+g]
+// counters: closest count [g], shadow count [WF_G+g], work [2*WF_G+g], [3*WF_G+g]; g <= K + 1 <= 65
+enum : uint32_t { WF_G = 66, WF_CNT = 4 * WF_G };
 enum { WF_STATE = 5 };            // path-state float4 slots per path
 struct WfArgs {
     uint32_t P;       // path slots of this chunk

@@ -57,9 +57,9 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, u
 }
 
 __device__ __forceinline__ uint32_t *cnt_closest(const WfArgs &W, uint32_t g) { return W.cnt + g; }
-__device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 64 + g; }
-__device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 128 + g; }
-__device__ __forceinline__ uint32_t *work_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 192 + g; }
+__device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + WF_G + g; }
+__device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 2 * WF_G + g; }
+__device__ __forceinline__ uint32_t *work_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 3 * WF_G + g; }
 
 // Queue sort key (raysort.hip): 8x8-pixel sub-tile of the path's pixel, then an
 // 8x8 octahedral direction bin.  Any deterministic key is exact -- it only
@@ -686,7 +686,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
         hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, st, A, W, g);
         uint32_t cnt[2] = {0u, 0u}; // shadow queue g, closest queue g + 1
-        if ((err = (int)hipMemcpyAsync(&cnt[0], W.cnt + 64 + g, 4, hipMemcpyDeviceToHost, st)) ||
+        if ((err = (int)hipMemcpyAsync(&cnt[0], W.cnt + WF_G + g, 4, hipMemcpyDeviceToHost, st)) ||
             (err = (int)hipMemcpyAsync(&cnt[1], W.cnt + g + 1, 4, hipMemcpyDeviceToHost, st)) ||
             (err = (int)hipStreamSynchronize(st)))
             break;

@@ -82,52 +82,70 @@ static inline uint32_t rng_index(rng_t *r, uint32_t n) {
 }
 
 /* ------------------------------------------------------------- sincos -- */
-/* Correctly-rounded-in-practice sinf/cosf evaluated in double (identical op
- * sequence in csrc/kernels.hip).  Exhaustively equal to (float)sin((double)x) on
- * [0, 2pi]; differs from glibc sinf/cosf (0.56 ulp) on ~0.09%/0.04% of inputs by
- * one ulp -- see DESIGN.md.  or_set_trig_mode(1) switches to glibc. */
+/* glibc's sinf / cosf, which src/brdf.cpp:52-53 calls: glibc 2.35 x86-64 (FMA
+ * ifunc) sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h -- double
+ * polynomials after a 2^24-scaled 2/pi reduction, each a*b+c of the source one
+ * fma as the -mfma build contracts it; coefficients = __sincosf_table[0] as libm
+ * holds it (table [1] = cosine coefficients negated, applied as a sign on the
+ * cosine polynomial, which is exact).  The kernels run the same op sequence
+ * (csrc/device_math.hpp cr_sincosf).  or_sincos_check sweeps it against the
+ * host libm: equal on every float with |x| < 120 (2.25e9 values).
+ * or_set_trig_mode(1) calls libm sinf / cosf instead. */
 static int g_trig_mode = 0;
 void or_set_trig_mode(int mode) { g_trig_mode = mode; }
-static void cr_sincosf(float xf, float *s, float *c) {
-    const double PIO2_1 = 1.57079632673412561417e+00, PIO2_1T = 6.07710050650619224932e-11;
-    const double TWO_OVER_PI = 6.36619772367581382433e-01;
-    double x = (double)xf;
-    double k = floor(x * TWO_OVER_PI + 0.5);
-    int q = (int)k;
-    double r = (x - k * PIO2_1) - k * PIO2_1T;
-    double r2 = r * r;
-    double ps = 1.0 / 355687428096000.0;
-    ps = -1.0 / 1307674368000.0 + r2 * ps;
-    ps = 1.0 / 6227020800.0 + r2 * ps;
-    ps = -1.0 / 39916800.0 + r2 * ps;
-    ps = 1.0 / 362880.0 + r2 * ps;
-    ps = -1.0 / 5040.0 + r2 * ps;
-    ps = 1.0 / 120.0 + r2 * ps;
-    ps = -1.0 / 6.0 + r2 * ps;
-    double sv = r + r * (r2 * ps);
-    double pc = 1.0 / 6402373705728000.0;
-    pc = -1.0 / 20922789888000.0 + r2 * pc;
-    pc = 1.0 / 87178291200.0 + r2 * pc;
-    pc = -1.0 / 479001600.0 + r2 * pc;
-    pc = 1.0 / 3628800.0 + r2 * pc;
-    pc = -1.0 / 40320.0 + r2 * pc;
-    pc = 1.0 / 720.0 + r2 * pc;
-    pc = -1.0 / 24.0 + r2 * pc;
-    pc = 1.0 / 2.0 + r2 * pc;
-    double cv = 1.0 - r2 * pc;
-    double S, C;
-    switch (q & 3) {
-    case 0: S = sv; C = cv; break;
-    case 1: S = cv; C = -sv; break;
-    case 2: S = -sv; C = -cv; break;
-    default: S = -cv; C = sv; break;
+static uint32_t abstop12(float x) { uint32_t u; memcpy(&u, &x, 4); return (u >> 20) & 0x7ffu; }
+static const double GS_HPI_INV = 0x1.45f306dc9c883p+23, GS_HPI = 0x1.921fb54442d18p+0;
+static const double GS_C0 = 0x1p0, GS_C1 = -0x1.ffffffd0c621cp-2, GS_C2 = 0x1.55553e1068f19p-5,
+                    GS_C3 = -0x1.6c087e89a359dp-10, GS_C4 = 0x1.99343027bf8c3p-16;
+static const double GS_S1 = -0x1.555545995a603p-3, GS_S2 = 0x1.1107605230bc4p-7, GS_S3 = -0x1.994eb3774cf24p-13;
+static double gs_sin_poly(double x, double x2) {
+    double x3 = x * x2, s1 = fma(x2, GS_S3, GS_S2), x7 = x3 * x2, s = fma(x3, GS_S1, x);
+    return fma(x7, s1, s);
+}
+static double gs_cos_poly(double x2) {
+    double x4 = x2 * x2, c2 = fma(x2, GS_C4, GS_C3), c1 = fma(x2, GS_C1, GS_C0), x6 = x4 * x2;
+    double c = fma(x4, GS_C2, c1);
+    return fma(x6, c2, c);
+}
+static void glibc_sincosf(float y, float *sn, float *cs) {
+    double x = (double)y;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        if (abstop12(y) < abstop12(0x1p-12f)) { *sn = y; *cs = 1.0f; return; }
+        double x2 = x * x;
+        *sn = (float)gs_sin_poly(x, x2);
+        *cs = (float)gs_cos_poly(x2);
+        return;
     }
-    *s = (float)S;
-    *c = (float)C;
+    double r = x * GS_HPI_INV;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    x = fma(-(double)n, GS_HPI, x);
+    double xs = ((n & 3) == 1 || (n & 3) == 2) ? -x : x, x2 = x * x;
+    double ps = gs_sin_poly(xs, x2), pc = (n & 2) ? -gs_cos_poly(x2) : gs_cos_poly(x2);
+    *sn = (float)((n & 1) ? pc : ps);
+    *cs = (float)((n & 1) ? ps : pc);
 }
 void or_sincos(float x, float *s, float *c) {
     if (g_trig_mode == 1) { *s = sinf(x); *c = cosf(x); }
-    else cr_sincosf(x, s, c);
+    else glibc_sincosf(x, s, c);
+}
+/* mismatches of glibc_sincosf vs libm sinf / cosf over the float bit patterns
+ * lo, lo + stride, ... <= hi (both signs when both_signs) */
+uint64_t or_sincos_check(uint32_t lo, uint32_t hi, uint32_t stride, int both_signs, int threads) {
+    uint64_t bad = 0;
+    const int nt = threads > 0 ? threads : omp_get_max_threads();
+    #pragma omp parallel for num_threads(nt) reduction(+ : bad) schedule(static)
+    for (int64_t i = lo; i <= (int64_t)hi; i += stride) {
+        for (int sg = 0; sg <= both_signs; sg++) {
+            uint32_t u = (uint32_t)i | (sg ? 0x80000000u : 0u);
+            float x, a, b, c, d;
+            memcpy(&x, &u, 4);
+            glibc_sincosf(x, &a, &b);
+            c = sinf(x);
+            d = cosf(x);
+            bad += (memcmp(&a, &c, 4) != 0) + (memcmp(&b, &d, 4) != 0);
+        }
+    }
+    return bad;
 }
 
 /* -------------------------------------------------------------- scene -- */

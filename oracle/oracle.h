@@ -104,9 +104,10 @@ float or_light_surface(const float p[9]);
 void or_tonemap(const float *rgb, uint32_t xres, uint32_t yres, float exposure, float defog, float kneeLow,
                 float kneeHigh, float gamma, uint8_t *out);
 
-/* trig mode: 0 = shared correctly-rounded sincos (bit-exact with the HIP path),
- * 1 = glibc sinf/cosf exactly as src/brdf.cpp:52-53 calls them. */
+/* trig mode: 0 = restatement of glibc sinf / cosf (bit-exact with the HIP path and
+ * with libm on every |x| < 120), 1 = call the host libm sinf / cosf */
 void or_set_trig_mode(int mode);
+uint64_t or_sincos_check(uint32_t lo, uint32_t hi, uint32_t stride, int both_signs, int threads);
 
 #ifdef __cplusplus
 }

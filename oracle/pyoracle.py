@@ -59,6 +59,7 @@ def lib():
             "or_render": (None, [P, FP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, FP, C.c_uint32, C.c_uint32,
                                  C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, FP, C.POINTER(C.c_uint64)]),
             "or_set_trig_mode": (None, [C.c_int]),
+            "or_sincos_check": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int]),
             "or_glm_normalize": (None, [FP, FP]),
             "or_glm_cross": (None, [FP, FP, FP]),
             "or_glm_dot": (C.c_float, [FP, FP]),
@@ -202,6 +203,12 @@ def tonemap(rgb, exposure, defog=0.0, knee_low=0.0, knee_high=5.0, gamma=2.2):
     lib().or_tonemap(_p(rgb), rgb.shape[1], rgb.shape[0], exposure, defog, knee_low, knee_high, gamma,
                      out.ctypes.data_as(C.POINTER(C.c_uint8)))
     return out
+
+
+def sincos_check(lo: int, hi: int, stride: int = 1, both_signs: bool = True, threads: int = 0) -> int:
+    """Mismatches of the glibc sinf / cosf restatement vs the host libm over float
+    bit patterns lo..hi step stride (and their negatives)."""
+    return int(lib().or_sincos_check(lo, hi, stride, int(both_signs), threads))
 
 
 def set_trig_mode(mode: int):

@@ -57,9 +57,16 @@ def main(src, dst, spp=128):
         if a[1] != "false":
             continue
         kind = "shadow" if a[0] == "true" else ("camera" if len(a) > 8 and a[8] == "true" else "closest")
+        d = v["dispatches"]
         kinds[kind] = {"kernel": k, "valu_issue_busy": v["valu_issue_busy"], "salu_issue_busy": v["salu_issue_busy"],
                        "ta_busy": v.get("ta_busy"), "shader_clock_ghz": v["shader_clock_ghz"],
-                       "salu_per_valu": v["salu_per_valu"]}
+                       "salu_per_valu": v["salu_per_valu"], "dispatches": d,
+                       "avg_launch_ms": round(v["seconds"] * 1e3 / d, 3),
+                       # per-launch instruction counts: bench.py roofline (issue ceilings) divides
+                       # them by its own live HIP-event launch time
+                       "valu_insts_per_launch": v["SQ_INSTS_VALU"] / d,
+                       "salu_insts_per_launch": v["SQ_INSTS_SALU"] / d,
+                       "vmem_rd_insts_per_launch": v["SQ_INSTS_VMEM_RD"] / d}
     json.dump({"spp": spp, "note": __doc__.strip().split("\n\n")[0], "kinds": kinds, "kernels": out},
               open(dst, "w"), indent=1)
     for k, v in out.items():

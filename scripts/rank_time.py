@@ -1,6 +1,8 @@
 """Per-rank render time of the tile split on ONE GPU (rehearses N-GPU scaling
-without N GPUs): renders rank 0's tiles of an N-way split and reports the pass
-time and Mray/s, for N in --nranks.
+without N GPUs): renders EVERY rank's tiles of an N-way split one after another
+and reports each rank's pass time; a strong-scaling step ends with the slowest
+rank, so the projected speedup is t(1) / max over ranks of t(rank), for N in
+--nranks.
     python scripts/rank_time.py [--config sponza] [--nranks 1,2,4,8] [--rounds 2]
 """
 import argparse
@@ -37,19 +39,25 @@ def main():
     res = {}
     for r in range(args.rounds):
         for n in (int(x) for x in args.nranks.split(",")):
-            p = ca.render_params(i["xres"], i["yres"], spp, i["k"], i["seed"], rank=0, nranks=n)
-            tiles = torch.zeros((ca.Device.tiles_for_rank(p, 0), 32, 32, 3), dtype=torch.float32, device="cuda")
-            dev.render_tiles_device(cam, p, tiles.data_ptr())
-            torch.cuda.synchronize()
-            c = dev.counters()
-            res.setdefault(n, []).append((dev.last_kernel_ms(), c["closest"] + c["shadow"]))
+            for rank in range(n):
+                p = ca.render_params(i["xres"], i["yres"], spp, i["k"], i["seed"], rank=rank, nranks=n)
+                tiles = torch.zeros((ca.Device.tiles_for_rank(p, rank), 32, 32, 3), dtype=torch.float32,
+                                    device="cuda")
+                dev.render_tiles_device(cam, p, tiles.data_ptr())
+                torch.cuda.synchronize()
+                c = dev.counters()
+                res.setdefault(n, {}).setdefault(rank, []).append((dev.last_kernel_ms(), c["closest"] + c["shadow"]))
     base = None
-    for n, xs in sorted(res.items()):
-        ms = statistics.median(x[0] for x in xs)
-        rays = xs[0][1]
-        base = base or ms
-        print(json.dumps({"nranks": n, "rank0_ms": round(ms, 2), "rank0_mray_s": round(rays / ms / 1e3, 1),
-                          "ideal_ms": round(base / n, 2), "projected_speedup": round(base / ms, 2)}), flush=True)
+    for n, ranks in sorted(res.items()):
+        ms = {rk: statistics.median(x[0] for x in xs) for rk, xs in ranks.items()}
+        rays = sum(xs[0][1] for xs in ranks.values())
+        slow = max(ms, key=ms.get)
+        base = base or ms[0]
+        print(json.dumps({"nranks": n, "rank_ms": [round(ms[rk], 2) for rk in sorted(ms)], "max_rank_ms":
+                          round(ms[slow], 2), "slowest_rank": slow, "rank0_ms": round(ms[0], 2),
+                          "imbalance": round(ms[slow] / (sum(ms.values()) / n), 3),
+                          "projected_mray_s": round(rays / ms[slow] / 1e3, 1), "ideal_ms": round(base / n, 2),
+                          "projected_speedup": round(base / ms[slow], 2)}), flush=True)
 
 
 if __name__ == "__main__":

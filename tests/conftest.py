@@ -28,10 +28,13 @@ def pytest_configure(config):
 
 
 def _ensure_built():
-    libs = [PKG / "lib" / "libchiaro_hip.so", PKG / "lib" / "libchiaroscuro.so", ROOT / "oracle" / "liboracle.so"]
-    if not all(p.exists() for p in libs):
-        subprocess.run(["make", "-s", "-j8", "-C", str(PKG)], check=True)
-        subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+    """The libraries under test are the ones built from this tree's sources: `make -q`
+    asks whether any target is older than its sources (a no-op check when the
+    pushed binaries are current) and only then rebuilds incrementally."""
+    for d, jobs in ((PKG, "-j8"), (ROOT / "oracle", "-j1")):
+        if subprocess.run(["make", "-q", "-C", str(d)], stdout=subprocess.DEVNULL).returncode != 0:
+            sys.stderr.write("conftest: %s is stale or unbuilt; running make\n" % d)
+            subprocess.run(["make", "-s", jobs, "-C", str(d)], check=True)
 
 
 _ensure_built()

@@ -1,13 +1,19 @@
 // GPU check of the exact fast-division helpers of device_math.hpp against the
 // correctly rounded hardware-sequence division (what the reference's float
-// division gives).  Built and run by tests/test_gpu_numerics.py.
+// division gives), and of the kernels' sinf / cosf against the host's glibc
+// libm (what src/brdf.cpp:52-53 calls).  Built and run by tests/test_gpu_numerics.py.
 //   rcp_rn      : every one of the 2^32 float bit patterns
 //   div_by_rcp  : random bit patterns of a and b (all classes, all exponents)
 //                 and pairs whose quotient sits next to a rounding midpoint
+//   cr_sincosf  : every float in [-2pi, 2pi] (concentric()'s theta lies in [0, 2pi])
+//                 against libm sinf / cosf on the host
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "device_math.hpp"
 
@@ -70,6 +76,51 @@ __global__ void div_random(uint64_t seed, unsigned long long *bad, unsigned long
     atomicAdd(fast, (unsigned long long)nf);
 }
 
+__global__ void sincos_batch(uint32_t u0, uint32_t n, float2 *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float sn, cs;
+    cr_sincosf(__uint_as_float(u0 + i), sn, cs);
+    out[i] = make_float2(sn, cs);
+}
+
+// device sincos vs host libm over float patterns [0, hi] of both signs
+static int sincos_sweep(uint32_t hi, unsigned long long &bad, uint32_t &first, unsigned long long &tested) {
+    const uint32_t B = 1u << 25;
+    float2 *d = nullptr;
+    if (hipMalloc(&d, (size_t)B * sizeof(float2)) != hipSuccess) return 2;
+    std::vector<float2> h(B);
+    bad = tested = 0;
+    first = 0;
+    for (int sg = 0; sg < 2; sg++) {
+        for (uint64_t u0 = 0; u0 <= hi; u0 += B) {
+            const uint32_t n = (uint32_t)std::min<uint64_t>(B, (uint64_t)hi + 1 - u0);
+            const uint32_t base = (uint32_t)u0 | (sg ? 0x80000000u : 0u);
+            hipLaunchKernelGGL(sincos_batch, dim3((n + 255) / 256), dim3(256), 0, 0, base, n, d);
+            if (hipMemcpy(h.data(), d, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost) != hipSuccess) return 2;
+            unsigned long long b = 0;
+            uint32_t f = 0;
+#pragma omp parallel for reduction(+ : b) schedule(static)
+            for (uint32_t i = 0; i < n; i++) {
+                const uint32_t u = base + i;
+                float x;
+                std::memcpy(&x, &u, 4);
+                const float es = sinf(x), ec = cosf(x);
+                if (std::memcmp(&es, &h[i].x, 4) || std::memcmp(&ec, &h[i].y, 4)) {
+                    b++;
+#pragma omp critical
+                    if (!f) f = u;
+                }
+            }
+            bad += b;
+            if (!first) first = f;
+            tested += n;
+        }
+    }
+    (void)hipFree(d);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 16;
     unsigned long long *d;
@@ -89,8 +140,15 @@ int main(int argc, char **argv) {
     (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
     (void)hipMemcpy(hf, f, sizeof(hf), hipMemcpyDeviceToHost);
     const unsigned long long pairs = (unsigned long long)rounds * (1ull << 16) * 256 * 64;
+    unsigned long long sc_bad = 0, sc_tested = 0;
+    uint32_t sc_first = 0;
+    float two_pi = 6.2831855f; // float above 2pi
+    uint32_t hi;
+    std::memcpy(&hi, &two_pi, 4);
+    if (sincos_sweep(hi, sc_bad, sc_first, sc_tested)) return 2;
     printf("{\"rcp_patterns\": 4294967296, \"rcp_mismatch\": %llu, \"rcp_first\": \"0x%08x\", "
-           "\"div_pairs\": %llu, \"div_fast_path\": %llu, \"div_mismatch\": %llu, \"div_first_a\": \"0x%08x\"}\n",
-           h[0], hf[0], pairs, h[2], h[1], hf[1]);
-    return (h[0] || h[1]) ? 1 : 0;
+           "\"div_pairs\": %llu, \"div_fast_path\": %llu, \"div_mismatch\": %llu, \"div_first_a\": \"0x%08x\", "
+           "\"sincos_tested\": %llu, \"sincos_mismatch\": %llu, \"sincos_first\": \"0x%08x\"}\n",
+           h[0], hf[0], pairs, h[2], h[1], hf[1], sc_tested, sc_bad, sc_first);
+    return (h[0] || h[1] || sc_bad) ? 1 : 0;
 }

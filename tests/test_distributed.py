@@ -1,10 +1,11 @@
 """Multi-rank frame protocol on the CPU (gloo, world_size 2) -- SURVEY §8e.
 
-Each rank computes the batch means of ITS tiles (tile t -> rank t % N) into the
-compact [ntiles_r][tile][tile][3] buffer that cr_render_tiles_device fills on a
-GPU (here from the oracle's per-path radiance, summed in sample order), rank 0
-gathers them with torch.distributed and unpermutes + blends them exactly as
-blend_tiles_kernel does.  The result must equal the oracle's single-process
+The product's DistributedFrame.render_layer (chiaroscuro_amd/tiles.py) drives
+each rank: it renders ITS tiles (tile t -> rank t % N) into the compact
+[ntiles_r][tile][tile][3] buffer through the device's render_tiles_device (here
+an oracle-backed stand-in, per-path radiance summed in sample order), gathers
+them on rank 0 with torch.distributed, and has the device unpermute + blend
+them (the stand-in mirrors blend_tiles_kernel).  The result must equal the oracle's single-process
 progressive render bit for bit, layer after layer: the image does not depend
 on the partition.  The tile arithmetic is also checked against the C-ABI's
 cr_tiles_for_rank.
@@ -36,7 +37,8 @@ def _setup_paths():
 
 
 def blend_tiles_reference(gathered, layout, frame, layer):
-    """numpy mirror of blend_tiles_kernel (csrc/kernels.hip) -- test helper only."""
+    """numpy mirror of blend_tiles_kernel (csrc/kernels.hip) -- test helper only;
+    the kernel itself is checked on the GPU (test_gpu_parity tile tests)."""
     T = layout.tile
     for r in range(layout.nranks):
         for lt in range(layout.tiles_for_rank(r)):
@@ -47,57 +49,105 @@ def blend_tiles_reference(gathered, layout, frame, layer):
             frame[y0:y0 + h, x0:x0 + w] = (old * np.float32(layer - 1) + m) / np.float32(layer)
 
 
-def rank_tiles(osc, cam, info, layout, rank, layer):
-    """This rank's compact buffer: per pixel temp = sum_s path(s) in order, mean = temp * (1/spp)."""
-    buf = np.zeros((layout.max_tiles, TILE, TILE, 3), np.float32)
-    inv = np.float32(1.0) / np.float32(SPP)
-    for lt in range(layout.tiles_for_rank(rank)):
-        x0, y0 = layout.tile_origin(rank, lt)
-        for yy in range(min(TILE, YRES - y0)):
-            for xx in range(min(TILE, XRES - x0)):
-                temp = np.zeros(3, np.float32)
-                for s in range(SPP):
-                    temp = temp + osc.path(cam, XRES, YRES, info["k"], info["background"], info["seed"], layer,
-                                           x0 + xx, y0 + yy, s)
-                buf[lt, yy, xx] = temp * inv
-    return buf
+def _view(ptr: int, shape):
+    """numpy view of a CPU torch buffer handed over by address (as the C-ABI gets it)."""
+    import ctypes
+    n = int(np.prod(shape))
+    return np.ctypeslib.as_array((ctypes.c_float * n).from_address(ptr)).reshape(shape)
+
+
+class OracleTileDevice:
+    """Stand-in for chiaroscuro_amd.Device behind DistributedFrame on the CPU: the
+    same three entry points taking buffer addresses, computed by the oracle --
+    per pixel temp = sum_s path(s) in sample order, mean = temp * (1/spp)."""
+
+    def __init__(self, osc, cam, info):
+        self.osc, self.cam, self.info = osc, cam, info
+        self.calls = []
+
+    def _mean(self, p, x, y):
+        temp = np.zeros(3, np.float32)
+        for s in range(p.spp):
+            temp = temp + self.osc.path(self.cam, p.xres, p.yres, p.k, self.info["background"], p.seed, p.layer,
+                                        x, y, s)
+        return temp * (np.float32(1.0) / np.float32(p.spp))
+
+    def render_tiles_device(self, cam, p, ptr, stream=0):
+        from chiaroscuro_amd.tiles import TileLayout
+        lay = TileLayout(p.xres, p.yres, p.nranks, p.tile)
+        T = lay.tile
+        buf = _view(ptr, (lay.max_tiles, T, T, 3))
+        for lt in range(lay.tiles_for_rank(p.rank)):
+            x0, y0 = lay.tile_origin(p.rank, lt)
+            for yy in range(min(T, p.yres - y0)):
+                for xx in range(min(T, p.xres - x0)):
+                    buf[lt, yy, xx] = self._mean(p, x0 + xx, y0 + yy)
+        self.calls.append(("tiles", p.rank, p.layer))
+
+    def blend_tiles_device(self, p, gathered_ptr, frame_ptr, stream=0):
+        from chiaroscuro_amd.tiles import TileLayout
+        lay = TileLayout(p.xres, p.yres, p.nranks, p.tile)
+        g = _view(gathered_ptr, (p.nranks, lay.max_tiles, lay.tile, lay.tile, 3))
+        blend_tiles_reference(g, lay, _view(frame_ptr, (p.yres, p.xres, 3)), p.layer)
+        self.calls.append(("blend", p.rank, p.layer))
+
+    def render_device(self, cam, p, frame_ptr, stream=0):
+        f = _view(frame_ptr, (p.yres, p.xres, 3))
+        for y in range(p.yres):
+            for x in range(p.xres):
+                m = self._mean(p, x, y)
+                f[y, x] = m if p.layer == 1 else (f[y, x] * np.float32(p.layer - 1) + m) / np.float32(p.layer)
+        self.calls.append(("frame", p.rank, p.layer))
 
 
 def _worker(rank, world, port, q):
     try:
         _setup_paths()
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CHIARO_QUIET="1")
-        import torch
         import torch.distributed as dist
         import chiaroscuro_amd as ca
         import pyoracle as po
         from chiaroscuro_amd import scenes
-        from chiaroscuro_amd.tiles import TileLayout
+        from chiaroscuro_amd.tiles import DistributedFrame
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
         sc = ca.Scene(scenes.config_rtc("cornell"))
         info = sc.info
         m = ca.Model(sc)
         osc = po.OracleScene(m.triangles(), leaf_size=info["leaf_size"])
-        cam = ca.camera(info["VP"], info["LA"], info["UP"], info["yview"], XRES, YRES).as_array()
-        layout = TileLayout(XRES, YRES, world, TILE)
-        frame = np.zeros((YRES, XRES, 3), np.float32)
+        cam = ca.camera(info["VP"], info["LA"], info["UP"], info["yview"], XRES, YRES)
+        dev = OracleTileDevice(osc, cam.as_array(), info)
+        # the product's frame protocol: render my tiles, gather to rank 0, blend there
+        fr = DistributedFrame(dev, XRES, YRES, rank, world, TILE, dist, device="cpu")
         ok = True
+        ref = None
         for layer in range(1, LAYERS + 1):
-            mine = torch.from_numpy(rank_tiles(osc, cam, info, layout, rank, layer))
-            gathered = [torch.zeros_like(mine) for _ in range(world)] if rank == 0 else None
-            dist.gather(mine, gathered, dst=0)
+            p = ca.render_params(XRES, YRES, SPP, info["k"], info["seed"], layer=layer, rank=rank, nranks=world,
+                                 tile=TILE, background=info["background"])
+            fr.render_layer(cam, p)
             if rank == 0:
-                blend_tiles_reference(torch.stack(gathered).numpy(), layout, frame, layer)
-                ref = np.zeros((YRES, XRES, 3), np.float32) if layer == 1 else ref
-                ref, _ = osc.render(cam, XRES, YRES, SPP, info["k"], info["seed"], layer=layer,
+                ref, _ = osc.render(cam.as_array(), XRES, YRES, SPP, info["k"], info["seed"], layer=layer,
                                     bg=info["background"], pixels=ref, threads=1)
+                frame = fr.frame.numpy()
                 ok = ok and bool((frame.view(np.uint32) == ref.view(np.uint32)).all()) and float(frame.mean()) > 0
+            else:
+                ok = ok and fr.frame is None and fr.gathered is None
+        want = [("tiles", rank, L) for L in range(1, LAYERS + 1)]
+        if rank == 0:
+            want = [c for L in range(1, LAYERS + 1) for c in (("tiles", 0, L), ("blend", 0, L))]
+        ok = ok and dev.calls == want
+        # a partition that disagrees with the process group is refused
+        try:
+            DistributedFrame(dev, XRES, YRES, rank, world + 1, TILE, dist, device="cpu")
+            ok = False
+        except ValueError:
+            pass
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, ok))
     except Exception as e:  # surfaced by the parent
-        q.put((rank, repr(e)))
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
 
 
 def test_tile_layout_matches_cabi(ca):

@@ -93,3 +93,18 @@ def test_goldens_are_current():
     subprocess.run([sys.executable, str(GOLD / "make_ref_golden.py")], check=True, capture_output=True)
     after = {p.name: p.read_bytes() for p in GOLD.glob("ref_*.json")}
     assert before == after
+
+
+def test_sincos_restatement_equals_host_libm(po):
+    """The oracle's (and the kernels') sinf / cosf restate glibc's algorithm
+    (s_sinf.c / s_cosf.c, FMA build): equal to the host libm that the reference
+    links, on every 31st float of [0, 2pi] (concentric()'s theta domain) and of
+    [2pi, 120) with both signs, plus every float near the quadrant / small-argument
+    boundaries (the full 2.25e9-value sweep is or_sincos_check(0, 0x42F00000, 1))."""
+    two_pi = int(np.float32(6.2831855).view(np.uint32))
+    assert po.sincos_check(0, two_pi, 31) == 0
+    assert po.sincos_check(two_pi, 0x42F00000, 97) == 0
+    for c in (np.float32(np.pi / 4), np.float32(2.0 ** -12), np.float32(np.pi / 2), np.float32(np.pi),
+              np.float32(3 * np.pi / 2)):
+        u = int(c.view(np.uint32))
+        assert po.sincos_check(u - (1 << 16), u + (1 << 16), 1) == 0
