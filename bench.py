@@ -138,7 +138,7 @@ def issue_roofline(dom, iss, views, issue, pass_view):
             "rocprof_avg_launch_ms": dom["rocprof_avg_launch_ms"], "bytes": bytes_view,
             "other_traces": {k: v for k, v in views.items() if v is not None and v is not dom},
             "issue": issue, "pass": pass_view}
-    if not iss or t <= 0:
+    if not iss or t <= 0 or "valu_insts_per_launch" not in iss:
         return {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(dom["achieved"] / HBM_PEAK_GBS, 5), "traffic": dom["traffic"],
                 "note": "no instruction-issue profile of this configuration: algorithmic bytes vs HBM", **base}
