@@ -6,7 +6,7 @@
 # line.  profiles/ written on the GPU box is copied to gpurun_out/profiles (merged back).
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/profiles
-TAG=${1:-r01}
+TAG=${1:?tag, e.g. r02}
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
 bash scripts/profile.sh $TAG --steps 2 --warmup 1 --no-cpu-baseline || exit 1
