@@ -181,6 +181,9 @@ def main():
     ap.add_argument("--kernel", type=int, default=-1,
                     help="2 wavefront (default), 0 persistent megakernel, 1 one-thread-per-pixel")
     ap.add_argument("--variant", type=int, default=-1, help="kernel build variant (default: the kernel's)")
+    ap.add_argument("--gather", default="torch", choices=("torch", "cabi"),
+                    help="N > 1: tile gather by torch.distributed (default) or the library's own RCCL "
+                         "communicator (cr_comm_init / cr_render_dist_device)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -229,8 +232,7 @@ def main():
     cam = ca.camera(info["VP"], info["LA"], info["UP"], info["yview"], xres, yres)
     tile = 32
     stream = torch.cuda.current_stream().cuda_stream
-    fr = DistributedFrame(dev, xres, yres, rank, world, tile, dist)
-    tiles = fr.tiles
+    fr = DistributedFrame(dev, xres, yres, rank, world, tile, dist, gather=args.gather)
 
     totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0,
               "trace_ms": [0.0] * 4, "trace_launches": [0] * 4}
@@ -295,7 +297,8 @@ def main():
     if world == 1:
         dev.render_device(cam, pc, scratch.data_ptr(), stream)
     else:
-        dev.render_tiles_device(cam, pc, tiles.data_ptr(), stream)
+        scratch_tiles = torch.zeros((fr.layout.max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda")
+        dev.render_tiles_device(cam, pc, scratch_tiles.data_ptr(), stream)
     cc = dev.counters()
     cts = dev.trace_stats() if wavefront else None
     totals["bytes"] = ca.algorithmic_bytes(cc, cc["pixels"])
@@ -387,7 +390,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic scene (deterministic generator), seeded counter RNG",
             "config": {"workload": label, "spp_per_step": spp, "k": k, "tile": tile,
-                       "parallelism": "tile-split x%d" % world, "rays": int(rays_all),
+                       "parallelism": "tile-split x%d" % world, "gather": args.gather if world > 1 else None,
+                       "rays": int(rays_all),
                        "rank_render_ms": rank_render_ms,
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": roofline,

@@ -23,7 +23,9 @@ PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_DIR = PKG_ROOT / "lib"
 
 CR_OK = 0
-CR_ERRORS = {-1: "CR_E_INVALID", -2: "CR_E_HIP", -3: "CR_E_NOSCENE", -4: "CR_E_DEPTH", -5: "CR_E_OOM"}
+CR_ERRORS = {-1: "CR_E_INVALID", -2: "CR_E_HIP", -3: "CR_E_NOSCENE", -4: "CR_E_DEPTH", -5: "CR_E_OOM",
+             -6: "CR_E_COMM"}
+COMM_ID_BYTES = 128  # CR_COMM_ID_BYTES
 
 f3 = C.c_float * 3
 
@@ -79,7 +81,7 @@ class ChiaroSceneInfo(C.Structure):
                 ("preview_height", C.c_uint32), ("leaf_size", C.c_uint32), ("seed", C.c_uint32),
                 ("k", C.c_int32), ("using_preview", C.c_int32), ("VP", f3), ("LA", f3), ("UP", f3),
                 ("background", f3), ("yview", C.c_float), ("exposure", C.c_float), ("n_invalid", C.c_uint32),
-                ("obj_path", C.c_char * 1024), ("render_path", C.c_char * 1024)]
+                ("obj_path", C.c_char * 1024), ("render_path", C.c_char * 1024), ("gpus", C.c_uint32)]
 
 
 TRACE_KINDS = ("camera", "closest", "shadow", "tail")  # cr_trace_stats order
@@ -109,7 +111,11 @@ _host = None
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
                "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_intersect",
                "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize",
-               "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap")
+               "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap",
+               "cr_comm_unique_id", "cr_comm_init", "cr_comm_destroy", "cr_render_dist_device",
+               "cr_device_count", "cr_group_create", "cr_group_destroy", "cr_group_last_error", "cr_group_size",
+               "cr_group_upload_scene", "cr_group_set_option", "cr_group_render", "cr_group_get_counters",
+               "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
                 "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
@@ -140,6 +146,11 @@ def libs():
     if not hip_path.exists() or not host_path.exists():
         raise RuntimeError("chiaroscuro_amd: native libraries not built (%s); run "
                            "`make -C chiaroscuro-raytracer_amd` or __graft_entry__.build()" % LIB_DIR)
+    # torch first: it carries its own HIP runtime and RCCL under the sonames
+    # libchiaro_hip.so needs (libamdhip64.so.7, librccl.so.1), so loaded in this
+    # order the process holds one copy of each (the other order maps a second
+    # runtime next to torch's, whose exit-time teardown collides with the first)
+    import torch  # noqa: F401
     hip = C.CDLL(str(hip_path), mode=C.RTLD_GLOBAL)
     host = C.CDLL(str(host_path))
     _sig(hip, "cr_create", P, [C.c_int])
@@ -162,6 +173,24 @@ def libs():
     _sig(hip, "cr_tonemap_device", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32, P, P, P])
     _sig(hip, "cr_tonemap", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32,
                                       C.POINTER(C.c_uint8)])
+
+    _sig(hip, "cr_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8), C.c_size_t])
+    _sig(hip, "cr_comm_init", C.c_int, [P, C.c_int, C.c_int, C.POINTER(C.c_uint8)])
+    _sig(hip, "cr_comm_destroy", C.c_int, [P])
+    _sig(hip, "cr_render_dist_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
+    _sig(hip, "cr_device_count", C.c_int, [])
+    _sig(hip, "cr_group_create", P, [C.c_int, C.POINTER(C.c_int)])
+    _sig(hip, "cr_group_destroy", None, [P])
+    _sig(hip, "cr_group_last_error", C.c_char_p, [P])
+    _sig(hip, "cr_group_size", C.c_int, [P])
+    _sig(hip, "cr_group_upload_scene", C.c_int, [P, C.POINTER(CrSceneDesc)])
+    _sig(hip, "cr_group_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
+    _sig(hip, "cr_group_render", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), FP])
+    _sig(hip, "cr_group_get_counters", C.c_int, [P, C.POINTER(CrCounters)])
+    _sig(hip, "cr_group_rank_ms", C.c_int, [P, FP])
+    _sig(hip, "cr_group_ctx", P, [P, C.c_int])
+    _sig(hip, "cr_group_tonemap", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32,
+                                            C.POINTER(C.c_uint8)])
 
     _sig(host, "chiaro_last_error", C.c_char_p, [])
     _sig(host, "chiaro_scene_create", P, [C.c_int, C.POINTER(C.c_char_p)])
@@ -248,7 +277,8 @@ class Scene:
                 "leaf_size": i.leaf_size, "VP": list(i.VP), "LA": list(i.LA), "UP": list(i.UP),
                 "yview": i.yview, "exposure": i.exposure, "background": list(i.background),
                 "preview_height": i.preview_height, "using_preview": bool(i.using_preview),
-                "n_invalid": i.n_invalid, "obj_path": i.obj_path.decode(), "render_path": i.render_path.decode()}
+                "n_invalid": i.n_invalid, "obj_path": i.obj_path.decode(), "render_path": i.render_path.decode(),
+                "gpus": i.gpus}
 
     def __del__(self):
         if getattr(self, "_h", None) and _host is not None:
@@ -427,6 +457,28 @@ class Device:
     def set_option(self, key: str, value: int):
         self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")
 
+    # multi-process frame split (one process per GPU, RCCL inside the library)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """cr_comm_unique_id: the RCCL id rank 0 makes and hands to every rank."""
+        buf = (C.c_uint8 * COMM_ID_BYTES)()
+        rc = libs()[0].cr_comm_unique_id(buf, COMM_ID_BYTES)
+        if rc != CR_OK:
+            raise RuntimeError("cr_comm_unique_id failed (%s)" % CR_ERRORS.get(rc, rc))
+        return bytes(buf)
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid[:COMM_ID_BYTES].ljust(COMM_ID_BYTES, b"\0"))
+        self._chk(libs()[0].cr_comm_init(self._c, int(nranks), int(rank), buf), "cr_comm_init")
+
+    def comm_destroy(self):
+        self._chk(libs()[0].cr_comm_destroy(self._c), "cr_comm_destroy")
+
+    def render_dist_device(self, cam, p, d_frame_ptr: int, stream: int = 0):
+        """cr_render_dist_device: my tiles, RCCL gather to rank 0, blend there."""
+        self._chk(libs()[0].cr_render_dist_device(self._c, C.byref(cam), C.byref(p), C.c_void_p(d_frame_ptr),
+                                                  C.c_void_p(stream)), "cr_render_dist_device")
+
     def synchronize(self):
         self._chk(libs()[0].cr_synchronize(self._c), "cr_synchronize")
 
@@ -434,6 +486,52 @@ class Device:
         if getattr(self, "_c", None):
             libs()[0].cr_destroy(self._c)
             self._c = None
+
+    def __del__(self):
+        if _hip is not None:
+            self.close()
+
+
+class Group:
+    """cr_group (include/chiaro_hip.h): one process driving N GPUs, the frame
+    tile-split over them and gathered to the first over RCCL."""
+
+    def __init__(self, devices):
+        hip, _ = libs()
+        devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+        self._g = hip.cr_group_create(len(devices), devs)
+        self.devices = list(devices)
+
+    def _chk(self, rc, what):
+        if rc != CR_OK:
+            raise RuntimeError("%s failed (%s): %s" % (what, CR_ERRORS.get(rc, rc),
+                                                       libs()[0].cr_group_last_error(self._g).decode()))
+
+    def upload(self, desc: CrSceneDesc):
+        self._chk(libs()[0].cr_group_upload_scene(self._g, C.byref(desc)), "cr_group_upload_scene")
+
+    def set_option(self, key: str, value: int):
+        self._chk(libs()[0].cr_group_set_option(self._g, key.encode(), int(value)), "cr_group_set_option")
+
+    def render(self, cam: CrCamera, p: CrRenderParams) -> np.ndarray:
+        out = np.zeros((p.yres, p.xres, 3), np.float32)
+        self._chk(libs()[0].cr_group_render(self._g, C.byref(cam), C.byref(p), _ptr(out)), "cr_group_render")
+        return out
+
+    def counters(self) -> dict:
+        c = CrCounters()
+        libs()[0].cr_group_get_counters(self._g, C.byref(c))
+        return c.as_dict()
+
+    def rank_ms(self) -> list:
+        out = np.zeros(len(self.devices), np.float32)
+        libs()[0].cr_group_rank_ms(self._g, _ptr(out))
+        return [float(x) for x in out]
+
+    def close(self):
+        if getattr(self, "_g", None):
+            libs()[0].cr_group_destroy(self._g)
+            self._g = None
 
     def __del__(self):
         if _hip is not None:

@@ -56,20 +56,32 @@ class DistributedFrame:
              the gloo tests pass an oracle-backed stand-in with device="cpu")
     dist     torch.distributed (initialised), or None for a single rank
     device   torch device of the frame / tile / gather buffers
+    gather   "torch": torch.distributed.gather of the tile buffers (RCCL under the
+             nccl backend), blend through cr_blend_tiles_device;
+             "cabi": the library's own RCCL communicator (cr_comm_init, the id
+             broadcast over `dist`) and cr_render_dist_device (render, grouped
+             send / receive to rank 0, blend, async-error polling) per layer
     """
 
     def __init__(self, dev, xres: int, yres: int, rank: int, nranks: int, tile: int = 32, dist=None,
-                 device: str = "cuda"):
+                 device: str = "cuda", gather: str = "torch"):
         import torch
         if nranks > 1 and (dist is None or dist.get_world_size() != nranks or dist.get_rank() != rank):
             raise ValueError("DistributedFrame: nranks %d / rank %d disagree with the process group" % (nranks, rank))
-        self.dev, self.dist, self.rank = dev, dist, rank
+        if gather not in ("torch", "cabi"):
+            raise ValueError("DistributedFrame: gather must be 'torch' or 'cabi'")
+        self.dev, self.dist, self.rank, self.gather = dev, dist, rank, gather
         self.layout = TileLayout(xres, yres, nranks, tile)
         L = self.layout
         f32 = dict(dtype=torch.float32, device=device)
         self.frame = torch.zeros((yres, xres, 3), **f32) if rank == 0 or nranks == 1 else None
-        self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), **f32) if nranks > 1 else None
-        self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), **f32) if nranks > 1 and rank == 0 else None
+        split = nranks > 1 and gather == "torch"
+        self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), **f32) if split else None
+        self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), **f32) if split and rank == 0 else None
+        if nranks > 1 and gather == "cabi":
+            uid = [dev.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            dev.comm_init(nranks, rank, uid[0])
 
     def render_layer(self, cam, params, stream: int = 0):
         """params: chiaroscuro_amd.render_params(..., layer=L, rank, nranks, tile)."""
@@ -79,6 +91,9 @@ class DistributedFrame:
             raise ValueError("render_layer: params do not match this frame's partition")
         if L.nranks == 1:
             self.dev.render_device(cam, params, self.frame.data_ptr(), stream)
+            return
+        if self.gather == "cabi":
+            self.dev.render_dist_device(cam, params, self.frame.data_ptr() if self.rank == 0 else 0, stream)
             return
         self.dev.render_tiles_device(cam, params, self.tiles.data_ptr(), stream)
         self.dist.gather(self.tiles, [self.gathered[r] for r in range(L.nranks)] if self.rank == 0 else None, dst=0)

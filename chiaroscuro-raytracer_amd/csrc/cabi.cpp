@@ -3,10 +3,7 @@
 // Owns the device copies of the scene (re-laid out for the kernels, see
 // kernels.hip header), the progressive accumulator, the counters and the
 // per-launch HIP events.  No C++ exception or hipError_t crosses the ABI.
-#include "chiaro_hip.h"
-#include "kernels.hpp"
-
-#include <hip/hip_runtime.h>
+#include "ctx.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -15,63 +12,7 @@
 #include <string>
 #include <vector>
 
-struct cr_ctx {
-    int device = -1;
-    int num_cus = 0;
-    std::string err;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    cr::WfStreams wfs{nullptr, nullptr, nullptr}; // wavefront side stream + fork / join events
-    float last_ms = 0.f;
-    // scene
-    bool has_scene = false;
-    cr::DevScene S{};
-    uint32_t stack_depth = 1;
-    std::vector<void *> scene_bufs;
-    // work buffers
-    unsigned long long *d_counters = nullptr;
-    uint32_t *d_work = nullptr;
-    float *d_accum = nullptr;
-    size_t accum_elems = 0;
-    void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
-    size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
-    cr_counters last{};
-    cr::TraceEvents tev;     // wavefront trace launches of the last render (cr_get_trace_stats)
-    cr_trace_stats last_trace{};
-    // options
-    // Defaults from sweeps on MI355X, sponza stand-in 1080p x 128 spp:
-    //   wavefront (kernel 2), trace variant 9, refill 64/56/48, sorted queues, tail below 1M rays
-    //   persistent megakernel (kernel 0), variant 0, refill 16:                615 Mray/s
-    int kernel = 2;
-    int full_counters = 1;
-    int variant = -1;       // -1: the kernel's default build
-    uint32_t block = 0;
-    uint32_t waves_per_cu = 0;
-    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 56 wavefront)
-    uint32_t refill_shadow = 0; // wavefront shadow trace; 0: refill if set, else 48
-    uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: refill if set, else 64
-    uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
-    int wf_sort = 1;                // wavefront: sort large shadow / secondary queues for coherence
-    uint32_t wf_sort_min = 1u << 20; // ... of at least this many rays
-    // sweep (1080p x 128 spp, refill 56): no sort 807; (8x8 px, 8x8 dirs) 891; (16x16, 16x16) 912;
-    // (16x16, 32x32 Morton) 930; (32x32, 32x32) 914 Mray/s
-    uint32_t wf_sort_tile = 4;      // key: log2 pixel sub-tile edge
-    // direction bins per octahedral axis: 32 -> 64 575.6 -> 570.2 ms per pass, rank 0 of 8 79.6 -> 78.0
-    // (world bits 5 / 7 and 16 bins measured slower; 7 bits x 64 bins: 31-bit keys, 607 ms)
-    uint32_t wf_dir_res = 64;       // key: direction bins per octahedral axis
-    int wf_world_keys = 2;          // key: world-space origins for queues starting at hits of gen >= 2
-    uint32_t wf_world_bits = 6;     // key: Morton bits per axis of the origin
-    // closest queues shorter than this finish in one wf_tail launch (0: never).  Sweep, sponza
-    // 1080p x 128 spp: 0 / 256K / 1M / 4M / 16M -> 594.7 / 591.6 / 590.2 / 592.9 / 626.5 ms;
-    // rank 0 of an 8-way split: 0 / 64K / 256K / 1M / 4M -> 88.8 / 85.9 / 83.3 / 83.1 / 84.2 ms
-    uint32_t wf_tail_min = 1u << 20;
-    // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a
-    // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
-    // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do
-    uint64_t sample_buf = cr::SAMPLE_BUF_BYTES;
-};
-
-namespace {
+namespace crx {
 
 int fail(cr_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -80,11 +21,7 @@ int fail(cr_ctx *c, int code, const std::string &msg) {
 int hip_fail(cr_ctx *c, hipError_t e, const char *what) {
     return fail(c, CR_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
-#define HIPCHK(call)                                                                                                 \
-    do {                                                                                                             \
-        hipError_t e_ = (call);                                                                                      \
-        if (e_ != hipSuccess) return hip_fail(c, e_, #call);                                                         \
-    } while (0)
+
 
 void free_scene(cr_ctx *c) {
     for (void *p : c->scene_bufs) hipFree(p);
@@ -326,7 +263,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     return CR_OK;
 }
 
-} // namespace
+} // namespace crx
+
+using namespace crx;
 
 extern "C" {
 
@@ -366,6 +305,7 @@ void cr_destroy(cr_ctx *c) {
     if (!c) return;
     if (c->device >= 0) {
         hipSetDevice(c->device);
+        release_dist(c);
         free_scene(c);
         if (c->d_accum) hipFree(c->d_accum);
         if (c->d_gstack) hipFree(c->d_gstack);

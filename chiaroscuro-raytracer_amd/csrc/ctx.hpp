@@ -1,0 +1,94 @@
+// ctx.hpp -- the state behind one cr_ctx (one GPU) and the render entry shared by
+// the single-GPU C-ABI (cabi.cpp) and the multi-GPU one (group.cpp).
+#pragma once
+#include "chiaro_hip.h"
+#include "kernels.hpp"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+struct cr_ctx {
+    int device = -1;
+    int num_cus = 0;
+    std::string err;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    cr::WfStreams wfs{nullptr, nullptr, nullptr}; // wavefront side stream + fork / join events
+    float last_ms = 0.f;
+    // scene
+    bool has_scene = false;
+    cr::DevScene S{};
+    uint32_t stack_depth = 1;
+    std::vector<void *> scene_bufs;
+    // work buffers
+    unsigned long long *d_counters = nullptr;
+    uint32_t *d_work = nullptr;
+    float *d_accum = nullptr;
+    size_t accum_elems = 0;
+    void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
+    size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
+    cr_counters last{};
+    cr::TraceEvents tev;     // wavefront trace launches of the last render (cr_get_trace_stats)
+    cr_trace_stats last_trace{};
+    // options
+    // Defaults from sweeps on MI355X, sponza stand-in 1080p x 128 spp:
+    //   wavefront (kernel 2), trace variant 9, refill 64/56/48, sorted queues, tail below 1M rays
+    //   persistent megakernel (kernel 0), variant 0, refill 16:                615 Mray/s
+    int kernel = 2;
+    int full_counters = 1;
+    int variant = -1;       // -1: the kernel's default build
+    uint32_t block = 0;
+    uint32_t waves_per_cu = 0;
+    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 56 wavefront)
+    uint32_t refill_shadow = 0; // wavefront shadow trace; 0: refill if set, else 48
+    uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: refill if set, else 64
+    uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
+    int wf_sort = 1;                // wavefront: sort large shadow / secondary queues for coherence
+    uint32_t wf_sort_min = 1u << 20; // ... of at least this many rays
+    // sweep (1080p x 128 spp, refill 56): no sort 807; (8x8 px, 8x8 dirs) 891; (16x16, 16x16) 912;
+    // (16x16, 32x32 Morton) 930; (32x32, 32x32) 914 Mray/s
+    uint32_t wf_sort_tile = 4;      // key: log2 pixel sub-tile edge
+    // direction bins per octahedral axis: 32 -> 64 575.6 -> 570.2 ms per pass, rank 0 of 8 79.6 -> 78.0
+    // (world bits 5 / 7 and 16 bins measured slower; 7 bits x 64 bins: 31-bit keys, 607 ms)
+    uint32_t wf_dir_res = 64;       // key: direction bins per octahedral axis
+    int wf_world_keys = 2;          // key: world-space origins for queues starting at hits of gen >= 2
+    uint32_t wf_world_bits = 6;     // key: Morton bits per axis of the origin
+    // closest queues shorter than this finish in one wf_tail launch (0: never).  Sweep, sponza
+    // 1080p x 128 spp: 0 / 256K / 1M / 4M / 16M -> 594.7 / 591.6 / 590.2 / 592.9 / 626.5 ms;
+    // rank 0 of an 8-way split: 0 / 64K / 256K / 1M / 4M -> 88.8 / 85.9 / 83.3 / 83.1 / 84.2 ms
+    uint32_t wf_tail_min = 1u << 20;
+    // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a
+    // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
+    // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do
+    uint64_t sample_buf = cr::SAMPLE_BUF_BYTES;
+    // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
+    // communicator per process, this rank's compact tile buffer, the root's gather area
+    ncclComm_t comm = nullptr;
+    int comm_rank = 0, comm_nranks = 1;
+    float *d_tiles = nullptr, *d_gathered = nullptr;
+    size_t tiles_bytes = 0, gathered_bytes = 0;
+};
+
+
+#define HIPCHK(call)                                                                                                 \
+    do {                                                                                                             \
+        hipError_t e_ = (call);                                                                                      \
+        if (e_ != hipSuccess) return crx::hip_fail(c, e_, #call);                                                    \
+    } while (0)
+
+namespace crx {
+int fail(cr_ctx *c, int code, const std::string &msg);
+int hip_fail(cr_ctx *c, hipError_t e, const char *what);
+int check_params(cr_ctx *c, const cr_render_params *p);
+uint32_t tile_of(const cr_render_params *p);
+int grow(cr_ctx *c, void **buf, size_t &cap, size_t need);
+// one render pass of p's tiles (MODE_TILES: compact [tiles][T][T][3] batch means
+// into out) or of the whole frame blended into out (MODE_BLEND), on stream st;
+// returns after the pass, counters and trace stats are read back
+int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st);
+// group.cpp: the communicator and buffers of the multi-process split (cr_destroy)
+void release_dist(cr_ctx *c);
+} // namespace crx

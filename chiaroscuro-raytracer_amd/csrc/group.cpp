@@ -1,0 +1,409 @@
+// group.cpp -- the multi-GPU frame split at the C-ABI, RCCL inside.
+//
+// The frame is cut into tile x tile tiles, tile t belongs to rank t % nranks;
+// every rank renders the batch means of its tiles into a compact buffer
+// [tiles][T][T][3], the root gathers the buffers over RCCL (xGMI between the
+// GPUs of a node) and unpermutes + blends the layer into its frame on the
+// device: frame = (frame * (L - 1) + mean) / L (src/rayTracer.cpp:64).  The
+// RNG key holds the global pixel index, so the image does not depend on the
+// number of ranks (tests/test_gpu_parity.py tile tests, tests/test_gpu_group.py).
+//
+// Two shapes of the same protocol:
+//   cr_comm_* / cr_render_dist_device  one process per GPU (the MI355X layout:
+//       bench.py under torch.distributed.run); a ncclComm per process from a
+//       unique id the caller distributes; grouped ncclSend / ncclRecv to rank 0
+//   cr_group_*  one host process driving N GPUs (the reference's callers --
+//       main.cpp:16, src/openglPreview.cpp:247 -- are single-process): a
+//       cr_ctx per GPU, the passes on one host thread per GPU (a pass waits on
+//       its queue lengths), ncclCommInitAll and the grouped send / receive from
+//       one thread.  A device listed twice cannot join a RCCL communicator; such
+//       a group gathers with device-to-device copies instead (the one-GPU tests
+//       of the N-rank protocol use that).
+// After every gather the host polls ncclCommGetAsyncError while it waits, so a
+// failed peer surfaces as CR_E_COMM instead of a hang.
+#include "ctx.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+namespace crx {
+
+static int nccl_fail(cr_ctx *c, ncclResult_t r, const char *what) {
+    return fail(c, CR_E_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+void release_dist(cr_ctx *c) {
+    if (c->comm) ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    c->comm_rank = 0;
+    c->comm_nranks = 1;
+    if (c->d_tiles) hipFree(c->d_tiles);
+    if (c->d_gathered) hipFree(c->d_gathered);
+    c->d_tiles = c->d_gathered = nullptr;
+    c->tiles_bytes = c->gathered_bytes = 0;
+}
+
+// Wait for the stream's work while watching the communicator's asynchronous error.
+static int wait_comm(cr_ctx *c, ncclComm_t comm, hipStream_t st, const char *what) {
+    for (;;) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return hip_fail(c, q, what);
+        ncclResult_t ae = ncclSuccess;
+        if (comm && ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+            ncclCommAbort(comm);
+            if (c->comm == comm) c->comm = nullptr;
+            return nccl_fail(c, ae, what);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    ncclResult_t ae = ncclSuccess;
+    if (comm && ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess) return nccl_fail(c, ae, what);
+    return CR_OK;
+}
+
+// Elements of one rank's compact tile buffer (the root's largest: rank 0 owns
+// the most tiles), so every rank sends and the root receives the same count.
+static size_t slot_elems(const cr_render_params *p) {
+    const size_t T = tile_of(p);
+    return (size_t)cr_tiles_for_rank(p, 0) * T * T * 3;
+}
+
+static cr::BlendArgs blend_args(const cr_render_params *p, const float *gathered, float *frame) {
+    cr::BlendArgs B{};
+    B.gathered = gathered;
+    B.frame = frame;
+    B.xres = p->xres;
+    B.yres = p->yres;
+    B.tile = tile_of(p);
+    B.tiles_x = (p->xres + B.tile - 1) / B.tile;
+    B.nranks = p->nranks;
+    B.max_tiles = cr_tiles_for_rank(p, 0);
+    B.layer = p->layer;
+    return B;
+}
+
+} // namespace crx
+
+using namespace crx;
+
+// ------------------------------------------------------ one process per GPU --
+extern "C" {
+
+int cr_comm_unique_id(uint8_t *out, size_t n) {
+    if (!out || n < CR_COMM_ID_BYTES || sizeof(ncclUniqueId) > CR_COMM_ID_BYTES) return CR_E_INVALID;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return CR_E_COMM;
+    std::memset(out, 0, CR_COMM_ID_BYTES);
+    std::memcpy(out, &id, sizeof(id));
+    return CR_OK;
+}
+
+int cr_comm_init(cr_ctx *c, int nranks, int rank, const uint8_t *id) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (nranks < 1 || rank < 0 || rank >= nranks || !id) return fail(c, CR_E_INVALID, "bad nranks/rank/id");
+    HIPCHK(hipSetDevice(c->device));
+    release_dist(c);
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, nranks, uid, rank);
+    if (r != ncclSuccess) return nccl_fail(c, r, "ncclCommInitRank");
+    c->comm = comm;
+    c->comm_rank = rank;
+    c->comm_nranks = nranks;
+    return CR_OK;
+}
+
+int cr_comm_destroy(cr_ctx *c) {
+    if (!c) return CR_E_INVALID;
+    if (c->device >= 0) {
+        HIPCHK(hipSetDevice(c->device));
+        release_dist(c);
+    }
+    return CR_OK;
+}
+
+int cr_render_dist_device(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *d_frame, void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!p || !cam) return fail(c, CR_E_INVALID, "null camera/params");
+    if (!c->comm) return fail(c, CR_E_INVALID, "no communicator (cr_comm_init)");
+    cr_render_params q = *p;
+    q.rank = (uint32_t)c->comm_rank;
+    q.nranks = (uint32_t)c->comm_nranks;
+    const bool root = c->comm_rank == 0;
+    if (root && !d_frame) return fail(c, CR_E_INVALID, "root needs a frame");
+    if (int rc = check_params(c, &q)) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (q.nranks == 1) return run_render(c, cam, &q, d_frame, cr::MODE_BLEND, st);
+    const size_t slot = slot_elems(&q);
+    float *mine;
+    if (root) {
+        if (int r = grow(c, (void **)&c->d_gathered, c->gathered_bytes, slot * q.nranks * sizeof(float))) return r;
+        mine = c->d_gathered; // the root's own tiles land in slot 0
+    } else {
+        if (int r = grow(c, (void **)&c->d_tiles, c->tiles_bytes, slot * sizeof(float))) return r;
+        mine = c->d_tiles;
+    }
+    if (int rc = run_render(c, cam, &q, mine, cr::MODE_TILES, st)) return rc;
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) {
+        if (root) {
+            for (uint32_t k = 1; k < q.nranks && r == ncclSuccess; k++)
+                r = ncclRecv(c->d_gathered + k * slot, slot, ncclFloat32, (int)k, c->comm, st);
+        } else {
+            r = ncclSend(mine, slot, ncclFloat32, 0, c->comm, st);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r == ncclSuccess) r = e;
+    }
+    if (r != ncclSuccess) return nccl_fail(c, r, "tile gather");
+    if (root) {
+        const int e = cr::launch_blend(blend_args(&q, c->d_gathered, d_frame), st);
+        if (e) return hip_fail(c, (hipError_t)e, "blend kernel launch");
+    }
+    return wait_comm(c, c->comm, st, "tile gather");
+}
+
+} // extern "C"
+
+// ---------------------------------------------------- one process, N GPUs --
+struct cr_group {
+    std::vector<int> devices;
+    std::vector<cr_ctx *> ctx;
+    std::vector<ncclComm_t> comm; // empty: gather by device copies (a device listed twice)
+    std::vector<float *> tiles;   // rank r >= 1: compact buffer on device r
+    std::vector<size_t> tiles_bytes;
+    float *gathered = nullptr;    // root device: [nranks][slot]
+    size_t gathered_bytes = 0;
+    float *frame = nullptr;       // root device: the progressive accumulator [yres][xres][3]
+    size_t frame_elems = 0;
+    std::string err;
+    cr_counters last{};
+    std::vector<float> rank_ms;
+};
+
+namespace {
+int gfail(cr_group *g, int code, const std::string &msg) {
+    g->err = msg;
+    return code;
+}
+int gctx_fail(cr_group *g, size_t r, int code) {
+    return gfail(g, code, "rank " + std::to_string(r) + " (device " + std::to_string(g->devices[r]) + "): " +
+                              cr_last_error(g->ctx[r]));
+}
+// run f(r) for every rank on its own host thread; first failure wins
+template <class F> int for_ranks(cr_group *g, F f) {
+    const size_t n = g->ctx.size();
+    std::vector<int> rc(n, CR_OK);
+    std::vector<std::thread> th;
+    for (size_t r = 1; r < n; r++) th.emplace_back([&, r] { rc[r] = f(r); });
+    rc[0] = f(0);
+    for (auto &t : th) t.join();
+    for (size_t r = 0; r < n; r++)
+        if (rc[r]) return gctx_fail(g, r, rc[r]);
+    return CR_OK;
+}
+} // namespace
+
+extern "C" {
+
+int cr_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+cr_group *cr_group_create(int ngpus, const int *devices) {
+    cr_group *g = new cr_group();
+    if (ngpus < 1 || ngpus > 64) {
+        g->err = "ngpus must be in [1, 64]";
+        return g;
+    }
+    for (int r = 0; r < ngpus; r++) g->devices.push_back(devices ? devices[r] : r);
+    for (int r = 0; r < ngpus; r++) {
+        g->ctx.push_back(cr_create(g->devices[r]));
+        if (g->ctx.back()->device < 0) {
+            g->err = "rank " + std::to_string(r) + ": " + cr_last_error(g->ctx.back());
+            return g;
+        }
+    }
+    g->tiles.assign(ngpus, nullptr);
+    g->tiles_bytes.assign(ngpus, 0);
+    g->rank_ms.assign(ngpus, 0.f);
+    std::vector<int> sorted = g->devices;
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end()) {
+        g->comm.assign(ngpus, nullptr);
+        const ncclResult_t r = ncclCommInitAll(g->comm.data(), ngpus, g->devices.data());
+        if (r != ncclSuccess) {
+            g->comm.clear();
+            g->err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+        }
+    }
+    return g;
+}
+
+void cr_group_destroy(cr_group *g) {
+    if (!g) return;
+    for (ncclComm_t c : g->comm)
+        if (c) ncclCommDestroy(c);
+    for (size_t r = 0; r < g->ctx.size(); r++) {
+        if (g->ctx[r]->device >= 0) {
+            hipSetDevice(g->devices[r]);
+            if (g->tiles[r]) hipFree(g->tiles[r]);
+            if (r == 0) {
+                if (g->gathered) hipFree(g->gathered);
+                if (g->frame) hipFree(g->frame);
+            }
+        }
+        cr_destroy(g->ctx[r]);
+    }
+    delete g;
+}
+
+const char *cr_group_last_error(cr_group *g) { return g ? g->err.c_str() : "null group"; }
+
+int cr_group_size(cr_group *g) { return g ? (int)g->ctx.size() : 0; }
+
+// Usable: every ctx on a device, and a communicator unless a device repeats.
+static bool group_ok(cr_group *g) {
+    if (g->ctx.empty()) return false;
+    for (cr_ctx *c : g->ctx)
+        if (c->device < 0) return false;
+    std::vector<int> sorted = g->devices;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    return !distinct || !g->comm.empty();
+}
+
+int cr_group_upload_scene(cr_group *g, const cr_scene_desc *d) {
+    if (!g) return CR_E_INVALID;
+    if (!group_ok(g)) return CR_E_HIP;
+    return for_ranks(g, [&](size_t r) { return cr_upload_scene(g->ctx[r], d); });
+}
+
+int cr_group_set_option(cr_group *g, const char *key, int64_t value) {
+    if (!g || g->ctx.empty()) return CR_E_INVALID;
+    for (size_t r = 0; r < g->ctx.size(); r++)
+        if (int rc = cr_set_option(g->ctx[r], key, value)) return gctx_fail(g, r, rc);
+    return CR_OK;
+}
+
+int cr_group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out) {
+    if (!g) return CR_E_INVALID;
+    if (!group_ok(g)) return gfail(g, CR_E_HIP, g->err.empty() ? "group not initialised" : g->err);
+    if (!cam || !p || !accum_rgb_out) return gfail(g, CR_E_INVALID, "null camera/params/output");
+    const uint32_t n = (uint32_t)g->ctx.size();
+    cr_render_params q = *p;
+    q.rank = 0;
+    q.nranks = n;
+    if (int rc = check_params(g->ctx[0], &q)) return gctx_fail(g, 0, rc);
+    const size_t elems = (size_t)q.xres * q.yres * 3;
+    hipStream_t st0 = g->ctx[0]->stream;
+    if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
+    if (elems != g->frame_elems) {
+        if (g->frame) hipFree(g->frame);
+        g->frame = nullptr;
+        g->frame_elems = 0;
+        if (hipMalloc(&g->frame, elems * sizeof(float)) != hipSuccess) return gfail(g, CR_E_OOM, "frame");
+        g->frame_elems = elems;
+        if (hipMemset(g->frame, 0, elems * sizeof(float)) != hipSuccess) return gfail(g, CR_E_HIP, "frame");
+    }
+    if (n == 1) {
+        if (int rc = run_render(g->ctx[0], cam, &q, g->frame, cr::MODE_BLEND, st0)) return gctx_fail(g, 0, rc);
+    } else {
+        const size_t slot = slot_elems(&q);
+        if (int rc = grow(g->ctx[0], (void **)&g->gathered, g->gathered_bytes, slot * n * sizeof(float)))
+            return gctx_fail(g, 0, rc);
+        int rc = for_ranks(g, [&](size_t r) -> int {
+            cr_ctx *c = g->ctx[r];
+            if (hipSetDevice(g->devices[r]) != hipSuccess) return fail(c, CR_E_HIP, "hipSetDevice");
+            float *mine = g->gathered;
+            if (r > 0) {
+                if (int e = grow(c, (void **)&g->tiles[r], g->tiles_bytes[r], slot * sizeof(float))) return e;
+                mine = g->tiles[r];
+            }
+            cr_render_params qr = q;
+            qr.rank = (uint32_t)r;
+            return run_render(c, cam, &qr, mine, cr::MODE_TILES, c->stream);
+        });
+        if (rc) return rc;
+        if (g->comm.empty()) { // a device listed twice: device-to-device copies into the root's slots
+            for (uint32_t r = 1; r < n; r++)
+                if (hipMemcpyPeerAsync(g->gathered + r * slot, g->devices[0], g->tiles[r], g->devices[r],
+                                       slot * sizeof(float), st0) != hipSuccess)
+                    return gfail(g, CR_E_HIP, "tile copy");
+        } else {
+            ncclResult_t r = ncclGroupStart();
+            for (uint32_t k = 1; k < n && r == ncclSuccess; k++) {
+                r = ncclSend(g->tiles[k], slot, ncclFloat32, 0, g->comm[k], g->ctx[k]->stream);
+                if (r == ncclSuccess)
+                    r = ncclRecv(g->gathered + k * slot, slot, ncclFloat32, (int)k, g->comm[0], st0);
+            }
+            const ncclResult_t e = ncclGroupEnd();
+            if (r == ncclSuccess) r = e;
+            if (r != ncclSuccess) return gfail(g, CR_E_COMM, std::string("tile gather: ") + ncclGetErrorString(r));
+        }
+        if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
+        const int e = cr::launch_blend(blend_args(&q, g->gathered, g->frame), st0);
+        if (e) return gfail(g, CR_E_HIP, std::string("blend kernel launch: ") + hipGetErrorString((hipError_t)e));
+        for (uint32_t k = 0; k < n; k++) {
+            hipSetDevice(g->devices[k]);
+            if (int w = wait_comm(g->ctx[k], g->comm.empty() ? nullptr : g->comm[k], g->ctx[k]->stream,
+                                  "tile gather"))
+                return gctx_fail(g, k, w);
+        }
+        hipSetDevice(g->devices[0]);
+    }
+    if (hipMemcpy(accum_rgb_out, g->frame, elems * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+        return gfail(g, CR_E_HIP, "frame copy");
+    // counters summed over ranks; each rank's pass time
+    cr_counters sum{};
+    uint64_t *s = (uint64_t *)&sum;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint64_t *v = (const uint64_t *)&g->ctx[k]->last;
+        for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) s[i] += v[i];
+        g->rank_ms[k] = g->ctx[k]->last_ms;
+    }
+    g->last = sum;
+    return CR_OK;
+}
+
+cr_ctx *cr_group_ctx(cr_group *g, int rank) {
+    return g && rank >= 0 && rank < (int)g->ctx.size() ? g->ctx[rank] : nullptr;
+}
+
+int cr_group_tonemap(cr_group *g, const cr_tonemap_params *t, uint32_t xres, uint32_t yres, uint8_t *bytes_out) {
+    if (!g || !t || !bytes_out) return CR_E_INVALID;
+    const size_t n = (size_t)3 * xres * yres;
+    if (!g->frame || g->frame_elems != n) return gfail(g, CR_E_INVALID, "no rendered frame of this size");
+    if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
+    void *d_bytes = nullptr;
+    if (hipMalloc(&d_bytes, n ? n : 1) != hipSuccess) return gfail(g, CR_E_OOM, "tonemap buffer");
+    cr_ctx *c = g->ctx[0];
+    int rc = cr_tonemap_device(c, t, xres, yres, g->frame, (uint8_t *)d_bytes, c->stream);
+    if (rc == CR_OK && (hipMemcpyAsync(bytes_out, d_bytes, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                        hipStreamSynchronize(c->stream) != hipSuccess))
+        rc = fail(c, CR_E_HIP, "tonemap copy");
+    hipFree(d_bytes);
+    return rc ? gctx_fail(g, 0, rc) : CR_OK;
+}
+
+int cr_group_get_counters(cr_group *g, cr_counters *out) {
+    if (!g || !out) return CR_E_INVALID;
+    *out = g->last;
+    return CR_OK;
+}
+
+int cr_group_rank_ms(cr_group *g, float *out) {
+    if (!g || !out) return CR_E_INVALID;
+    std::copy(g->rank_ms.begin(), g->rank_ms.end(), out);
+    return CR_OK;
+}
+
+} // extern "C"

@@ -85,6 +85,7 @@ int chiaro_scene_info_get(const chiaro_scene *s, chiaro_scene_info *o) {
     o->n_invalid = (uint32_t)S.errors.size();
     cpy(o->obj_path, S.objPath, sizeof o->obj_path);
     cpy(o->render_path, S.renderPath, sizeof o->render_path);
+    o->gpus = S.gpus;
     return CR_OK;
 }
 

@@ -63,20 +63,40 @@ cr_camera make_camera(vec3 eye, vec3 center, vec3 up, float yview, unsigned xres
 RayTracer::RayTracer(Model &_model, Scene &_scene, int device)
     : scene(_scene), pixels((size_t)_scene.yres * _scene.xres * 3, 0.f), data((size_t)_scene.yres * _scene.xres * 3),
       kdtree(_model, _scene) {
-    ctx_ = cr_create(device);
     cr_scene_desc d;
     kdtree.describe(scene, d);
-    const int rc = cr_upload_scene(ctx_, &d);
-    if (rc != CR_OK) {
-        std::string msg = std::string("chiaro: scene upload failed: ") + cr_last_error(ctx_);
-        cr_destroy(ctx_);
-        ctx_ = nullptr;
-        throw std::runtime_error(msg);
+    if (scene.gpus > 1) {
+        // GPUs device, device + 1, ...; with fewer GPUs than asked for the ranks wrap
+        // around (a device then serves several ranks: same image, no speed-up)
+        const int ndev = cr_device_count();
+        if (ndev > 0 && (int)scene.gpus > ndev)
+            std::cerr << "chiaro: gpus " << scene.gpus << " but " << ndev << " GPU(s) visible; ranks share GPUs\n";
+        std::vector<int> devs;
+        for (unsigned r = 0; r < scene.gpus; r++) devs.push_back(ndev > 0 ? (device + (int)r) % ndev : device);
+        group_ = cr_group_create((int)scene.gpus, devs.data());
+        if (cr_group_upload_scene(group_, &d) != CR_OK) {
+            std::string msg = std::string("chiaro: scene upload failed: ") + cr_group_last_error(group_);
+            cr_group_destroy(group_);
+            group_ = nullptr;
+            throw std::runtime_error(msg);
+        }
+        ctx_ = cr_group_ctx(group_, 0);
+    } else {
+        ctx_ = cr_create(device);
+        if (cr_upload_scene(ctx_, &d) != CR_OK) {
+            std::string msg = std::string("chiaro: scene upload failed: ") + cr_last_error(ctx_);
+            cr_destroy(ctx_);
+            ctx_ = nullptr;
+            throw std::runtime_error(msg);
+        }
     }
     kdtree.attach(ctx_);
 }
 
-RayTracer::~RayTracer() { cr_destroy(ctx_); }
+RayTracer::~RayTracer() {
+    if (group_) cr_group_destroy(group_); // owns ctx_
+    else cr_destroy(ctx_);
+}
 
 void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) {
     // rayTracer.cpp:24 -- including the reference's `(lastUp == lastUp)`: a
@@ -110,9 +130,15 @@ void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) {
     p.rank = 0;
     p.nranks = 1;
     p.tile = 32;
-    const int rc = cr_render(ctx_, &cam, &p, pixels.data());
-    if (rc != CR_OK) throw std::runtime_error(std::string("chiaro: render failed: ") + cr_last_error(ctx_));
-    cr_get_counters(ctx_, &counters_);
+    if (group_) {
+        if (cr_group_render(group_, &cam, &p, pixels.data()) != CR_OK)
+            throw std::runtime_error(std::string("chiaro: render failed: ") + cr_group_last_error(group_));
+        cr_group_get_counters(group_, &counters_);
+    } else {
+        if (cr_render(ctx_, &cam, &p, pixels.data()) != CR_OK)
+            throw std::runtime_error(std::string("chiaro: render failed: ") + cr_last_error(ctx_));
+        cr_get_counters(ctx_, &counters_);
+    }
     // rayTracer.cpp:51,66-68 (computed after the render instead of racily inside it)
     maxVal = 0.f;
     for (float v : pixels) maxVal = maxVal > v ? maxVal : v;
@@ -131,8 +157,12 @@ void RayTracer::normalizeImage(float exposure, float defog, float kneeLow, float
     if (exposure == FLT_MAX) exposure = scene.exposure;
     cr_tonemap_params t;
     cr_tonemap_setup(exposure, defog, kneeLow, kneeHigh, gamma, &t);
-    if (cr_tonemap(ctx_, &t, scene.xres, scene.yres, data.data()) != CR_OK)
+    if (group_) {
+        if (cr_group_tonemap(group_, &t, scene.xres, scene.yres, data.data()) != CR_OK)
+            throw std::runtime_error(std::string("chiaro: tonemap failed: ") + cr_group_last_error(group_));
+    } else if (cr_tonemap(ctx_, &t, scene.xres, scene.yres, data.data()) != CR_OK) {
         throw std::runtime_error(std::string("chiaro: tonemap failed: ") + cr_last_error(ctx_));
+    }
 }
 
 namespace {

@@ -22,8 +22,9 @@ cr_camera make_camera(vec3 eye, vec3 center, vec3 up, float yview, unsigned xres
 
 class RayTracer {
   public:
-    // device: HIP device index.  Throws std::runtime_error when no GPU / the HIP
-    // library cannot be used (the product never falls back to the CPU).
+    // device: HIP device index (scene.gpus > 1: GPUs device .. device + gpus - 1, the
+    // layers tile-split over them, cr_group_*).  Throws std::runtime_error when no
+    // GPU / the HIP library cannot be used (the product never falls back to the CPU).
     RayTracer(Model &_model, Scene &_scene, int device = 0);
     ~RayTracer();
     RayTracer(const RayTracer &) = delete;
@@ -44,7 +45,8 @@ class RayTracer {
     // --- additions of this build (not in the reference API) ---
     const float *pixelData() const { return pixels.data(); } // [yres][xres][3], row 0 = top
     unsigned layers() const { return layers_; }
-    cr_ctx *context() { return ctx_; }
+    cr_ctx *context() { return ctx_; }          // with gpus > 1: the root GPU's ctx
+    cr_group *group() { return group_; }        // gpus > 1, else null
     KDTree &tree() { return kdtree; }
     const cr_counters &lastCounters() const { return counters_; }
     double lastSeconds() const { return lastSeconds_; }
@@ -55,6 +57,7 @@ class RayTracer {
     std::vector<uint8_t> data;
     KDTree kdtree;
     cr_ctx *ctx_ = nullptr;
+    cr_group *group_ = nullptr;
     cr_counters counters_{};
     double lastSeconds_ = 0.0;
     // rayTracer.cpp:18-22 progressive-layer state (per instance here, not function-static)

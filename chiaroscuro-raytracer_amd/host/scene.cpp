@@ -10,7 +10,7 @@ namespace chiaro {
 Scene::Scene(const std::string &filename)
     : renderPath("renders/output.exr"), k(3), xres(400), yres(300), VP(0, 0, 2), LA(0, 0, 0), UP(0, 1, 0), yview(1),
       usingOpenGLPreview(true), previewHeight(900), kdtreeLeafSize(8), background(0), samples(100), exposure(5),
-      seed(0xC41A05C0u), rtcPath(filename) {
+      seed(0xC41A05C0u), gpus(1), rtcPath(filename) {
     std::ifstream file(filename);
     std::string input;
     while (std::getline(file, input)) {
@@ -60,6 +60,8 @@ Scene::Scene(int argc, char **argv) : Scene(std::string(argc > 1 ? argv[1] : "co
             kdtreeLeafSize = std::stoi(next(i));
         else if (p == "seed")
             seed = (uint32_t)std::stoul(next(i), nullptr, 0);
+        else if (p == "gpus")
+            gpus = (unsigned)std::stoul(next(i));
         else {
             std::cerr << "Invalid argument \"" << p << "\"\n";
             errors.push_back(p);

@@ -45,8 +45,10 @@ class Scene {
     std::vector<LightTriangle> lightTriangles; // filled by KDTree
     std::vector<std::string> params;
     float exposure;
-    // additive keys of this build (not in the reference): "seed", "background"
+    // additive keys of this build (not in the reference): "seed", "background",
+    // "gpus" (the RayTracer tile-splits each layer over GPUs 0..gpus-1, cr_group_*)
     uint32_t seed;
+    unsigned gpus;
     std::string rtcPath;   // argv[1] as given
     std::vector<std::string> errors; // "Invalid argument" lines also printed to stderr
 

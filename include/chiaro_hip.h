@@ -27,6 +27,13 @@
  *                        OpenMP row loop, src/rayTracer.cpp:55).
  *   cr_tonemap_setup / cr_tonemap / cr_tonemap_device
  *                        RayTracer::normalizeImage (src/rayTracer.cpp:172-222)
+ *   cr_group_*           RayTracer::rayTrace (src/rayTracer.cpp:17-74) with the frame
+ *                        tile-split over N GPUs of one process and gathered over
+ *                        RCCL (the reference's single-process callers main.cpp:16,
+ *                        src/openglPreview.cpp:247 through the host RayTracer).
+ *   cr_comm_* / cr_render_dist_device
+ *                        the same split with one process per GPU (RCCL
+ *                        communicator from a unique id the caller distributes).
  *   cr_intersect         KDTree::intersectRay       (src/kdtree.cpp:210-216)
  *   cr_intersect_shadow  KDTree::intersectShadowRay (src/kdtree.cpp:283-290)
  *
@@ -48,6 +55,7 @@ extern "C" {
 #define CR_E_NOSCENE (-3)  /* render before cr_upload_scene        */
 #define CR_E_DEPTH (-4)    /* kd-tree deeper than the kernels support */
 #define CR_E_OOM (-5)      /* device allocation failed             */
+#define CR_E_COMM (-6)     /* RCCL error (init, gather, a failed peer) */
 
 typedef struct cr_ctx cr_ctx;
 
@@ -230,6 +238,51 @@ int cr_get_trace_stats(cr_ctx *ctx, cr_trace_stats *out);
  * "block", "waves_per_cu".  Returns CR_OK or CR_E_INVALID. */
 int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
 int cr_synchronize(cr_ctx *ctx);
+
+/* ---------------------------------------------------------- multi-GPU --
+ * The frame split of SURVEY §8e behind the C-ABI, RCCL inside (csrc/group.cpp):
+ * tile t of the frame belongs to rank t % nranks; each rank renders its tiles'
+ * batch means, the root (rank 0) gathers them over RCCL (xGMI) and blends the
+ * layer into its frame ((old*(L-1) + mean)/L, src/rayTracer.cpp:64) on the
+ * device.  The image equals the single-GPU render bit for bit. */
+
+/* One process per GPU.  Rank 0 makes the id (cr_comm_unique_id), the caller
+ * hands it to every rank (any channel), each rank calls cr_comm_init on its ctx
+ * (collective: returns once all nranks have joined). */
+#define CR_COMM_ID_BYTES 128
+int cr_comm_unique_id(uint8_t *id_out, size_t id_bytes);
+int cr_comm_init(cr_ctx *ctx, int nranks, int rank, const uint8_t *id);
+int cr_comm_destroy(cr_ctx *ctx);
+/* Collective over the communicator: this rank's tiles of layer p->layer (p->rank /
+ * p->nranks are taken from the communicator), gathered to rank 0 and blended into
+ * d_frame [yres][xres][3] there (other ranks: d_frame unused, may be NULL).
+ * Returns when the layer is complete on this rank's stream. */
+int cr_render_dist_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *d_frame,
+                          void *stream);
+
+/* One process driving N GPUs: a ctx per device (devices NULL -> 0..ngpus-1), the
+ * passes on one host thread per GPU, grouped RCCL send / receive to rank 0.  A
+ * device listed twice cannot join a RCCL communicator: such a group gathers with
+ * device-to-device copies (same protocol, for one-GPU tests).  Errors of create
+ * show on the first call / cr_group_last_error. */
+typedef struct cr_group cr_group;
+int cr_device_count(void); /* HIP devices visible to this process (0 without a GPU) */
+cr_group *cr_group_create(int ngpus, const int *devices);
+void cr_group_destroy(cr_group *g);
+const char *cr_group_last_error(cr_group *g);
+int cr_group_size(cr_group *g);
+int cr_group_upload_scene(cr_group *g, const cr_scene_desc *desc);
+int cr_group_set_option(cr_group *g, const char *key, int64_t value); /* on every rank's ctx */
+/* cr_render across the group: layer p->layer of the whole frame (p->rank / p->nranks
+ * ignored, p->tile used), blended into the root's accumulator, copied to
+ * accum_rgb_out [yres][xres][3] (host). */
+int cr_group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out);
+int cr_group_get_counters(cr_group *g, cr_counters *out); /* summed over the ranks */
+int cr_group_rank_ms(cr_group *g, float *ms_out);          /* [ngpus] each rank's last pass (HIP events) */
+/* rank's ctx (rank 0: the root, which also answers cr_intersect*), NULL if out of range */
+cr_ctx *cr_group_ctx(cr_group *g, int rank);
+/* cr_tonemap on the root's accumulator (the frame of the last cr_group_render) */
+int cr_group_tonemap(cr_group *g, const cr_tonemap_params *t, uint32_t xres, uint32_t yres, uint8_t *bytes_out);
 
 #ifdef __cplusplus
 }

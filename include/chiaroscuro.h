@@ -38,6 +38,7 @@ typedef struct {
     uint32_t n_invalid; /* tokens reported as "Invalid argument" */
     char obj_path[1024];
     char render_path[1024];
+    uint32_t gpus;      /* additive "gpus" key: GPUs the RayTracer splits a layer over */
 } chiaro_scene_info;
 
 const char *chiaro_last_error(void);

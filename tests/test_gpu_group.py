@@ -1,0 +1,111 @@
+"""The multi-GPU C-ABI (csrc/group.cpp) on one MI355X.
+
+cr_group: a one-GPU group runs RCCL's communicator of one rank; a group that
+lists the same device several times runs the whole N-rank protocol (per-rank
+passes on their own host threads, compact tile buffers, gather into the root's
+slots, unpermute + progressive blend) with device copies in place of the RCCL
+send / receive.  cr_comm / cr_render_dist_device: a one-rank RCCL communicator.
+All bit-exact with the oracle's single-process render, counters summed over
+the ranks equal to the oracle's."""
+import numpy as np
+import pytest
+
+from helpers import Pair, assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths")
+SEED = 0xC41A05C0
+
+
+@pytest.fixture(scope="module")
+def sponza(ca, po, scenes):
+    return Pair(ca, po, scenes.config_rtc("sponza"), device=False)
+
+
+@pytest.mark.parametrize("devices,size", [([0], (96, 54, 3)), ([0, 0, 0, 0], (310, 180, 2)),
+                                          ([0, 0, 0, 0, 0, 0, 0, 0], (200, 120, 2))])
+def test_group_render_layers_bitexact(ca, sponza, devices, size):
+    x, y, s = size
+    g = ca.Group(devices)
+    g.upload(sponza.kd.describe())
+    g.set_option("wf_tail_min", 0)
+    cam = sponza.camera(ca, x, y)
+    o = None
+    for layer in (1, 2):
+        p = ca.render_params(x, y, s, 6, SEED, layer=layer)
+        img = g.render(cam, p)
+        gc = g.counters()
+        o, oc = sponza.oracle.render(cam.as_array(), x, y, s, 6, SEED, layer=layer, pixels=o)
+        assert_bitwise(img, o, "group %s layer %d" % (devices, layer))
+        assert {k: gc[k] for k in KEYS} == oc
+        assert gc["pixels"] == x * y
+    ms = g.rank_ms()
+    assert len(ms) == len(devices) and all(t > 0 for t in ms)
+    g.close()
+
+
+def test_group_tonemap_equals_single_ctx(ca, sponza):
+    """cr_group_tonemap on the root's accumulator == cr_tonemap of a single-GPU render."""
+    import ctypes
+    x, y = 64, 40
+    cam = sponza.camera(ca, x, y)
+    p = ca.render_params(x, y, 2, 6, SEED)
+    g = ca.Group([0, 0])
+    g.upload(sponza.kd.describe())
+    g.render(cam, p)
+    d = ca.Device(0)
+    d.upload(sponza.kd.describe())
+    d.render(cam, p)
+    t = ca.tonemap_params(2.0)
+    a = np.zeros((y, x, 3), np.uint8)
+    b = np.zeros((y, x, 3), np.uint8)
+    hip, _ = ca.libs()
+    assert hip.cr_group_tonemap(g._g, ctypes.byref(t), x, y, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))) == 0
+    assert hip.cr_tonemap(d._c, ctypes.byref(t), x, y, b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))) == 0
+    assert np.array_equal(a, b) and a.any()
+    g.close()
+    d.close()
+
+
+def test_comm_one_rank_render_dist(ca, sponza):
+    """cr_comm_init (ncclCommInitRank, one rank) + cr_render_dist_device over two layers."""
+    import torch
+    x, y, s = 96, 54, 2
+    d = ca.Device(0)
+    d.upload(sponza.kd.describe())
+    d.comm_init(1, 0, ca.Device.comm_unique_id())
+    cam = sponza.camera(ca, x, y)
+    frame = torch.zeros((y, x, 3), dtype=torch.float32, device="cuda")
+    o = None
+    for layer in (1, 2):
+        p = ca.render_params(x, y, s, 6, SEED, layer=layer)
+        d.render_dist_device(cam, p, frame.data_ptr())
+        torch.cuda.synchronize()
+        o, _ = sponza.oracle.render(cam.as_array(), x, y, s, 6, SEED, layer=layer, pixels=o)
+        assert_bitwise(frame.cpu().numpy(), o, "cr_render_dist_device layer %d" % layer)
+    d.comm_destroy()
+    with pytest.raises(RuntimeError):
+        d.render_dist_device(cam, ca.render_params(x, y, s, 6, SEED), frame.data_ptr())
+    d.close()
+
+
+def test_raytracer_gpus_key(ca, scenes):
+    """The additive .rtc key `gpus`: a RayTracer whose layers are split over a
+    group (3 ranks, wrapping onto the one GPU of the test box) renders the same
+    progressive layers as the plain one, and normalizeImage gives the same bytes."""
+    rtc = scenes.config_rtc("cornell")
+    out, data = [], []
+    for gpus in ("1", "3"):
+        sc = ca.Scene(rtc, "xres", "40", "yres", "30", "samples", "2", "gpus", gpus)
+        assert sc.info["gpus"] == int(gpus) and sc.info["n_invalid"] == 0
+        rt = ca.RayTracer(ca.Model(sc), sc)
+        i = sc.info
+        rt.rayTrace(i["VP"], i["LA"], i["UP"], i["yview"])
+        rt.rayTrace(i["VP"], i["LA"], i["UP"], i["yview"])
+        assert rt.layers == 2
+        out.append(rt.pixels)
+        rt.normalizeImage(2.0)
+        data.append(rt.getData())
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32)) and out[0].any()
+    assert np.array_equal(data[0], data[1])
