@@ -59,14 +59,11 @@ def main():
     cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], xres, yres)
     stream = torch.cuda.current_stream().cuda_stream
     fr = DistributedFrame(dev, xres, yres, rank, world, 32, dist, gather=args.gather)
-    rng = np.random.default_rng(7)
-    probe = (rng.integers(0, yres, 4096), rng.integers(0, xres, 4096))
-    layers, rays, prev = [], 0, None
+    layers, rays = [], 0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ok_identity = True
     for L in range(1, args.layers + 1):
         p = ca.render_params(xres, yres, spp, k, seed, layer=L, rank=rank, nranks=world, tile=32)
         tl = time.perf_counter()
@@ -76,13 +73,6 @@ def main():
         rays += c["closest"] + c["shadow"]
         layers.append({"layer": L, "wall_ms": round((time.perf_counter() - tl) * 1e3, 2),
                        "render_ms": round(dev.last_kernel_ms(), 2)})
-        if rank == 0 and L <= 3:  # progressive identity on sampled pixels (host recompute of the blend)
-            cur = fr.frame[probe[0], probe[1]].cpu().numpy()
-            if prev is not None:
-                # mean_L is not kept; the identity is checked through L-1 -> L bounds:
-                # every blended value lies between the previous value * (L-1)/L and that + max/L
-                ok_identity &= bool(np.all(cur >= prev * np.float32((L - 1) / L) * (1 - 1e-6)))
-            prev = cur
         if rank == 0:
             print("layer %d: %s" % (L, layers[-1]), file=sys.stderr, flush=True)
     torch.cuda.synchronize()
@@ -102,7 +92,6 @@ def main():
         f = fr.frame.cpu().numpy()
         out["frame_finite_nonneg"] = bool(np.isfinite(f).all() and (f >= 0).all())
         out["frame_mean"] = float(f.mean())
-        out["progressive_bound_ok"] = ok_identity
         if args.check_ystep:
             import pyoracle as po
             osc = po.OracleScene(m.triangles(), leaf_size=i["leaf_size"], textures=m.textures(),
