@@ -124,7 +124,9 @@ HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_g
                 "chiaro_raytracer_create", "chiaro_raytracer_raytrace", "chiaro_raytracer_pixels",
                 "chiaro_raytracer_data", "chiaro_raytracer_maxval", "chiaro_raytracer_layers",
                 "chiaro_raytracer_counters", "chiaro_raytracer_normalize", "chiaro_raytracer_export",
-                "chiaro_raytracer_ctx", "chiaro_raytracer_destroy", "chiaro_camera")
+                "chiaro_raytracer_ctx", "chiaro_raytracer_destroy", "chiaro_camera",
+                "chiaro_preview_create", "chiaro_preview_key", "chiaro_preview_mouse", "chiaro_preview_scroll",
+                "chiaro_preview_texture", "chiaro_preview_state", "chiaro_preview_destroy")
 
 P = C.c_void_p
 FP = C.POINTER(C.c_float)
@@ -223,6 +225,13 @@ def libs():
     _sig(host, "chiaro_raytracer_ctx", P, [P])
     _sig(host, "chiaro_raytracer_destroy", None, [P])
     _sig(host, "chiaro_camera", C.c_int, [FP, FP, FP, C.c_float, C.c_uint32, C.c_uint32, C.POINTER(CrCamera)])
+    _sig(host, "chiaro_preview_create", P, [P, P])
+    _sig(host, "chiaro_preview_key", C.c_int, [P, C.c_int, C.c_float, C.c_int])
+    _sig(host, "chiaro_preview_mouse", C.c_int, [P, C.c_float, C.c_float])
+    _sig(host, "chiaro_preview_scroll", C.c_int, [P, C.c_float])
+    _sig(host, "chiaro_preview_texture", C.POINTER(C.c_uint8), [P, UP, UP])
+    _sig(host, "chiaro_preview_state", C.c_int, [P, FP, FP, FP, FP, C.POINTER(C.c_int), UP])
+    _sig(host, "chiaro_preview_destroy", None, [P])
     _hip, _host = hip, host
     return hip, host
 
@@ -591,6 +600,48 @@ class RayTracer:
         if getattr(self, "_h", None) and _host is not None:
             _host.chiaro_raytracer_destroy(self._h)
             self._h = None
+
+
+class Preview:
+    """The interactive preview's render path without a window (chiaro_preview_*,
+    src/openglPreview.cpp:12-257): keys R / TAB / = / - / W S A D E Q, mouse, scroll,
+    and the screen texture (getData after normalizeImage)."""
+    KEYS = {"R": 0, "TAB": 1, "=": 2, "-": 3, "W": 4, "S": 5, "A": 6, "D": 7, "E": 8, "Q": 9}
+
+    def __init__(self, scene: Scene, rt: RayTracer):
+        _, host = libs()
+        self._scene, self._rt = scene, rt
+        self._p = host.chiaro_preview_create(scene._h, rt._h)
+        if not self._p:
+            raise RuntimeError("Preview: " + _host_err())
+
+    def key(self, k: str, dt: float = 0.0, shift: bool = False):
+        if libs()[1].chiaro_preview_key(self._p, self.KEYS[k], float(dt), int(shift)):
+            raise RuntimeError("Preview.key: " + _host_err())
+
+    def mouse(self, dx: float, dy: float):
+        libs()[1].chiaro_preview_mouse(self._p, float(dx), float(dy))
+
+    def scroll(self, dy: float):
+        libs()[1].chiaro_preview_scroll(self._p, float(dy))
+
+    def texture(self) -> np.ndarray:
+        w, h = C.c_uint32(), C.c_uint32()
+        d = libs()[1].chiaro_preview_texture(self._p, C.byref(w), C.byref(h))
+        return np.ctypeslib.as_array(d, shape=(h.value, w.value, 3)).copy()
+
+    def state(self) -> dict:
+        pos, front, up = np.zeros(3, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+        zoom, show, n = C.c_float(), C.c_int(), C.c_uint32()
+        libs()[1].chiaro_preview_state(self._p, _ptr(pos), _ptr(front), _ptr(up), C.byref(zoom), C.byref(show),
+                                       C.byref(n))
+        return {"position": pos, "front": front, "up": up, "zoom": zoom.value, "show_render": bool(show.value),
+                "renders": n.value}
+
+    def __del__(self):
+        if getattr(self, "_p", None) and _host is not None:
+            _host.chiaro_preview_destroy(self._p)
+            self._p = None
 
 
 def algorithmic_bytes(c: dict, pixels_written: int, texel_bytes: int = 3) -> int:

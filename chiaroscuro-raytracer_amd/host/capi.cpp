@@ -3,6 +3,7 @@
 
 #include "kdtree.hpp"
 #include "model.hpp"
+#include "preview.hpp"
 #include "raytracer.hpp"
 #include "scene.hpp"
 
@@ -24,6 +25,9 @@ struct chiaro_kdtree {
 };
 struct chiaro_raytracer {
     std::unique_ptr<RayTracer> r;
+};
+struct chiaro_preview {
+    std::unique_ptr<PreviewSession> p;
 };
 
 namespace {
@@ -298,3 +302,73 @@ int chiaro_camera(const float eye[3], const float center[3], const float up[3], 
 }
 
 } // extern "C"
+
+chiaro_preview *chiaro_preview_create(chiaro_scene *s, chiaro_raytracer *r) {
+    if (!s || !r) return nullptr;
+    return guard(
+        [&]() -> chiaro_preview * {
+            auto *p = new chiaro_preview();
+            p->p.reset(new PreviewSession(*s->s, *r->r));
+            return p;
+        },
+        (chiaro_preview *)nullptr);
+}
+
+int chiaro_preview_key(chiaro_preview *p, int key, float dt, int shift) {
+    if (!p) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            PreviewSession &P = *p->p;
+            switch (key) {
+            case CHIARO_KEY_R: P.pressRender(); break;
+            case CHIARO_KEY_TAB: P.toggleView(); break;
+            case CHIARO_KEY_EQUAL: P.exposureUp(); break;
+            case CHIARO_KEY_MINUS: P.exposureDown(); break;
+            case CHIARO_KEY_W: P.move(FORWARD, dt, shift != 0); break;
+            case CHIARO_KEY_S: P.move(BACKWARD, dt, shift != 0); break;
+            case CHIARO_KEY_A: P.move(LEFT, dt, shift != 0); break;
+            case CHIARO_KEY_D: P.move(RIGHT, dt, shift != 0); break;
+            case CHIARO_KEY_E: P.move(UPWARD, dt, shift != 0); break;
+            case CHIARO_KEY_Q: P.move(DOWNWARD, dt, shift != 0); break;
+            default: return CR_E_INVALID;
+            }
+            return CR_OK;
+        },
+        CR_E_HIP);
+}
+
+int chiaro_preview_mouse(chiaro_preview *p, float xoffset, float yoffset) {
+    if (!p) return CR_E_INVALID;
+    p->p->look(xoffset, yoffset);
+    return CR_OK;
+}
+
+int chiaro_preview_scroll(chiaro_preview *p, float yoffset) {
+    if (!p) return CR_E_INVALID;
+    p->p->scroll(yoffset);
+    return CR_OK;
+}
+
+const uint8_t *chiaro_preview_texture(chiaro_preview *p, uint32_t *w, uint32_t *h) {
+    if (!p) return nullptr;
+    if (w) *w = p->p->width();
+    if (h) *h = p->p->height();
+    return p->p->texture();
+}
+
+int chiaro_preview_state(const chiaro_preview *p, float pos[3], float front[3], float up[3], float *zoom,
+                         int *show_render, uint32_t *renders) {
+    if (!p) return CR_E_INVALID;
+    const PreviewCamera &c = p->p->camera;
+    for (int i = 0; i < 3; i++) {
+        if (pos) pos[i] = c.Position[i];
+        if (front) front[i] = c.Front[i];
+        if (up) up[i] = c.Up[i];
+    }
+    if (zoom) *zoom = c.Zoom;
+    if (show_render) *show_render = p->p->showRender ? 1 : 0;
+    if (renders) *renders = p->p->renders;
+    return CR_OK;
+}
+
+void chiaro_preview_destroy(chiaro_preview *p) { delete p; }

@@ -11,6 +11,10 @@
  *   chiaro_raytracer_data / _maxval / _normalize / _export
  *                            getData / maxVal / normalizeImage / exportImage (rayTracer.cpp:171-279)
  *   chiaro_camera            the camera basis of rayTrace          src/rayTracer.cpp:41-49
+ *   chiaro_preview_*         OpenGLPreview's render path without a window: camera,
+ *                            key R / TAB / = / - / WASDQE, mouse, scroll, the screen
+ *                            texture                               src/openglPreview.cpp:12-257,
+ *                                                                  src/camera.cpp
  *
  * Errors: functions return NULL / a negative code; chiaro_last_error() (per thread)
  * gives the message.  C++ exceptions never cross this boundary.
@@ -86,6 +90,27 @@ void chiaro_raytracer_destroy(chiaro_raytracer *r);
 
 int chiaro_camera(const float eye[3], const float center[3], const float up[3], float yview, uint32_t xres,
                   uint32_t yres, cr_camera *out);
+
+/* Headless preview session over a RayTracer (and its Scene: exposure keys change it). */
+typedef struct chiaro_preview chiaro_preview;
+enum {
+    CHIARO_KEY_R = 0,     /* render a layer at the camera, show it            */
+    CHIARO_KEY_TAB = 1,   /* toggle render / model view                        */
+    CHIARO_KEY_EQUAL = 2, /* exposure + 0.2, re-normalise                      */
+    CHIARO_KEY_MINUS = 3, /* exposure - 0.2, re-normalise                      */
+    CHIARO_KEY_W = 4, CHIARO_KEY_S = 5, CHIARO_KEY_A = 6, CHIARO_KEY_D = 7, CHIARO_KEY_E = 8, CHIARO_KEY_Q = 9
+};
+chiaro_preview *chiaro_preview_create(chiaro_scene *s, chiaro_raytracer *r);
+/* one key press; dt = frame time for the movement keys, shift = LEFT_SHIFT held */
+int chiaro_preview_key(chiaro_preview *p, int key, float dt, int shift);
+int chiaro_preview_mouse(chiaro_preview *p, float xoffset, float yoffset);
+int chiaro_preview_scroll(chiaro_preview *p, float yoffset);
+/* the screen texture (RayTracer::getData after normalizeImage), width x height x RGB8 */
+const uint8_t *chiaro_preview_texture(chiaro_preview *p, uint32_t *width, uint32_t *height);
+/* camera Position, Front, Up, Zoom (degrees); show_render, renders so far */
+int chiaro_preview_state(const chiaro_preview *p, float position[3], float front[3], float up[3], float *zoom,
+                         int *show_render, uint32_t *renders);
+void chiaro_preview_destroy(chiaro_preview *p);
 
 #ifdef __cplusplus
 }
