@@ -36,6 +36,11 @@ def test_preview_progressive_render(ca, po, scenes):
             o, _ = pair.oracle.render(cam, 48, 36, 2, i["k"], i["seed"], layer=L, pixels=o)
         return o
 
+    # the reference camera's Yaw starts as atan2 in radians but is read as degrees
+    # (src/camera.cpp:16, 76): from cornell's VP / LA it looks along +x, out of the
+    # box; turn it to -z (yaw -90 degrees) with the mouse as a user would
+    pv.mouse(-900.0, 0.0)
+    assert pv.state()["front"][2] < -0.99
     for n in (1, 2, 3):  # R pressed three times at one camera: layers 1..3
         pv.key("R")
         assert rt.layers == n and pv.state()["renders"] == n and pv.state()["show_render"]
@@ -51,6 +56,7 @@ def test_preview_progressive_render(ca, po, scenes):
     pv.key("TAB")
     pv.key("W", dt=0.5)
     pv.mouse(12.0, -4.0)
+    pv.scroll(3.0)
     st = pv.state()
     assert not np.array_equal(st["position"], np.float32(i["VP"]))
     pv.key("R")  # new camera: accumulation restarts
