@@ -340,20 +340,51 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     HIPCHK(hipSetDevice(c->device));
     free_scene(c);
     const uint32_t nt = d->n_tris;
-    // nodes -> {split bits | first, axis | child<<2}
-    std::vector<uint2> nodes(d->n_nodes);
-    for (uint32_t i = 0; i < d->n_nodes; i++) {
+    // nodes -> {split bits | first, axis | child<<2}, validated first
+    const uint32_t NN = d->n_nodes;
+    for (uint32_t i = 0; i < NN; i++) {
         const cr_kdnode &n = d->nodes[i];
         if (n.axis == 3) {
             if (n.count >= (1u << 30) || (uint64_t)n.child_or_first + n.count > d->n_refs)
                 return fail(c, CR_E_INVALID, "bad leaf range");
-            nodes[i] = make_uint2(n.child_or_first, 3u | (n.count << 2));
+        } else if (n.axis > 2 || (uint64_t)n.child_or_first + 1 >= NN || n.child_or_first >= (1u << 30)) {
+            return fail(c, CR_E_INVALID, "bad inner node");
+        }
+    }
+    // node numbering: the first NODE_BFS nodes breadth-first from the root (each inner
+    // node's two children take consecutive ids, as KDTree::build allocates them), the
+    // rest in the reference's depth-first order -- the top of the tree is nodes
+    // 0..NODE_BFS-1 for the LDS node tile; only addresses change, not the traversal
+    std::vector<uint32_t> newid(NN, 0xffffffffu), order;
+    order.reserve(NN);
+    order.push_back(0);
+    newid[0] = 0;
+    for (size_t h = 0; h < order.size() && order.size() + 2 <= cr::NODE_BFS; h++) {
+        const cr_kdnode &n = d->nodes[order[h]];
+        if (n.axis == 3) continue;
+        for (uint32_t k = 0; k < 2; k++) {
+            const uint32_t ch = n.child_or_first + k;
+            if (newid[ch] != 0xffffffffu) return fail(c, CR_E_INVALID, "kd node with two parents");
+            newid[ch] = (uint32_t)order.size();
+            order.push_back(ch);
+        }
+    }
+    for (uint32_t i = 0; i < NN; i++)
+        if (newid[i] == 0xffffffffu) {
+            newid[i] = (uint32_t)order.size();
+            order.push_back(i);
+        }
+    std::vector<uint2> nodes(NN);
+    for (uint32_t i = 0; i < NN; i++) {
+        const cr_kdnode &n = d->nodes[i];
+        if (n.axis == 3) {
+            nodes[newid[i]] = make_uint2(n.child_or_first, 3u | (n.count << 2));
         } else {
-            if (n.axis > 2 || n.child_or_first + 1 >= d->n_nodes || n.child_or_first >= (1u << 30))
-                return fail(c, CR_E_INVALID, "bad inner node");
+            const uint32_t ch = newid[n.child_or_first];
+            if (newid[n.child_or_first + 1] != ch + 1) return fail(c, CR_E_INVALID, "kd siblings not adjacent");
             uint32_t sb;
             std::memcpy(&sb, &n.split, 4);
-            nodes[i] = make_uint2(sb, n.axis | (n.child_or_first << 2));
+            nodes[newid[i]] = make_uint2(sb, n.axis | (ch << 2));
         }
     }
     // fat node records: a node's own record followed by both children's
@@ -436,6 +467,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         return rc;
     }
     c->S.nlights = d->n_lights;
+    c->S.n_nodes = d->n_nodes;
     c->S.bmin = make_float3(d->box_min[0], d->box_min[1], d->box_min[2]);
     c->S.bmax = make_float3(d->box_max[0], d->box_max[1], d->box_max[2]);
     c->stack_depth = d->max_depth > 0 ? d->max_depth : 1;

@@ -38,8 +38,13 @@ struct DevScene {
     const uint4 *texs;    // {w, h, nc, byte offset}
     const uint8_t *texels;
     uint32_t nlights;
+    uint32_t n_nodes;
     float3 bmin, bmax;    // padded root box
 };
+// cr_upload_scene numbers the first NODE_BFS nodes breadth-first (sibling pairs kept
+// adjacent, the rest in the reference's depth-first order), so the top of the tree
+// is nodes 0..NODE_BFS-1 (the LDS node tile of trace builds 10-11).
+enum : uint32_t { NODE_BFS = 512 };
 
 struct RenderArgs {
     DevScene S;

@@ -124,10 +124,13 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // are bound by the scalar unit's exec-mask bookkeeping, SURVEY §8d / DESIGN §3.3):
 // a descent step branches only around its stack push, and a uniform leaf's
 // triangle tests keep their result by select (tri_test_wave).
-template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false>
+// TILE (FAT builds): fat records of nodes 0..TILE-1 -- the top of the tree, which
+// cr_upload_scene numbers breadth-first -- are read from the block's LDS copy
+// `tile` instead of through the vector-memory address path.
+template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
-                                               Ctr &c) {
+                                               Ctr &c, const uint4 *tile = nullptr) {
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -182,14 +185,22 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
     uint2 nd;
     if (FAT) { // two levels per dependent load: a node's record carries its children's
         uint4 f0, f1;
-        load_fat<SC>(S, T.node, f0, f1);
+        auto fetch = [&](uint32_t node) {
+            if (TILE && node < (uint32_t)TILE) {
+                f0 = tile[2 * node];
+                f1 = tile[2 * node + 1];
+            } else {
+                load_fat<SC>(S, node, f0, f1);
+            }
+        };
+        fetch(T.node);
         nd = make_uint2(f0.x, f0.y);
         while ((nd.y & 3u) != 3u) {
             const uint32_t k = step(nd);
             nd = k ? make_uint2(f1.x, f1.y) : make_uint2(f0.z, f0.w);
             if ((nd.y & 3u) == 3u) break;
             step(nd);
-            load_fat<SC>(S, T.node, f0, f1);
+            fetch(T.node);
             nd = make_uint2(f0.x, f0.y);
         }
     } else {

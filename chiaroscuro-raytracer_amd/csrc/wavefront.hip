@@ -170,10 +170,17 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // same code: it is the largest launch of a pass and never runs beside another
 // trace, so profiles and the bench roofline see it separately.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false, bool BF = false>
+          bool CAM = false, bool BF = false, int TILE = 0>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
+    // TILE: the top of the tree (fat records of nodes 0..TILE-1) copied into LDS after the stack ring
+    uint4 *tile = (uint4 *)(ring_lds + R * blockDim.x);
+    if (TILE) {
+        const uint32_t nt = 2u * min((uint32_t)TILE, S.n_nodes);
+        for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) tile[i] = S.fat[i];
+        __syncthreads();
+    }
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63u;
     const uint32_t n = SHADOW ? *cnt_shadow(W, g) : *cnt_closest(W, g);
     uint32_t *work = SHADOW ? work_shadow(W, g) : work_closest(W, g);
@@ -223,8 +230,8 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF>(S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW,
-                                                                 exclude, T, c);
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE>(S, ring_lds, W.gstack, W.gstride, gid, o,
+                                                                       d, SHADOW, exclude, T, c, tile);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
@@ -560,20 +567,26 @@ struct WfVariant {
     void (*camera)(RenderArgs, WfArgs, uint32_t);
     void (*closest)(RenderArgs, WfArgs, uint32_t);
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
-    int ring, waves_per_simd;
+    int ring, waves_per_simd, tile;
 };
-#define CR_WF_BF(R, W, SC, FD, FAT, PF, BF)                                                                    \
-    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF>, wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF>, \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF>, R, W}
+#define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL)                                                                 \
+    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL>,                                              \
+     wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL>,                                             \
+     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL>, R, W, TL}
+#define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
 #define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
 #define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
 static const WfVariant kWf[] = {
     CR_WF(4, 8, false, false, false), CR_WF(8, 8, false, false, false), CR_WF(8, 8, true, false, false),
     CR_WF(8, 6, false, false, false), CR_WF(8, 6, true, false, false),  CR_WF(8, 8, true, true, false),
     CR_WF(8, 8, true, false, true),   CR_WF(8, 8, false, false, true),  CR_WF_PF(8, 8, true, false, false, 2),
-    CR_WF_BF(8, 8, true, false, true, 1, true)};
+    CR_WF_BF(8, 8, true, false, true, 1, true),
+    // 10-12: build 9 with the top of the tree in LDS (TILE nodes, 32 B each, after the
+    // stack ring: 8 blocks x (R x 2 KiB + TILE x 32 B) within the CU's 160 KiB)
+    CR_WF_T(8, 8, true, false, true, 1, true, 128), CR_WF_T(4, 8, true, false, true, 1, true, 384),
+    CR_WF_T(4, 8, true, false, true, 1, true, 0)};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
-                                   wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4};
+                                   wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
 
@@ -652,7 +665,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     wf_tail_geometry(num_cus, tblk, tblocks);
     if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
-    const size_t lds = (size_t)v.ring * blk * sizeof(uint2);
+    const size_t lds = (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
     int err = 0;
     // the rest of the chunk from closest queue g on, in one launch
