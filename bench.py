@@ -184,6 +184,8 @@ def main():
     ap.add_argument("--gather", default="torch", choices=("torch", "cabi"),
                     help="N > 1: tile gather by torch.distributed (default) or the library's own RCCL "
                          "communicator (cr_comm_init / cr_render_dist_device)")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="cr_set_option before the scene upload (experiments; the default build is timed without)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -220,6 +222,9 @@ def main():
     model = ca.Model(scene)
     kd = ca.KDTree(model, scene)
     dev = ca.Device(dev_index)
+    for kv in args.opt:
+        key, val = kv.split("=", 1)
+        dev.set_option(key, int(val, 0))
     dev.upload(kd.describe())
     if args.kernel >= 0:
         dev.set_option("kernel", args.kernel)

@@ -359,7 +359,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     order.reserve(NN);
     order.push_back(0);
     newid[0] = 0;
-    for (size_t h = 0; h < order.size() && order.size() + 2 <= cr::NODE_BFS; h++) {
+    for (size_t h = 0; h < order.size() && order.size() + 2 <= c->node_bfs; h++) {
         const cr_kdnode &n = d->nodes[order[h]];
         if (n.axis == 3) continue;
         for (uint32_t k = 0; k < 2; k++) {
@@ -691,6 +691,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_dir_res") && v >= 1 && v <= 256 && (v & (v - 1)) == 0)
         c->wf_dir_res = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
+    else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);
     return CR_OK;
