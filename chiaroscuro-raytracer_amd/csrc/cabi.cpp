@@ -131,9 +131,10 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(1, (1ull << 31) / std::max<uint32_t>(A.n_items, 1)));
         chunk = std::min<uint64_t>(chunk, p->spp);
         const bool chunked = chunk < p->spp;
-        // wavefront: a second stack-overflow area for the closest trace that runs beside a shadow trace
+        // wavefront: a second stack-overflow area for the closest trace that runs beside a
+        // shadow trace, per lane
         if (int r = grow(c, &c->d_gstack, c->gstack_bytes,
-                         (wf ? 2 : 1) * cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
+                         (wf ? 2 * c->wf_lanes : 1) * cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
             return r;
         if (int r = grow(c, &c->d_samples, c->samples_bytes, per_sample * chunk)) return r;
         if (chunked)
@@ -142,14 +143,20 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         A.samples = (float *)c->d_samples;
         A.run = (float *)c->d_run;
         cr::WfArgs W{};
+        cr::WfArgs W2{};
+        const int lanes = wf ? c->wf_lanes : 1;
         if (wf) {
             // path slots per wavefront chunk, and the queues / state carved from one buffer
-            // ... at most ~45% of the currently free HBM (the buffer is reused, so only a
-            // growth needs the headroom)
-            uint64_t P = std::min<uint64_t>((uint64_t)A.n_items * chunk, c->wf_paths);
+            // per lane ... at most ~45% of the currently free HBM in all (the buffers are
+            // reused, so only a growth needs the headroom).  Two lanes: two chunks in flight,
+            // the second starting once the first is past its camera-ray trace.
+            uint64_t P = (uint64_t)A.n_items * chunk;
+            if (lanes == 2) P = (P + 1) / 2;
+            P = std::min<uint64_t>(P, c->wf_paths);
             size_t freeb = 0, totalb = 0;
             if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-                const uint64_t cap = (uint64_t)((freeb + c->wf_bytes) * 0.45) / cr::wf_bytes_per_path(p->k);
+                const uint64_t cap = (uint64_t)((freeb + c->wf_bytes + c->wf2_bytes) * 0.45) /
+                                     cr::wf_bytes_per_path(p->k) / (uint64_t)lanes;
                 P = std::max<uint64_t>(std::min<uint64_t>(P, cap), std::min<uint64_t>(P, 1u << 20));
             }
             const size_t f4 = 16 * (size_t)P;
@@ -165,43 +172,50 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                                 (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
                                 8192;
             if (int r = grow(c, &c->d_wf, c->wf_bytes, need)) return r;
-            char *b = (char *)c->d_wf;
-            auto take = [&](size_t bytes) {
-                char *r = b;
-                b += (bytes + 255) & ~(size_t)255;
-                return r;
+            if (lanes == 2)
+                if (int r = grow(c, &c->d_wf2, c->wf2_bytes, need)) return r;
+            auto carve = [&](void *base, cr::WfArgs &W, int lane) {
+                char *b = (char *)base;
+                auto take = [&](size_t bytes) {
+                    char *r = b;
+                    b += (bytes + 255) & ~(size_t)255;
+                    return r;
+                };
+                W.ray[0] = (float4 *)take(2 * f4);
+                W.ray[1] = (float4 *)take(2 * f4);
+                W.hit[0] = (uint4 *)take(f4);
+                W.hit[1] = (uint4 *)take(f4);
+                W.sray = (float4 *)take(2 * f4);
+                W.ps = (float4 *)take(cr::WF_STATE * f4);
+                W.dw = (float4 *)take(2 * (size_t)p->k * f4);
+                W.sexcl = (uint32_t *)take(4 * (size_t)P);
+                W.occ = (uint32_t *)take(4 * (size_t)P);
+                W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
+                W.sort = c->wf_sort && nkeys <= (1ull << 32);
+                W.key_bits = key_bits;
+                W.sort_min = c->wf_sort_min;
+                W.sort_tile = c->wf_sort_tile;
+                W.dir_res = c->wf_dir_res;
+                W.world_keys = nworld <= (1ull << 32) ? c->wf_world_keys : 0;
+                W.world_bits = c->wf_world_bits;
+                W.tail_min = c->wf_tail_min;
+                if (c->wf_sort) {
+                    for (int q = 0; q < 2; q++)
+                        for (int i = 0; i < 2; i++) {
+                            W.key[q][i] = (uint32_t *)take(4 * (size_t)P);
+                            W.perm[q][i] = (uint32_t *)take(4 * (size_t)P);
+                        }
+                    W.sort_tmp = take(sort_tmp);
+                    W.sort_tmp_bytes = sort_tmp;
+                }
+                const size_t area = (size_t)c->stack_depth * A.gstride;
+                W.gstack = A.gstack + 2 * (size_t)lane * area;
+                W.gstack2 = W.gstack + area;
+                W.gstride = A.gstride;
+                W.P = (uint32_t)P;
             };
-            W.ray[0] = (float4 *)take(2 * f4);
-            W.ray[1] = (float4 *)take(2 * f4);
-            W.hit[0] = (uint4 *)take(f4);
-            W.hit[1] = (uint4 *)take(f4);
-            W.sray = (float4 *)take(2 * f4);
-            W.ps = (float4 *)take(cr::WF_STATE * f4);
-            W.dw = (float4 *)take(2 * (size_t)p->k * f4);
-            W.sexcl = (uint32_t *)take(4 * (size_t)P);
-            W.occ = (uint32_t *)take(4 * (size_t)P);
-            W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
-            W.sort = c->wf_sort && nkeys <= (1ull << 32);
-            W.key_bits = key_bits;
-            W.sort_min = c->wf_sort_min;
-            W.sort_tile = c->wf_sort_tile;
-            W.dir_res = c->wf_dir_res;
-            W.world_keys = nworld <= (1ull << 32) ? c->wf_world_keys : 0;
-            W.world_bits = c->wf_world_bits;
-            W.tail_min = c->wf_tail_min;
-            if (c->wf_sort) {
-                for (int q = 0; q < 2; q++)
-                    for (int i = 0; i < 2; i++) {
-                        W.key[q][i] = (uint32_t *)take(4 * (size_t)P);
-                        W.perm[q][i] = (uint32_t *)take(4 * (size_t)P);
-                    }
-                W.sort_tmp = take(sort_tmp);
-                W.sort_tmp_bytes = sort_tmp;
-            }
-            W.gstack = A.gstack;
-            W.gstack2 = A.gstack + (size_t)c->stack_depth * A.gstride;
-            W.gstride = A.gstride;
-            W.P = (uint32_t)P;
+            carve(c->d_wf, W, 0);
+            if (lanes == 2) carve(c->d_wf2, W2, 1);
         } else {
             if (int r = grow(c, &c->d_pathbuf, c->pathbuf_bytes, cr::persistent_pathbuf_bytes(p->k, A.gstride)))
                 return r;
@@ -214,7 +228,11 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             A.s_count = (uint32_t)std::min<uint64_t>(chunk, p->spp - s0);
             A.n_work = A.n_items * A.s_count;
             int e = 0;
-            if (wf) {
+            if (wf && lanes == 2) {
+                cr::WfLane L[2] = {{W, st, c->wfs.side, c->wfs.fork, c->wfs.join, c->lane_ev[0], c->hcnt},
+                                   {W2, c->stream2, c->side2, c->fork2, c->join2, c->lane_ev[1], c->hcnt + 2}};
+                e = cr::run_wavefront_lanes(A, L, 2, c->num_cus, st, &c->tev);
+            } else if (wf) {
                 const uint32_t P = W.P;
                 for (uint32_t w0 = 0; w0 < A.n_work && !e; w0 += P) {
                     W.w0 = w0;
@@ -292,6 +310,13 @@ cr_ctx *cr_create(int device) {
         hipStreamCreateWithFlags(&c->wfs.side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->wfs.fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->wfs.join, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fork2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->join2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->lane_ev[1], hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void **)&c->hcnt, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->d_counters, cr::CTR_SLOTS * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_work, 16 * sizeof(uint32_t)) != hipSuccess) {
@@ -324,6 +349,14 @@ void cr_destroy(cr_ctx *c) {
         if (c->wfs.side) hipStreamDestroy(c->wfs.side);
         if (c->wfs.fork) hipEventDestroy(c->wfs.fork);
         if (c->wfs.join) hipEventDestroy(c->wfs.join);
+        if (c->stream2) hipStreamDestroy(c->stream2);
+        if (c->side2) hipStreamDestroy(c->side2);
+        if (c->fork2) hipEventDestroy(c->fork2);
+        if (c->join2) hipEventDestroy(c->join2);
+        for (hipEvent_t e : c->lane_ev)
+            if (e) hipEventDestroy(e);
+        if (c->hcnt) hipHostFree(c->hcnt);
+        if (c->d_wf2) hipFree(c->d_wf2);
     }
     delete c;
 }
@@ -691,6 +724,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_dir_res") && v >= 1 && v <= 256 && (v & (v - 1)) == 0)
         c->wf_dir_res = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_lanes") && (v == 1 || v == 2)) c->wf_lanes = (int)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);

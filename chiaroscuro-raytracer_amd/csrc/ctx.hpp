@@ -17,6 +17,13 @@ struct cr_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     cr::WfStreams wfs{nullptr, nullptr, nullptr}; // wavefront side stream + fork / join events
+    // second wavefront lane (wf_lanes 2): its main / side streams, fork / join events;
+    // per lane a queue-length event and pinned host words for the lengths
+    hipStream_t stream2 = nullptr, side2 = nullptr;
+    hipEvent_t fork2 = nullptr, join2 = nullptr, lane_ev[2] = {nullptr, nullptr};
+    uint32_t *hcnt = nullptr;
+    void *d_wf2 = nullptr;
+    size_t wf2_bytes = 0;
     float last_ms = 0.f;
     // scene
     bool has_scene = false;
@@ -64,6 +71,7 @@ struct cr_ctx {
     // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
     // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do
     uint64_t sample_buf = cr::SAMPLE_BUF_BYTES;
+    int wf_lanes = 1;                 // wavefront chunks in flight at once (1 or 2)
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

@@ -149,6 +149,22 @@ struct TraceEvents {
     int cap = 0, n = 0;
 };
 // One chunk: camera, closest 1, then per generation shade, shadow || next closest, resolve.
+// Two chunks in flight (cr_set_option "wf_lanes" 2): each lane owns a buffer set
+// (W, W.P = its capacity), a main and a side stream with fork / join events, an
+// event marking its queue lengths copied, and 2 pinned host words for them.  The
+// host advances both lanes' generations without blocking (event polling); a
+// chunk starts on a free lane once the other lane's chunk is past its camera-ray
+// trace, so a VALU-bound camera trace runs beside address-bound secondary traces
+// and one chunk's generation tails beside the other's work.  Lane 0's main
+// stream is `st`; lane 1's joins `st` at entry and exit.
+struct WfLane {
+    WfArgs W;
+    hipStream_t st, side;
+    hipEvent_t fork, join, ready;
+    uint32_t *hcnt;
+};
+int run_wavefront_lanes(const RenderArgs &A, WfLane *lanes, int nlanes, int num_cus, hipStream_t st,
+                        TraceEvents *te);
 int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st, const WfStreams &ss,
                            TraceEvents *te = nullptr);
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,

@@ -27,6 +27,8 @@
 // queues and the trace waves stay coherent.
 #include "traverse.hpp"
 
+#include <thread>
+
 namespace cr {
 
 enum : uint32_t { NO_SLOT = 0xffffffffu, NO_PATH = 0xffffffffu };
@@ -726,6 +728,135 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
             break;
         }
     }
+    return err ? err : (int)hipGetLastError();
+}
+
+int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hipStream_t st, TraceEvents *te) {
+    const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
+    uint32_t blk, blocks, tblk, tblocks;
+    wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
+    wf_tail_geometry(num_cus, tblk, tblocks);
+    for (int i = 0; i < nl; i++)
+        if (L[i].W.gstride < blk * blocks || L[i].W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
+    const size_t lds = (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4);
+    const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8;
+    int err = 0;
+    struct Run {
+        WfArgs W;
+        uint32_t g = 0;
+        int phase = 0; // 0 idle, 1 shade g, 2 wait for queue lengths of g
+        bool past_camera = false;
+    } run[2];
+    auto tail = [&](WfLane &ln, WfArgs &W, uint32_t g) {
+        const size_t tlds = (size_t)8 * tblk * sizeof(uint2);
+        W.order = nullptr;
+        if ((err = trace_event(te, ln.st, TK_TAIL, true))) return;
+        if (A.full_counters)
+            hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+        else
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+        err = trace_event(te, ln.st, TK_TAIL, false);
+    };
+    auto closest = [&](const WfArgs &W, uint32_t g, hipStream_t s, const uint32_t *order, uint2 *gstack) {
+        WfArgs Wc = W;
+        Wc.order = order;
+        Wc.gstack = gstack;
+        const int kind = g == 1 ? TK_CAMERA : TK_CLOSEST;
+        if ((err = trace_event(te, s, kind, true))) return;
+        hipLaunchKernelGGL(g == 1 ? v.camera : v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
+        err = trace_event(te, s, kind, false);
+    };
+    auto shade = [&](WfLane &ln, Run &r) { // wf_shade(g), then the queue lengths to the host, async
+        hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, r.g);
+        if ((err = (int)hipMemcpyAsync(&ln.hcnt[0], r.W.cnt + WF_G + r.g, 4, hipMemcpyDeviceToHost, ln.st)) ||
+            (err = (int)hipMemcpyAsync(&ln.hcnt[1], r.W.cnt + r.g + 1, 4, hipMemcpyDeviceToHost, ln.st)) ||
+            (err = (int)hipEventRecord(ln.ready, ln.st)))
+            return;
+        r.phase = 2;
+    };
+    auto start = [&](WfLane &ln, Run &r, uint32_t w0, uint32_t P) {
+        r.W = ln.W;
+        r.W.w0 = w0;
+        r.W.P = P;
+        r.g = 1;
+        r.past_camera = false;
+        if ((err = (int)hipMemsetAsync(r.W.cnt, 0, WF_CNT * sizeof(uint32_t), ln.st))) return;
+        hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, ln.st, A, r.W);
+        if (P < r.W.tail_min) {
+            tail(ln, r.W, 1);
+            r.phase = 0;
+            r.past_camera = true;
+            return;
+        }
+        closest(r.W, 1, ln.st, nullptr, r.W.gstack); // camera rays: path order is already coherent
+        if (!err) shade(ln, r);
+    };
+    // one generation's traces once its queue lengths are on the host; false: not yet
+    auto advance = [&](WfLane &ln, Run &r) -> bool {
+        const hipError_t q = hipEventQuery(ln.ready);
+        if (q == hipErrorNotReady) return false;
+        if (q != hipSuccess) {
+            err = (int)q;
+            return true;
+        }
+        r.past_camera = true;
+        const uint32_t g = r.g, ns = ln.hcnt[0];
+        const uint32_t nc = g < (uint32_t)A.K ? ln.hcnt[1] : 0u;
+        const bool next = nc >= r.W.tail_min && nc > 0;
+        const uint32_t *order_s = order_queue(r.W, 0, ns, ln.st, err);
+        const uint32_t *order_c = next ? order_queue(r.W, 1, nc, ln.st, err) : nullptr;
+        if (err) return true;
+        if (next) {
+            if ((err = (int)hipEventRecord(ln.fork, ln.st)) || (err = (int)hipStreamWaitEvent(ln.side, ln.fork, 0)))
+                return true;
+            closest(r.W, g + 1, ln.side, order_c, r.W.gstack2);
+            if (err) return true;
+        }
+        WfArgs Ws = r.W;
+        Ws.order = order_s;
+        if ((err = trace_event(te, ln.st, TK_SHADOW, true))) return true;
+        hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, ln.st, A, Ws, g);
+        if ((err = trace_event(te, ln.st, TK_SHADOW, false))) return true;
+        hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, g);
+        if (next) {
+            if ((err = (int)hipEventRecord(ln.join, ln.side)) || (err = (int)hipStreamWaitEvent(ln.st, ln.join, 0)))
+                return true;
+            r.g = g + 1;
+            shade(ln, r);
+        } else {
+            if (nc > 0) tail(ln, r.W, g + 1);
+            r.phase = 0;
+        }
+        return true;
+    };
+    // lanes > 0 start after the work already queued on st
+    for (int i = 1; i < nl && !err; i++)
+        if (!(err = (int)hipEventRecord(L[i].ready, st))) err = (int)hipStreamWaitEvent(L[i].st, L[i].ready, 0);
+    uint32_t next_w0 = 0;
+    while (!err) {
+        bool progress = false, busy = false;
+        for (int i = 0; i < nl && !err; i++) {
+            if (run[i].phase == 0) {
+                bool others_past = true;
+                for (int j = 0; j < nl; j++)
+                    if (j != i && run[j].phase != 0 && !run[j].past_camera) others_past = false;
+                if (next_w0 < A.n_work && others_past) {
+                    const uint32_t P = min(L[i].W.P, A.n_work - next_w0);
+                    start(L[i], run[i], next_w0, P);
+                    next_w0 += P;
+                    progress = true;
+                }
+            } else {
+                progress = advance(L[i], run[i]) || progress;
+            }
+            busy = busy || run[i].phase != 0;
+        }
+        if (!busy && next_w0 >= A.n_work) break;
+        if (!progress) std::this_thread::yield();
+    }
+    // st waits for the other lanes' last work
+    for (int i = 1; i < nl && !err; i++)
+        if (!(err = (int)hipEventRecord(L[i].ready, L[i].st))) err = (int)hipStreamWaitEvent(st, L[i].ready, 0);
     return err ? err : (int)hipGetLastError();
 }
 

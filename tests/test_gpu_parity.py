@@ -69,6 +69,26 @@ def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
+    """Two chunks in flight (wf_lanes 2: the frame's paths split in two, the second
+    chunk started once the first is past its camera trace, per-lane buffers,
+    streams and stacks), with the default per-generation launches and with the
+    tail kernel, counting and lean builds."""
+    for pair, (x, y, s) in ((sponza, (128, 72, 4)), (nanobox, (64, 48, 4)), (cornell, (64, 64, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_lanes", lanes)
+        try:
+            for tail_min in (0, 20000):
+                pair.dev.set_option("wf_tail_min", tail_min)
+                g, gc, o, oc = _render_both(ca, pair, x, y, s)
+                assert_bitwise(g, o, "wf_lanes %d tail_min %d %dx%dx%d" % (lanes, tail_min, x, y, s))
+                assert {k: gc[k] for k in ORACLE_KEYS} == oc
+        finally:
+            pair.dev.set_option("wf_lanes", 1)
+            pair.dev.set_option("wf_tail_min", 0)
+
+
 @pytest.mark.parametrize("tail_min", [1 << 30, 12000, 3000])
 def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min):
     """wf_tail (the last generations of a chunk in one launch, per-path bodies
@@ -329,12 +349,15 @@ def test_c5_sample_chunking_progressive(ca, sponza, nanobox, kernel):
             pair.dev.set_option("kernel", 2)
 
 
-def test_c5_multi_chunk_wavefront(ca, sponza, nanobox):
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_c5_multi_chunk_wavefront(ca, sponza, nanobox, lanes):
     """More work items than path slots: the wavefront runs chunk after chunk of
-    wf_paths = 4096 paths (cabi.cpp w0 loop), also combined with sample chunking,
-    over progressive layers 1..3, counting and lean builds."""
+    wf_paths = 4096 paths (cabi.cpp w0 loop; with 2 lanes two chunks in flight,
+    run_wavefront_lanes), also combined with sample chunking, over progressive
+    layers 1..3, counting and lean builds."""
     for pair, (x, y) in ((sponza, (96, 54)), (nanobox, (64, 48))):
         pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_lanes", lanes)
         pair.dev.set_option("wf_paths", 4096)
         cam = pair.camera(ca, x, y)
         o = None
@@ -357,6 +380,7 @@ def test_c5_multi_chunk_wavefront(ca, sponza, nanobox):
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_paths", 256 << 20)
             pair.dev.set_option("sample_buf_bytes", 4 << 30)
+            pair.dev.set_option("wf_lanes", 1)
 
 
 def test_c5_eight_rank_tile32_split_sponza(ca, sponza):
