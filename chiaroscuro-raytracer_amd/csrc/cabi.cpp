@@ -167,7 +167,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             while (key_bits < 32 && (1ull << key_bits) < nkeys) key_bits++;
             const uint64_t nworld = (1ull << (3 * c->wf_world_bits)) * c->wf_dir_res * c->wf_dir_res;
             while (c->wf_world_keys && key_bits < 32 && (1ull << key_bits) < nworld) key_bits++;
-            const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits) : 0;
+            const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
             const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 8 * (size_t)P +
                                 (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
                                 8192;
@@ -193,6 +193,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
                 W.sort = c->wf_sort && nkeys <= (1ull << 32);
                 W.key_bits = key_bits;
+                W.sort_lib = c->wf_sort_lib;
                 W.sort_min = c->wf_sort_min;
                 W.sort_tile = c->wf_sort_tile;
                 W.dir_res = c->wf_dir_res;
@@ -724,6 +725,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_dir_res") && v >= 1 && v <= 256 && (v & (v - 1)) == 0)
         c->wf_dir_res = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_sort_lib") && (v == 0 || v == 1)) c->wf_sort_lib = (int)v;
     else if (!std::strcmp(key, "wf_lanes") && (v == 1 || v == 2)) c->wf_lanes = (int)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;

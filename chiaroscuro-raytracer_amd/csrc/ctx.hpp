@@ -71,6 +71,7 @@ struct cr_ctx {
     // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
     // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do
     uint64_t sample_buf = cr::SAMPLE_BUF_BYTES;
+    int wf_sort_lib = 0;              // 1: hipcub's radix sort for the queues (comparison)
     int wf_lanes = 1;                 // wavefront chunks in flight at once (1 or 2)
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL

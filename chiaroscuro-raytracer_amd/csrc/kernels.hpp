@@ -123,6 +123,7 @@ struct WfArgs {
     size_t sort_tmp_bytes;
     int sort;         // 1: write keys and sort the queues of large generations
     int key_bits;     // significant key bits
+    int sort_lib;     // 1: hipcub's radix sort instead of raysort.hip's (comparison)
     uint32_t sort_min;   // queues shorter than this are traced in append order
     uint32_t sort_tile;  // log2 of the pixel sub-tile edge of the key (3: 8x8 pixels)
     uint32_t dir_res;    // octahedral direction bins per axis (8: 64 bins; power of two)
@@ -167,9 +168,10 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *lanes, int nlanes, int num_
                         TraceEvents *te);
 int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hipStream_t st, const WfStreams &ss,
                            TraceEvents *te = nullptr);
+// raysort.hip: stable radix sort of (key, value) pairs; lib: hipcub's instead
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
-               hipStream_t st);
-size_t wf_sort_tmp_bytes(uint32_t n, int key_bits);
+               hipStream_t st, bool lib = false);
+size_t wf_sort_tmp_bytes(uint32_t n, int key_bits, bool lib = false);
 // Persistent grid geometry chosen by launch_render (block threads, blocks).
 void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);
 

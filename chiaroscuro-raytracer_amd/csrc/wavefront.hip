@@ -614,7 +614,7 @@ static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStre
     if (!W.sort || err || n < W.sort_min) return nullptr;
     uint32_t *keys[2] = {W.key[set][0], W.key[set][1]}, *vals[2] = {W.perm[set][0], W.perm[set][1]};
     size_t tb = W.sort_tmp_bytes;
-    const int sel = sort_queue(keys, vals, n, W.key_bits, W.sort_tmp, tb, st);
+    const int sel = sort_queue(keys, vals, n, W.key_bits, W.sort_tmp, tb, st, W.sort_lib != 0);
     if (sel < 0) {
         err = (int)hipErrorUnknown;
         return nullptr;
@@ -861,10 +861,10 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
 }
 
 // Bytes of sort workspace for queues of up to n rays (temp storage only).
-size_t wf_sort_tmp_bytes(uint32_t n, int key_bits) {
+size_t wf_sort_tmp_bytes(uint32_t n, int key_bits, bool lib) {
     size_t tb = 0;
     uint32_t *k[2] = {nullptr, nullptr}, *v[2] = {nullptr, nullptr};
-    sort_queue(k, v, n, key_bits, nullptr, tb, nullptr);
+    sort_queue(k, v, n, key_bits, nullptr, tb, nullptr, lib);
     return tb;
 }
 

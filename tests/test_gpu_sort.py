@@ -1,0 +1,26 @@
+"""GPU check of the wavefront queue sort (csrc/raysort.hip): the hand-written
+stable radix sort equals std::stable_sort and hipcub's DeviceRadixSort on
+random and clustered keys, at tile edges (4095 / 4096 / 4097 pairs) and key
+widths 1..32.  (The image never depends on the order -- the render parity
+tests force sorting of every queue -- but the coherence the sort buys does.)"""
+import json
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.gpu
+def test_queue_sort_is_stable_and_exact(tmp_path):
+    exe = tmp_path / "sort_check"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-I", str(ROOT / "chiaroscuro-raytracer_amd" / "csrc"), "-I", str(ROOT / "include"),
+                    str(ROOT / "tests" / "native" / "sort_check.hip"), "-o", str(exe)],
+                   check=True, capture_output=True, timeout=600)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    print(res, r.stderr[-2000:])
+    assert res["mismatch"] == 0 and res["differs_from_hipcub"] == 0 and res["cases"] == 154, res
+    assert r.returncode == 0
