@@ -39,17 +39,34 @@ __device__ __forceinline__ uint32_t tile_item(uint32_t wave, uint32_t round, uin
     return (wave * RS_ROUNDS + round) * 64u + lane;
 }
 
+// Per-wave histograms (no LDS atomic contention between waves); a round whose
+// valid lanes all hold one digit -- common: neighbouring queue entries are rays of
+// the same pixel -- adds its count with one atomic instead of 64 conflicting ones.
 __global__ void __launch_bounds__(RS_THREADS) rs_upsweep(const uint32_t *keys, uint32_t n, uint32_t shift,
                                                          uint32_t ntiles, uint32_t *H) {
-    __shared__ uint32_t hist[RS_BINS];
-    const uint32_t tile = blockIdx.x;
-    hist[threadIdx.x] = 0;
+    __shared__ uint32_t hist[RS_WAVES][RS_BINS];
+    const uint32_t tile = blockIdx.x, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t w = 0; w < RS_WAVES; w++) hist[w][threadIdx.x] = 0;
     __syncthreads();
     const uint32_t base = tile * RS_TILE;
-    for (uint32_t i = threadIdx.x; i < RS_TILE; i += RS_THREADS)
-        if (base + i < n) atomicAdd(&hist[(keys[base + i] >> shift) & (RS_BINS - 1)], 1u);
+    const uint32_t count = min(RS_TILE, n - base);
+#pragma unroll 4
+    for (uint32_t r = 0; r < RS_ROUNDS; r++) {
+        const uint32_t i = tile_item(wave, r, lane);
+        const bool ok = i < count;
+        const uint32_t d = ok ? (keys[base + i] >> shift) & (RS_BINS - 1) : 0u;
+        const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+        const uint64_t m_ok = __ballot(ok);
+        if (__ballot(ok && d == d0) == m_ok) {
+            if (lane == 0 && m_ok) atomicAdd(&hist[wave][d0], (uint32_t)__popcll(m_ok));
+        } else if (ok) {
+            atomicAdd(&hist[wave][d], 1u);
+        }
+    }
     __syncthreads();
-    H[(size_t)threadIdx.x * ntiles + tile] = hist[threadIdx.x];
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < RS_WAVES; w++) t += hist[w][threadIdx.x];
+    H[(size_t)threadIdx.x * ntiles + tile] = t;
 }
 
 // Block-wide exclusive scan of one value per thread; returns the block total in *total.
@@ -143,12 +160,15 @@ __global__ void __launch_bounds__(RS_THREADS) rs_downsweep(const uint32_t *keys_
         key[r] = ok ? keys_in[base + i] : 0u;
         val[r] = ok ? vals_in[base + i] : 0u;
         const uint32_t d = (key[r] >> shift) & (RS_BINS - 1);
-        uint64_t peers = __ballot(ok);
+        const uint64_t m_ok = __ballot(ok);
+        uint64_t peers = m_ok;
+        if (__ballot(ok && d == (uint32_t)__shfl((int)d, 0, 64)) != m_ok) { // more than one digit this round
 #pragma unroll
-        for (uint32_t b = 0; b < RS_BITS; b++) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
+            for (uint32_t b = 0; b < RS_BITS; b++) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t m = __ballot(bit);
+                peers &= bit ? m : ~m;
+            }
         }
         // lanes of this round with my digit, then the wave's earlier rounds
         const uint32_t before = wave_cnt[wave][d];
