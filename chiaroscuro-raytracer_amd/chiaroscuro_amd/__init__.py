@@ -126,7 +126,8 @@ HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_g
                 "chiaro_raytracer_counters", "chiaro_raytracer_normalize", "chiaro_raytracer_export",
                 "chiaro_raytracer_ctx", "chiaro_raytracer_destroy", "chiaro_camera",
                 "chiaro_preview_create", "chiaro_preview_key", "chiaro_preview_mouse", "chiaro_preview_scroll",
-                "chiaro_preview_texture", "chiaro_preview_state", "chiaro_preview_destroy")
+                "chiaro_preview_texture", "chiaro_preview_state", "chiaro_preview_destroy",
+                "chiaro_preview_camera_replay")
 
 P = C.c_void_p
 FP = C.POINTER(C.c_float)
@@ -232,6 +233,8 @@ def libs():
     _sig(host, "chiaro_preview_texture", C.POINTER(C.c_uint8), [P, UP, UP])
     _sig(host, "chiaro_preview_state", C.c_int, [P, FP, FP, FP, FP, C.POINTER(C.c_int), UP])
     _sig(host, "chiaro_preview_destroy", None, [P])
+    _sig(host, "chiaro_preview_camera_replay", C.c_int, [FP, FP, FP, C.c_float, C.POINTER(C.c_int32), FP, C.c_int,
+                                                         FP])
     _hip, _host = hip, host
     return hip, host
 
@@ -600,6 +603,19 @@ class RayTracer:
         if getattr(self, "_h", None) and _host is not None:
             _host.chiaro_raytracer_destroy(self._h)
             self._h = None
+
+
+def preview_camera_replay(vp, la, up, yview, ops, args) -> np.ndarray:
+    """chiaro_preview_camera_replay: the preview camera after each op -> [nops][15]
+    (Position, Front, Up, Right, Yaw, Pitch, Zoom).  No GPU."""
+    ops = np.ascontiguousarray(ops, np.int32)
+    args = np.ascontiguousarray(args, np.float32).reshape(-1)
+    out = np.zeros((len(ops), 15), np.float32)
+    rc = libs()[1].chiaro_preview_camera_replay(_fa(vp), _fa(la), _fa(up), float(yview), _ptr(ops, C.c_int32),
+                                                _ptr(args), len(ops), _ptr(out))
+    if rc:
+        raise ValueError("chiaro_preview_camera_replay: bad op")
+    return out
 
 
 class Preview:

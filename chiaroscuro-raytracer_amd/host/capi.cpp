@@ -372,3 +372,26 @@ int chiaro_preview_state(const chiaro_preview *p, float pos[3], float front[3], 
 }
 
 void chiaro_preview_destroy(chiaro_preview *p) { delete p; }
+
+int chiaro_preview_camera_replay(const float vp[3], const float la[3], const float up[3], float yview,
+                                 const int32_t *ops, const float *args, int nops, float *out) {
+    if (!vp || !la || !up || nops < 0 || (nops && (!ops || !args || !out))) return CR_E_INVALID;
+    PreviewCamera c(vec3(vp[0], vp[1], vp[2]), vec3(la[0], la[1], la[2]), vec3(up[0], up[1], up[2]));
+    c.Zoom = preview_zoom(yview);
+    for (int i = 0; i < nops; i++) {
+        const float a0 = args[2 * i], a1 = args[2 * i + 1];
+        if (ops[i] >= 0 && ops[i] <= 5) c.ProcessKeyboard((CameraMovement)ops[i], a0);
+        else if (ops[i] == 6) c.ProcessMouseMovement(a0, a1);
+        else if (ops[i] == 7) c.ProcessMouseScroll(a0);
+        else if (ops[i] == 8) c.MovementSpeed = a0;
+        else return CR_E_INVALID;
+        const vec3 v[4] = {c.Position, c.Front, c.Up, c.Right};
+        float *o = out + 15 * (size_t)i;
+        for (int k = 0; k < 4; k++)
+            for (int j = 0; j < 3; j++) o[3 * k + j] = v[k][j];
+        o[12] = c.Yaw;
+        o[13] = c.Pitch;
+        o[14] = c.Zoom;
+    }
+    return CR_OK;
+}

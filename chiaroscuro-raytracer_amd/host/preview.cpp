@@ -65,9 +65,11 @@ void PreviewCamera::updateCameraVectors() {
     Up = normalize(cross(Right, Front));
 }
 
+float preview_zoom(float yview) { return degrees(2.f * atanf(0.5f * yview)); }
+
 // src/openglPreview.cpp:12-15, 39
 PreviewSession::PreviewSession(Scene &s, RayTracer &r) : camera(s.VP, s.LA, s.UP), scene(s), renderer(r) {
-    camera.Zoom = degrees(2.f * atanf(0.5f * scene.yview));
+    camera.Zoom = preview_zoom(scene.yview);
 }
 
 // src/openglPreview.cpp:139-146, 247-251

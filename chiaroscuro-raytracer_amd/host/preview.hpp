@@ -24,6 +24,9 @@ struct PreviewCamera {
     void updateCameraVectors();
 };
 
+// OpenGLPreview's initial Zoom: glm::degrees(2 * atanf(0.5 * yview)) (src/openglPreview.cpp:39)
+float preview_zoom(float yview);
+
 class PreviewSession {
   public:
     // OpenGLPreview(Scene*) + setRenderer: camera from VP / LA / UP, Zoom from yview

@@ -111,6 +111,13 @@ const uint8_t *chiaro_preview_texture(chiaro_preview *p, uint32_t *width, uint32
 int chiaro_preview_state(const chiaro_preview *p, float position[3], float front[3], float up[3], float *zoom,
                          int *show_render, uint32_t *renders);
 void chiaro_preview_destroy(chiaro_preview *p);
+/* The preview camera alone (no GPU): Camera(VP, LA, UP) with Zoom from yview, then
+ * nops operations -- op 0..5 ProcessKeyboard(FORWARD..DOWNWARD, dt = a0), 6
+ * ProcessMouseMovement(a0, a1), 7 ProcessMouseScroll(a0), 8 MovementSpeed = a0
+ * (args: 2 per op) -- and after each: Position, Front, Up, Right, Yaw, Pitch, Zoom
+ * (15 floats per op) into out.  A GL-free front-end can plan camera paths with it. */
+int chiaro_preview_camera_replay(const float vp[3], const float la[3], const float up[3], float yview,
+                                 const int32_t *ops, const float *args, int nops, float *out);
 
 #ifdef __cplusplus
 }

@@ -9,8 +9,11 @@
 //   - glm normalize / cross / dot / distance / length, mat3 inverse
 //   - the kd-tree's per-triangle material normal   src/kdtree.cpp:58-60
 //     and light surface                            src/kdtree.cpp:72-77
+//   - the preview camera (src/camera.cpp, linked)  as OpenGLPreview drives it
+//     (src/openglPreview.cpp:12-15, 39, 178-195)
 // Nothing here is a stand-in for a missing header: every header it includes
 // ships in /root/reference/include.
+#include "camera.hpp"
 #include "mesh.hpp"
 
 #include <glm/glm.hpp>
@@ -70,5 +73,28 @@ void ref_material_normal(const float *n, float out[3]) {
 float ref_light_surface(const float *p) {
     glm::vec3 A(p[0], p[1], p[2]), B(p[3], p[4], p[5]), C(p[6], p[7], p[8]);
     return 0.5f * glm::length(glm::cross(B - A, C - A));
+}
+}
+
+extern "C" {
+// OpenGLPreview's camera: Camera(VP, LA, UP), Zoom from yview, then nops operations
+// (op 0..5 ProcessKeyboard(op, a0), 6 ProcessMouseMovement(a0, a1), 7
+// ProcessMouseScroll(a0), 8 MovementSpeed = a0); after each: Position, Front, Up,
+// Right, Yaw, Pitch, Zoom (15 floats).
+void ref_preview_camera(const float *vp, const float *la, const float *up, float yview, const int *ops,
+                        const float *args, int nops, float *out) {
+    Camera cam(glm::vec3(vp[0], vp[1], vp[2]), glm::vec3(la[0], la[1], la[2]), glm::vec3(up[0], up[1], up[2]));
+    cam.Zoom = glm::degrees(2.f * atanf(0.5f * yview));
+    for (int i = 0; i < nops; i++) {
+        const float a0 = args[2 * i], a1 = args[2 * i + 1];
+        if (ops[i] >= 0 && ops[i] <= 5) cam.ProcessKeyboard((Camera_Movement)ops[i], a0);
+        else if (ops[i] == 6) cam.ProcessMouseMovement(a0, a1);
+        else if (ops[i] == 7) cam.ProcessMouseScroll(a0);
+        else if (ops[i] == 8) cam.MovementSpeed = a0;
+        const glm::vec3 v[4] = {cam.Position, cam.Front, cam.Up, cam.Right};
+        float *o = out + 15 * i;
+        for (int k = 0; k < 4; k++) { o[3 * k] = v[k].x; o[3 * k + 1] = v[k].y; o[3 * k + 2] = v[k].z; }
+        o[12] = cam.Yaw; o[13] = cam.Pitch; o[14] = cam.Zoom;
+    }
 }
 }

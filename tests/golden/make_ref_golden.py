@@ -8,6 +8,8 @@ and records its outputs on fixed inputs as JSON fixtures:
   ref_texture.json  G5: Texture::getColorAt at wrap / edge coordinates, RGB, RGBA, grey
   ref_glm.json      G6 camera bases + normalize / cross / dot / distance / material
                     normal / light surface on fixed and random vectors
+  ref_preview_camera.json  the preview camera (src/camera.cpp as OpenGLPreview drives
+                    it) over scripted key / mouse / scroll sequences
 
 Floats are stored as their IEEE-754 bit patterns (uint32) so tests compare bitwise.
 Usage:  python tests/golden/make_ref_golden.py      (needs /root/reference)
@@ -114,7 +116,29 @@ def main() -> int:
         tri.append({"p": bits(p), "material_normal": bits(mn), "surface": bits([L.ref_light_surface(pp)])[0]})
     (ROOT / "tests" / "golden" / "ref_glm.json").write_text(
         json.dumps({"camera": camera, "primitives": prims, "triangles": tri}, indent=0))
-    print("wrote ref_texture.json, ref_glm.json")
+    # ---- preview camera (src/camera.cpp)
+    L.ref_preview_camera.argtypes = [FP, FP, FP, C.c_float, C.POINTER(C.c_int), FP, C.c_int, FP]
+    prng = np.random.default_rng(777)
+    seqs = []
+    for vp, la, up, yv in (((0.0, 1.0, 2.95), (0.0, 1.0, 0.0), (0.0, 1.0, 0.0), 1.0),
+                           ((278.0, 273.0, -800.0), (278.0, 273.0, 0.0), (0.0, 1.0, 0.0), 0.7),
+                           ((10.0, 16.0, 10.0), (0.0, 8.5, 0.0), (0.0, 1.0, 0.0), 1.0),
+                           ((0.3, -2.0, 5.0), (1.0, 0.5, -3.0), (0.1, 0.9, 0.2), 1.7)):
+        n = 120
+        ops = prng.integers(0, 9, n).astype(np.int32)
+        args = np.stack([prng.uniform(-40, 40, n), prng.uniform(-40, 40, n)], 1).astype(np.float32)
+        args[ops <= 5, 0] = np.abs(args[ops <= 5, 0]) / 100.0          # frame times
+        args[ops == 8, 0] = np.where(prng.random((ops == 8).sum()) < 0.5, 2.5, 30.0)  # shift speeds
+        out = np.zeros((n, 15), np.float32)
+        v_, vpp = fp(vp)
+        l_, lp = fp(la)
+        u_, upp = fp(up)
+        L.ref_preview_camera(vpp, lp, upp, yv, ops.ctypes.data_as(C.POINTER(C.c_int)), args.ctypes.data_as(FP), n,
+                             out.ctypes.data_as(FP))
+        seqs.append({"vp": list(vp), "la": list(la), "up": list(up), "yview": yv, "ops": ops.tolist(),
+                     "args": bits(args), "out": bits(out)})
+    (ROOT / "tests" / "golden" / "ref_preview_camera.json").write_text(json.dumps({"sequences": seqs}, indent=0))
+    print("wrote ref_texture.json, ref_glm.json, ref_preview_camera.json")
     return 0
 
 

@@ -108,3 +108,20 @@ def test_sincos_restatement_equals_host_libm(po):
               np.float32(3 * np.pi / 2)):
         u = int(c.view(np.uint32))
         assert po.sincos_check(u - (1 << 16), u + (1 << 16), 1) == 0
+
+
+def test_preview_camera_matches_reference(ca):
+    """The headless preview's camera (host/preview.cpp PreviewCamera) against the
+    reference's own src/camera.cpp driven as OpenGLPreview drives it (constructor
+    from VP / LA / UP, Zoom from yview, keyboard / mouse / scroll / speed ops):
+    Position, Front, Up, Right, Yaw, Pitch, Zoom after every op, bit for bit.
+    (Not the render loop itself: a pin on the preview driver)"""
+    data = json.loads((GOLD / "ref_preview_camera.json").read_text())
+    n = 0
+    for s in data["sequences"]:
+        args = f32(s["args"]).reshape(-1, 2)
+        got = ca.preview_camera_replay(s["vp"], s["la"], s["up"], s["yview"], s["ops"], args)
+        want = np.asarray(s["out"], np.uint32).reshape(-1, 15)
+        assert np.array_equal(got.view(np.uint32), want), np.argwhere(got.view(np.uint32) != want)[:5]
+        n += len(s["ops"])
+    assert n == 480
