@@ -438,9 +438,11 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     // leaf-ordered triangle records {A,id},{B-A},{C-A}: e1/e2 computed exactly as
     // intersectRayTriangle does each time (kdtree.cpp:222-223), so bit-identical.
     // load_rec addresses records with a 32-bit byte offset
-    if ((uint64_t)16 * cr::REC_STRIDE * (uint64_t)d->n_refs > 0xFFFFFFFFull)
+    if ((uint64_t)16 * cr::REC_STRIDE * ((uint64_t)d->n_refs + 1) > 0xFFFFFFFFull)
         return fail(c, CR_E_INVALID, "more than 89 M leaf references (triangle records exceed 4 GiB)");
-    std::vector<float4> recs((size_t)cr::REC_STRIDE * d->n_refs, make_float4(0.f, 0.f, 0.f, 0.f));
+    // + one zero record past the last: the paired scalar loads of uniform leaves
+    // (trace build 13) may read the record after a leaf's last one
+    std::vector<float4> recs((size_t)cr::REC_STRIDE * ((size_t)d->n_refs + 1), make_float4(0.f, 0.f, 0.f, 0.f));
     for (uint32_t r = 0; r < d->n_refs; r++) {
         const uint32_t t = d->refs[r];
         if (t >= nt) return fail(c, CR_E_INVALID, "leaf ref out of range");

@@ -81,6 +81,7 @@ typedef unsigned int cr_v2u __attribute__((ext_vector_type(2)));
 typedef float cr_v4f __attribute__((ext_vector_type(4)));
 typedef float cr_v8f __attribute__((ext_vector_type(8)));
 typedef unsigned int cr_v8u __attribute__((ext_vector_type(8)));
+typedef float cr_v16f __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ uint2 sload_node(const uint2 *p) {
     cr_v2u r;
     asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
@@ -94,6 +95,19 @@ __device__ __forceinline__ TriRec sload_rec(const float4 *p) {
                  : "s"(p));
     return TriRec{make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]),
                   make_float4(b[0], b[1], b[2], b[3])};
+}
+// Two consecutive records with one wait (96 B: the record after a leaf's last one
+// is in bounds, cr_upload_scene pads the buffer with one).
+__device__ __forceinline__ void sload_rec2(const float4 *p, TriRec &r0, TriRec &r1) {
+    cr_v16f a;
+    cr_v8f b;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx8 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(a), "=s"(b)
+                 : "s"(p));
+    r0 = TriRec{make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]),
+                make_float4(a[8], a[9], a[10], a[11])};
+    r1 = TriRec{make_float4(a[12], a[13], a[14], a[15]), make_float4(b[0], b[1], b[2], b[3]),
+                make_float4(b[4], b[5], b[6], b[7])};
 }
 template <bool SC> __device__ __forceinline__ uint2 load_node(const DevScene &S, uint32_t node) {
     if (SC && wave_uniform(node)) return sload_node(S.nodes + __builtin_amdgcn_readfirstlane(node));
@@ -127,7 +141,9 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // TILE (FAT builds): fat records of nodes 0..TILE-1 -- the top of the tree, which
 // cr_upload_scene numbers breadth-first -- are read from the block's LDS copy
 // `tile` instead of through the vector-memory address path.
-template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0>
+// UL2 (BF + SC builds): a uniform leaf's records come two per scalar-load wait.
+template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
+          bool UL2 = false>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr) {
@@ -269,9 +285,16 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
     if (BF && SC && wave_uniform(first)) { // uniform leaf, results by select
         const uint32_t uf = __builtin_amdgcn_readfirstlane(first), uc = __builtin_amdgcn_readfirstlane(count);
         const float4 *base = S.recs + (size_t)REC_STRIDE * uf;
+        TriRec pair[2];
         for (uint32_t j = 0; j < uc; j++) {
             tally_tri(uf + j);
-            const TriRec r = sload_rec(base + (size_t)REC_STRIDE * j);
+            TriRec r;
+            if (UL2) {
+                if ((j & 1u) == 0) sload_rec2(base + (size_t)REC_STRIDE * j, pair[0], pair[1]);
+                r = pair[j & 1u];
+            } else {
+                r = sload_rec(base + (size_t)REC_STRIDE * j);
+            }
             const uint32_t id = rec_id(r);
             const bool live = !(shadow && (occluded || id == exclude));
             if (FULL) c.tritest += live ? 1u : 0u;

@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // same code: it is the largest launch of a pass and never runs beside another
 // trace, so profiles and the bench roofline see it separately.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false, bool BF = false, int TILE = 0>
+          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
@@ -232,8 +232,8 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE>(S, ring_lds, W.gstack, W.gstride, gid, o,
-                                                                       d, SHADOW, exclude, T, c, tile);
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2>(S, ring_lds, W.gstack, W.gstride,
+                                                                            gid, o, d, SHADOW, exclude, T, c, tile);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
@@ -571,10 +571,11 @@ struct WfVariant {
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd, tile;
 };
-#define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL)                                                                 \
-    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL>,                                              \
-     wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL>,                                             \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL>, R, W, TL}
+#define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2)                                                             \
+    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2>,                                          \
+     wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>,                                         \
+     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>, R, W, TL}
+#define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
 #define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
 #define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
 #define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
@@ -586,7 +587,9 @@ static const WfVariant kWf[] = {
     // 10-12: build 9 with the top of the tree in LDS (TILE nodes, 32 B each, after the
     // stack ring: 8 blocks x (R x 2 KiB + TILE x 32 B) within the CU's 160 KiB)
     CR_WF_T(8, 8, true, false, true, 1, true, 128), CR_WF_T(4, 8, true, false, true, 1, true, 384),
-    CR_WF_T(4, 8, true, false, true, 1, true, 0)};
+    CR_WF_T(4, 8, true, false, true, 1, true, 0),
+    // 13: build 9 with a uniform leaf's records two per scalar-load wait
+    CR_WF_U(8, 8, true, false, true, 1, true, 0, true)};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
