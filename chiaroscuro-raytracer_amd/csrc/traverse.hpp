@@ -285,16 +285,9 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
     if (BF && SC && wave_uniform(first)) { // uniform leaf, results by select
         const uint32_t uf = __builtin_amdgcn_readfirstlane(first), uc = __builtin_amdgcn_readfirstlane(count);
         const float4 *base = S.recs + (size_t)REC_STRIDE * uf;
-        TriRec pair[2];
-        for (uint32_t j = 0; j < uc; j++) {
+        // one triangle of the uniform leaf; false: every active lane occluded (stop)
+        auto utest = [&](const TriRec &r, uint32_t j) -> bool {
             tally_tri(uf + j);
-            TriRec r;
-            if (UL2) {
-                if ((j & 1u) == 0) sload_rec2(base + (size_t)REC_STRIDE * j, pair[0], pair[1]);
-                r = pair[j & 1u];
-            } else {
-                r = sload_rec(base + (size_t)REC_STRIDE * j);
-            }
             const uint32_t id = rec_id(r);
             const bool live = !(shadow && (occluded || id == exclude));
             if (FULL) c.tritest += live ? 1u : 0u;
@@ -302,14 +295,24 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             const bool acc = live && tri_test_wave(o, d, r, T.tmax, ux, uy, t);
             if (shadow) {
                 occluded = occluded || acc;
-                if (__ballot(!occluded) == 0) break; // every active lane occluded
-            } else {
-                bx = acc ? ux : bx;
-                by = acc ? uy : by;
-                T.tmax = acc ? t : T.tmax;
-                tri = acc ? id : tri;
-                found = found || acc;
+                return __ballot(!occluded) != 0;
             }
+            bx = acc ? ux : bx;
+            by = acc ? uy : by;
+            T.tmax = acc ? t : T.tmax;
+            tri = acc ? id : tri;
+            found = found || acc;
+            return true;
+        };
+        if (UL2) {
+            for (uint32_t j = 0; j < uc; j += 2) {
+                TriRec r0, r1;
+                sload_rec2(base + (size_t)REC_STRIDE * j, r0, r1);
+                if (!utest(r0, j) || j + 1 >= uc || !utest(r1, j + 1)) break;
+            }
+        } else {
+            for (uint32_t j = 0; j < uc; j++)
+                if (!utest(sload_rec(base + (size_t)REC_STRIDE * j), j)) break;
         }
     } else if (SC && wave_uniform(first)) { // every lane at the same leaf: scalar loads
         const float4 *base = S.recs + (size_t)REC_STRIDE * __builtin_amdgcn_readfirstlane(first);
