@@ -106,8 +106,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 6 = 2 + fat node records (a node and both children in 32 B: one dependent load per two
     // descent levels): 595.0 vs 597.5 ms per 1080p x 128 spp pass, 83.0 vs 84.2 ms for rank 0 of 8;
     // 9 = 6 with branch-light descent steps and uniform-leaf tests (fewer scalar-unit exec-mask
-    // instructions): 563.8 vs 565.5 ms, rank 0 of 8 77.48 vs 77.64 ms (5 interleaved rounds)
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 9 : 0);
+    // instructions): 563.8 vs 565.5 ms, rank 0 of 8 77.48 vs 77.64 ms (5 interleaved rounds);
+    // 14 = 9 whose camera-ray trace skips triangle tests (and whole leaves) outside their
+    // screen-space cull boxes (camcull.hpp): camera trace 193 -> 119 ms, 565 -> 489 ms per pass
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 14 : 0);
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -168,7 +170,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             const uint64_t nworld = (1ull << (3 * c->wf_world_bits)) * c->wf_dir_res * c->wf_dir_res;
             while (c->wf_world_keys && key_bits < 32 && (1ull << key_bits) < nworld) key_bits++;
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
-            const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 8 * (size_t)P +
+            const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 16 * (size_t)P +
                                 (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
                                 8192;
             if (int r = grow(c, &c->d_wf, c->wf_bytes, need)) return r;
@@ -191,6 +193,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.sexcl = (uint32_t *)take(4 * (size_t)P);
                 W.occ = (uint32_t *)take(4 * (size_t)P);
                 W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
+                W.cxy = (float2 *)take(8 * (size_t)P);
                 W.sort = c->wf_sort && nkeys <= (1ull << 32);
                 W.key_bits = key_bits;
                 W.sort_lib = c->wf_sort_lib;
@@ -222,8 +225,20 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 return r;
             A.pathbuf = (float4 *)c->d_pathbuf;
         }
+        // screen-space cull boxes of this camera for the camera-ray trace (camcull.hpp),
+        // computed inside the timed region of every render
+        const bool cull = wf && !c->full_counters && cr::wf_variant_culls(A.variant) && c->n_refs > 0;
+        if (cull) {
+            if (int r = grow(c, &c->d_cull, c->cull_bytes, 16 * ((size_t)c->n_refs + 3))) return r;
+            if (int r = grow(c, &c->d_cull_node, c->cull_node_bytes, 16 * (size_t)c->S.n_nodes)) return r;
+        }
+        A.cull = cull ? (const float4 *)c->d_cull : nullptr;
+        A.cull_node = cull ? (const float4 *)c->d_cull_node : nullptr;
         c->tev.n = 0;
         HIPCHK(hipEventRecord(c->ev0, st));
+        if (cull)
+            if (int e = cr::launch_cam_cull(A, c->n_refs, (float4 *)c->d_cull, (float4 *)c->d_cull_node, st))
+                return hip_fail(c, (hipError_t)e, "cull-box kernel launch");
         for (uint32_t s0 = 0; s0 < p->spp; s0 += (uint32_t)chunk) {
             A.s0 = s0;
             A.s_count = (uint32_t)std::min<uint64_t>(chunk, p->spp - s0);
@@ -339,6 +354,8 @@ void cr_destroy(cr_ctx *c) {
         if (c->d_samples) hipFree(c->d_samples);
         if (c->d_run) hipFree(c->d_run);
         if (c->d_wf) hipFree(c->d_wf);
+        if (c->d_cull) hipFree(c->d_cull);
+        if (c->d_cull_node) hipFree(c->d_cull_node);
         if (c->d_counters) hipFree(c->d_counters);
         if (c->d_work) hipFree(c->d_work);
         if (c->ev0) hipEventDestroy(c->ev0);
@@ -507,6 +524,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     c->S.bmin = make_float3(d->box_min[0], d->box_min[1], d->box_min[2]);
     c->S.bmax = make_float3(d->box_max[0], d->box_max[1], d->box_max[2]);
     c->stack_depth = d->max_depth > 0 ? d->max_depth : 1;
+    c->n_refs = d->n_refs;
     c->has_scene = true;
     return CR_OK;
 }

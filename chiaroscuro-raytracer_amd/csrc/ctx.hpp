@@ -29,6 +29,7 @@ struct cr_ctx {
     bool has_scene = false;
     cr::DevScene S{};
     uint32_t stack_depth = 1;
+    uint32_t n_refs = 0;     // leaf references (triangle records) of the scene
     std::vector<void *> scene_bufs;
     // work buffers
     unsigned long long *d_counters = nullptr;
@@ -37,6 +38,10 @@ struct cr_ctx {
     size_t accum_elems = 0;
     void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
     size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
+    void *d_cull = nullptr;  // camera-ray cull boxes, one per leaf reference (+ 3), per render
+    size_t cull_bytes = 0;
+    void *d_cull_node = nullptr; // ... their per-leaf unions, one per kd node
+    size_t cull_node_bytes = 0;
     cr_counters last{};
     cr::TraceEvents tev;     // wavefront trace launches of the last render (cr_get_trace_stats)
     cr_trace_stats last_trace{};

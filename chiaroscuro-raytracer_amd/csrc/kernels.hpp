@@ -74,6 +74,11 @@ struct RenderArgs {
     uint32_t s0, s_count, n_work;
     float *samples;               // [n_items][s_count][3] path radiance per work item
     float *run;                   // [n_items][3] running per-pixel sum across sample chunks
+    // wavefront camera trace builds with the screen-space cull (camcull.hpp): per leaf
+    // reference {xmin, xmax, ymin, ymax} of the sample positions at which its triangle can
+    // accept a camera ray of this camera (null: no cull)
+    const float4 *cull;
+    const float4 *cull_node;      // [n_nodes] per leaf: the union of its references' boxes
 };
 int num_persistent_variants();
 
@@ -131,15 +136,22 @@ struct WfArgs {
                          // generation >= g (shadow queue g, closest queue g + 1); 0: pixel keys only
     uint32_t world_bits; // bits per axis of the origin's Morton code
     uint32_t tail_min;   // a closest queue shorter than this hands the rest of the chunk to wf_tail (0: never)
+    float2 *cxy;         // [P] screen position (sx, sy) of path p's camera sample (written when A.cull)
 };
-// rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms
-inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32; }
+// rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
+// camera sample position
+inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8; }
 // Second stream and fork / join events of a render (shadow trace g beside closest trace g + 1).
 struct WfStreams {
     hipStream_t side;
     hipEvent_t fork, join;
 };
 int num_wf_variants();
+// true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
+bool wf_variant_culls(int variant);
+// cull boxes of this render's camera for the nrefs leaf references (+ 3 padding boxes)
+// and the per-leaf unions (node_boxes[n_nodes]; inner nodes: the whole plane)
+int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *node_boxes, hipStream_t st);
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
 void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks);
 // HIP events bracketing every trace launch (start, stop), recorded on the launch

@@ -138,13 +138,17 @@ __device__ __forceinline__ f3 tex_lookup(const DevScene &S, int ti, float u, flo
     return mk((float)px[0] * 0.00392156862f, (float)px[1] * 0.00392156862f, (float)px[2] * 0.00392156862f);
 }
 
-__device__ __forceinline__ f3 camera_dir(const RenderArgs &A, uint32_t x, uint32_t y, Rng &rng) {
+// sxy: the sample's screen position (sx, sy), which the direction is affine in (camcull.hpp)
+__device__ __forceinline__ f3 camera_dir(const RenderArgs &A, uint32_t x, uint32_t y, Rng &rng,
+                                         float2 *sxy = nullptr) {
     const f3 lu = mk(A.cam[3], A.cam[4], A.cam[5]), dx = mk(A.cam[6], A.cam[7], A.cam[8]),
              dy = mk(A.cam[9], A.cam[10], A.cam[11]);
     // rayTracer.cpp:61 -- the y-jitter draw is evaluated first (g++ order)
     const float uy = rng_uniform(rng, 0.f, 1.f);
     const float ux = rng_uniform(rng, 0.f, 1.f);
-    return add(add(lu, muls(dx, (float)x + ux)), muls(dy, (float)y + uy));
+    const float sx = (float)x + ux, sy = (float)y + uy;
+    if (sxy) *sxy = make_float2(sx, sy);
+    return add(add(lu, muls(dx, sx)), muls(dy, sy));
 }
 
 // Work item -> pixel: this rank's tiles (tile t -> rank t % nranks), row-major in a tile.

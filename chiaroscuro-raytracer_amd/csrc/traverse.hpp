@@ -109,6 +109,21 @@ __device__ __forceinline__ void sload_rec2(const float4 *p, TriRec &r0, TriRec &
     r1 = TriRec{make_float4(a[12], a[13], a[14], a[15]), make_float4(b[0], b[1], b[2], b[3]),
                 make_float4(b[4], b[5], b[6], b[7])};
 }
+// Four consecutive cull boxes (64 B; cull buffers carry three padding boxes).
+__device__ __forceinline__ cr_v16f sload_box4(const float4 *p) {
+    cr_v16f r;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
+    return r;
+}
+__device__ __forceinline__ float4 sload_box(const float4 *p) {
+    cr_v4f r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
+    return make_float4(r[0], r[1], r[2], r[3]);
+}
+template <bool SC> __device__ __forceinline__ float4 load_box(const float4 *b, uint32_t i) {
+    if (SC && wave_uniform(i)) return sload_box(b + __builtin_amdgcn_readfirstlane(i));
+    return b[i];
+}
 template <bool SC> __device__ __forceinline__ uint2 load_node(const DevScene &S, uint32_t node) {
     if (SC && wave_uniform(node)) return sload_node(S.nodes + __builtin_amdgcn_readfirstlane(node));
     return S.nodes[node];
@@ -142,11 +157,19 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // cr_upload_scene numbers breadth-first -- are read from the block's LDS copy
 // `tile` instead of through the vector-memory address path.
 // UL2 (BF + SC builds): a uniform leaf's records come two per scalar-load wait.
+// CULL (camera rays; BF + SC, PF 1): a triangle test runs only when the lane's sample
+// position (csx, csy) lies in the reference's cull box (camcull.hpp) -- outside it the
+// test cannot accept, so skipping it changes nothing.  A uniform leaf reads four boxes
+// per scalar load and tests a triangle only if some lane is inside its box; a divergent
+// lane reads its box (16 B) and, inside, the record (48 B).
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false>
+          bool UL2 = false, bool CULL = false>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
-                                               Ctr &c, const uint4 *tile = nullptr) {
+                                               Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
+                                               float csy = 0.f, const float4 *cull = nullptr,
+                                               const float4 *cull_node = nullptr) {
+    static_assert(!CULL || (BF && SC && PF == 1 && !FULL && !UL2), "cull: lean BF + SC builds");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -230,7 +253,13 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         c.leaf++;
         if (wave_leader()) c.wave_round++;
     }
-    const uint32_t first = nd.x, count = nd.y >> 2;
+    const uint32_t first = nd.x;
+    uint32_t count = nd.y >> 2;
+    bool lin = true; // CULL: the sample lies in the leaf's box (the union of its references')
+    if (CULL) {
+        const float4 lb = load_box<SC>(cull_node, T.node);
+        lin = csx >= lb.x && csx <= lb.y && csy >= lb.z && csy <= lb.w;
+    }
     bool found = false, occluded = false;
     uint32_t tri = 0;
     float bx = 0.f, by = 0.f;
@@ -304,7 +333,19 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             found = found || acc;
             return true;
         };
-        if (UL2) {
+        if (CULL) {
+            const float4 *cb = cull + uf;
+            for (uint32_t j = 0; j < uc && __ballot(lin); j += 4) {
+                const cr_v16f bx = sload_box4(cb + j);
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    if (j + k >= uc) break;
+                    const bool in = csx >= bx[4 * k] && csx <= bx[4 * k + 1] && csy >= bx[4 * k + 2] &&
+                                    csy <= bx[4 * k + 3];
+                    if (__ballot(in)) utest(sload_rec(base + (size_t)REC_STRIDE * (j + k)), j + k);
+                }
+            }
+        } else if (UL2) {
             for (uint32_t j = 0; j < uc; j += 2) {
                 TriRec r0, r1;
                 sload_rec2(base + (size_t)REC_STRIDE * j, r0, r1);
@@ -331,6 +372,16 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             if (j + 2 < count) ra = load_rec(S, first + j + 2);
             tally_tri(first + j + 1);
             if (!test(rb)) break;
+        }
+    } else if (CULL) { // boxes pipelined one ahead; a record only for a sample inside its box
+        if (!lin) count = 0;
+        float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (count) nb = cull[first];
+        for (uint32_t j = 0; j < count; j++) {
+            const float4 b = nb;
+            if (j + 1 < count) nb = cull[first + j + 1];
+            if (csx >= b.x && csx <= b.y && csy >= b.z && csy <= b.w)
+                if (!test(load_rec(S, first + j))) break;
         }
     } else {
         TriRec nx;

@@ -25,6 +25,7 @@
 // Queue appends are wave-aggregated (one atomic per wave, lane order kept), so
 // neighbouring paths -- samples of the same pixel -- stay neighbours in the
 // queues and the trace waves stay coherent.
+#include "camcull.hpp"
 #include "traverse.hpp"
 
 #include <thread>
@@ -149,7 +150,9 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
         // partial-tile paths get a dead ray, path = NO_PATH)
         if (valid) { // rayTracer.cpp:58-62: jittered camera ray of sample s
             Rng rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
-            const f3 d = camera_dir(A, px, py, rng);
+            float2 sxy;
+            const f3 d = camera_dir(A, px, py, rng, &sxy);
+            if (A.cull) W.cxy[p] = sxy;
             PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), 1u);
             PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key);
             PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
@@ -171,9 +174,12 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // CAM: the generation-1 closest trace (camera rays) as its own instantiation, the
 // same code: it is the largest launch of a pass and never runs beside another
 // trace, so profiles and the bench roofline see it separately.
+// CULL (camera instantiation only): triangle tests skipped by the screen-space cull
+// boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false>
+          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, bool CULL = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
+    static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
     // TILE: the top of the tree (fat records of nodes 0..TILE-1) copied into LDS after the stack ring
@@ -190,6 +196,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     Ctr c = {};
     uint32_t state = ST_NEED_WORK, idx = 0, exclude = 0, issued = 0;
     f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
+    float csx = 0.f, csy = 0.f;
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
     const uint32_t busy_st = SHADOW ? ST_SHADOW : ST_CLOSEST;
     const uint32_t refill = SHADOW ? A.refill_shadow : (g == 1 ? A.refill_camera : A.refill);
@@ -214,6 +221,11 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         o = ld3(r0);
                         d = ld3(r1);
                         if (SHADOW) exclude = W.sexcl[idx];
+                        if (CULL) { // ray idx of generation 1 is path idx's camera ray
+                            const float2 q = W.cxy[idx];
+                            csx = q.x;
+                            csy = q.y;
+                        }
                         if (!SHADOW && __float_as_uint(r0.w) == NO_PATH) {
                             W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
                         } else if (issued++, trav_begin(S, o, d, SHADOW, r1.w, T)) {
@@ -232,8 +244,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2>(S, ring_lds, W.gstack, W.gstride,
-                                                                            gid, o, d, SHADOW, exclude, T, c, tile);
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL>(
+                S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
+                A.cull_node);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
@@ -570,11 +583,13 @@ struct WfVariant {
     void (*closest)(RenderArgs, WfArgs, uint32_t);
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd, tile;
+    bool cull; // the camera trace reads the cull boxes
 };
-#define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2)                                                             \
-    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2>,                                          \
+#define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU)                                                         \
+    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
      wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>,                                         \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>, R, W, TL}
+     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>, R, W, TL, CU}
+#define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, false)
 #define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
 #define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
 #define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
@@ -589,11 +604,62 @@ static const WfVariant kWf[] = {
     CR_WF_T(8, 8, true, false, true, 1, true, 128), CR_WF_T(4, 8, true, false, true, 1, true, 384),
     CR_WF_T(4, 8, true, false, true, 1, true, 0),
     // 13: build 9 with a uniform leaf's records two per scalar-load wait
-    CR_WF_U(8, 8, true, false, true, 1, true, 0, true)};
+    CR_WF_U(8, 8, true, false, true, 1, true, 0, true),
+    // 14: build 9 whose camera trace skips triangle tests by the screen-space cull boxes
+    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, true)};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
-                                   wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0};
+                                   wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
+                                   false};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
+bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].cull; }
+
+// One thread per leaf reference: its cull box for this render's camera (camcull.hpp),
+// from the record's A, e1, e2 -- the floats the triangle test uses.  Boxes
+// nrefs..nrefs+2 are empty (the four-box scalar loads of uniform leaves read past a
+// leaf's end).  Samples lie in [0, xres] x [0, yres] (global pixel coordinates).
+__global__ void __launch_bounds__(256) cam_cull_kernel(RenderArgs A, uint32_t nrefs, float4 *boxes) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrefs + 3) return;
+    if (r >= nrefs) {
+        boxes[r] = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
+        return;
+    }
+    CullCam cc;
+    for (int i = 0; i < 12; i++) cc.cam[i] = A.cam[i];
+    cc.xres = (float)A.xres;
+    cc.yres = (float)A.yres;
+    const float4 *q = A.S.recs + (size_t)REC_STRIDE * r;
+    const float4 a = q[0], e1 = q[1], e2 = q[2];
+    const float av[3] = {a.x, a.y, a.z}, e1v[3] = {e1.x, e1.y, e1.z}, e2v[3] = {e2.x, e2.y, e2.z};
+    float b[4];
+    cam_cull_box(av, e1v, e2v, cc, b);
+    boxes[r] = make_float4(b[0], b[1], b[2], b[3]);
+}
+
+// One thread per node: a leaf's box is the union of its references' boxes (a sample
+// outside it is outside every one of them: the whole leaf loop is skipped).
+__global__ void __launch_bounds__(256) cam_cull_leaf_kernel(RenderArgs A, const float4 *boxes, float4 *node_boxes) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.S.n_nodes) return;
+    const uint2 nd = A.S.nodes[i];
+    float4 u = make_float4(-INFINITY, INFINITY, -INFINITY, INFINITY);
+    if ((nd.y & 3u) == 3u) {
+        u = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
+        for (uint32_t j = 0, n = nd.y >> 2; j < n; j++) {
+            const float4 b = boxes[nd.x + j];
+            u = make_float4(fminf(u.x, b.x), fmaxf(u.y, b.y), fminf(u.z, b.z), fmaxf(u.w, b.w));
+        }
+    }
+    node_boxes[i] = u;
+}
+
+int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *node_boxes, hipStream_t st) {
+    const uint32_t n = nrefs + 3;
+    hipLaunchKernelGGL(cam_cull_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, nrefs, boxes);
+    hipLaunchKernelGGL(cam_cull_leaf_kernel, dim3((A.S.n_nodes + 255) / 256), dim3(256), 0, st, A, boxes, node_boxes);
+    return (int)hipGetLastError();
+}
 
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks) {
     const WfVariant &v = kWf[(variant >= 0 && variant < kNumWf) ? variant : 0];

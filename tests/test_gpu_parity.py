@@ -55,7 +55,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
     wave-uniform nodes / leaves) renders the same bits."""
@@ -67,6 +67,50 @@ def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
         sponza.dev.set_option("variant", -1)
     assert_bitwise(g, o, "wavefront variant %d" % variant)
     assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
+# cameras per scene for the cull test: the config's own, one close to a surface looking along it
+# (edge-on triangles), one wide-angle from inside the geometry (triangles behind / beside the eye)
+CULL_CAMS = {
+    "sponza": [None, ((-1500, 20, -200), (600, 10, 150), (0, 1, 0), 0.6), ((-200, 300, 50), (900, 250, 0), (0, 1, 0), 2.5)],
+    "nanobox": [None, ((9, 0.3, 9), (-5, 0.2, -4), (0, 1, 0), 0.8), ((2, 9, 2), (0, 8, -1), (0, 1, 0), 3.0)],
+    "cornell": [None, ((-0.95, 0.02, 1.5), (0.9, 0.01, -0.9), (0, 1, 0), 1.2), ((0.1, 1.0, 0.3), (0.0, 0.9, -1.0), (0, 1, 0), 3.0)],
+    "cornell_box": [None, ((30, 5, 20), (500, 3, 500), (0, 1, 0), 0.7), ((278, 273, 280), (278, 273, 0), (0, 1, 0), 2.0)],
+}
+
+
+@pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell", "cornell_box"])
+def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_mm, cfg):
+    """Trace build 14: the camera-ray trace skips Moller-Trumbore tests by per-render
+    screen-space cull boxes (camcull.hpp).  A skipped test could not have accepted, so
+    the image and the per-query counters equal the oracle's -- at the config's camera,
+    at an edge-on camera close to a surface and at a wide-angle camera inside the scene;
+    also tile-split (global pixel coordinates) and at an odd frame size."""
+    pair = {"sponza": sponza, "nanobox": nanobox, "cornell": cornell, "cornell_box": cornell_mm}[cfg]
+    pair.dev.set_option("kernel", 2)
+    pair.dev.set_option("variant", 14)
+    try:
+        for ci, spec in enumerate(CULL_CAMS[cfg]):
+            for (x, y, s) in ((96, 54, 4), (61, 37, 3)):
+                cam = pair.camera(ca, x, y) if spec is None else ca.camera(spec[0], spec[1], spec[2], spec[3], x, y)
+                p = ca.render_params(x, y, s, 6, 0xC41A05C0)
+                pair.dev.set_option("counters", 0)
+                try:
+                    g = pair.dev.render(cam, p)
+                    lc = pair.dev.counters()
+                    ts = pair.dev.trace_stats()
+                    gt = _tiles_frame(ca, pair.dev, cam, x, y, s, 3, 16)
+                finally:
+                    pair.dev.set_option("counters", 1)
+                o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0)
+                what = "%s camera %d %dx%dx%d" % (cfg, ci, x, y, s)
+                assert ts["camera"]["launches"] == 1, what
+                assert_bitwise(g, o, "cull " + what)
+                assert_bitwise(gt, o, "cull, 3 ranks x tile 16, " + what)
+                assert {k: lc[k] for k in ("closest", "shadow", "hit", "texhit", "paths")} == \
+                    {k: oc[k] for k in ("closest", "shadow", "hit", "texhit", "paths")}, what
+    finally:
+        pair.dev.set_option("variant", -1)
 
 
 @pytest.mark.parametrize("lanes", [1, 2])
@@ -197,6 +241,21 @@ def test_depth_limits_and_background(ca, cornell):
     g = cornell.dev.render(cam, p)
     o, _ = cornell.oracle.render(cam.as_array(), 16, 16, 2, 3, 1, bg=(0.25, 0.5, 1.0))
     assert_bitwise(g, o, "background")
+
+
+def _tiles_frame(ca, dev, cam, xres, yres, spp, nranks, tile, seed=0xC41A05C0):
+    """The frame as nranks ranks render it: each rank's tiles, then the root's blend."""
+    import torch
+    p0 = ca.render_params(xres, yres, spp, 6, seed, nranks=nranks, tile=tile)
+    maxt = ca.Device.tiles_for_rank(p0, 0)
+    gathered = torch.zeros((nranks, maxt, tile, tile, 3), dtype=torch.float32, device="cuda")
+    for r in range(nranks):
+        dev.render_tiles_device(cam, ca.render_params(xres, yres, spp, 6, seed, rank=r, nranks=nranks, tile=tile),
+                                gathered[r].data_ptr())
+    frame = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda")
+    dev.blend_tiles_device(p0, gathered.data_ptr(), frame.data_ptr())
+    torch.cuda.synchronize()
+    return frame.cpu().numpy()
 
 
 def test_tiles_partition_invariance(ca, cornell):
