@@ -28,6 +28,8 @@ void free_scene(cr_ctx *c) {
     c->scene_bufs.clear();
     c->has_scene = false;
     c->S = cr::DevScene{};
+    c->d_levels = nullptr;
+    c->levels.clear();
 }
 
 template <class T> int upload(cr_ctx *c, const std::vector<T> &h, const T **out) {
@@ -108,8 +110,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 9 = 6 with branch-light descent steps and uniform-leaf tests (fewer scalar-unit exec-mask
     // instructions): 563.8 vs 565.5 ms, rank 0 of 8 77.48 vs 77.64 ms (5 interleaved rounds);
     // 14 = 9 whose camera-ray trace skips triangle tests (and whole leaves) outside their
-    // screen-space cull boxes (camcull.hpp): camera trace 193 -> 119 ms, 565 -> 489 ms per pass
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 14 : 0);
+    // screen-space cull boxes (camcull.hpp): camera trace 193 -> 119 ms, 565 -> 489 ms per pass;
+    // 15 = 14 that also skips every fetched subtree whose box excludes the sample:
+    // camera trace 118 -> 70 ms, 488 -> 439 ms per pass
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 15 : 0);
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -237,7 +241,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         c->tev.n = 0;
         HIPCHK(hipEventRecord(c->ev0, st));
         if (cull)
-            if (int e = cr::launch_cam_cull(A, c->n_refs, (float4 *)c->d_cull, (float4 *)c->d_cull_node, st))
+            if (int e = cr::launch_cam_cull(A, c->n_refs, (float4 *)c->d_cull, (float4 *)c->d_cull_node, c->d_levels,
+                                            (const uint32_t(*)[2])c->levels.data(), (int)c->levels.size(), st))
                 return hip_fail(c, (hipError_t)e, "cull-box kernel launch");
         for (uint32_t s0 = 0; s0 < p->spp; s0 += (uint32_t)chunk) {
             A.s0 = s0;
@@ -511,7 +516,39 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         if (off > 0xffffffffull) return fail(c, CR_E_INVALID, "texture atlas > 4 GiB");
         texs[i] = make_uint4((uint32_t)t.width, (uint32_t)t.height, (uint32_t)t.components, (uint32_t)off);
     }
+    // inner nodes grouped by depth, deepest level first (children have larger ids than
+    // their parent in this numbering: one forward pass gives the depths)
+    std::vector<uint32_t> depth(NN, 0), levels;
+    std::vector<std::pair<uint32_t, uint32_t>> level_off;
+    {
+        uint32_t maxd = 0;
+        for (uint32_t i = 0; i < NN; i++) {
+            if ((nodes[i].y & 3u) == 3u) continue;
+            const uint32_t ch = nodes[i].y >> 2;
+            if (ch <= i) return fail(c, CR_E_INVALID, "kd child numbered before its parent");
+            depth[ch] = depth[ch + 1] = depth[i] + 1;
+            maxd = std::max(maxd, depth[i]);
+        }
+        std::vector<uint32_t> cnt(maxd + 1, 0);
+        for (uint32_t i = 0; i < NN; i++)
+            if ((nodes[i].y & 3u) != 3u) cnt[depth[i]]++;
+        uint32_t off = 0;
+        for (int dd = (int)maxd; dd >= 0; dd--) {
+            level_off.emplace_back(off, cnt[dd]);
+            off += cnt[dd];
+        }
+        levels.resize(off);
+        std::vector<uint32_t> pos(maxd + 1);
+        for (uint32_t dd = 0; dd <= maxd; dd++) pos[dd] = level_off[maxd - dd].first;
+        for (uint32_t i = 0; i < NN; i++)
+            if ((nodes[i].y & 3u) != 3u) levels[pos[depth[i]]++] = i;
+    }
+    const uint32_t *levels_dev = nullptr;
     int rc;
+    if ((rc = upload(c, levels, &levels_dev))) {
+        free_scene(c);
+        return rc;
+    }
     if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
@@ -525,6 +562,8 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     c->S.bmax = make_float3(d->box_max[0], d->box_max[1], d->box_max[2]);
     c->stack_depth = d->max_depth > 0 ? d->max_depth : 1;
     c->n_refs = d->n_refs;
+    c->d_levels = levels_dev;
+    c->levels = std::move(level_off);
     c->has_scene = true;
     return CR_OK;
 }

@@ -30,6 +30,10 @@ struct cr_ctx {
     cr::DevScene S{};
     uint32_t stack_depth = 1;
     uint32_t n_refs = 0;     // leaf references (triangle records) of the scene
+    // inner kd nodes grouped by depth (device ids, deepest level first) and the
+    // [offset, count) of each level: the bottom-up pass of the subtree cull boxes
+    const uint32_t *d_levels = nullptr;
+    std::vector<std::pair<uint32_t, uint32_t>> levels;
     std::vector<void *> scene_bufs;
     // work buffers
     unsigned long long *d_counters = nullptr;

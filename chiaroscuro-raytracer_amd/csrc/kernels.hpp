@@ -78,7 +78,7 @@ struct RenderArgs {
     // reference {xmin, xmax, ymin, ymax} of the sample positions at which its triangle can
     // accept a camera ray of this camera (null: no cull)
     const float4 *cull;
-    const float4 *cull_node;      // [n_nodes] per leaf: the union of its references' boxes
+    const float4 *cull_node;      // [n_nodes] the union of the boxes of the node's subtree
 };
 int num_persistent_variants();
 
@@ -150,8 +150,11 @@ int num_wf_variants();
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
 // cull boxes of this render's camera for the nrefs leaf references (+ 3 padding boxes)
-// and the per-leaf unions (node_boxes[n_nodes]; inner nodes: the whole plane)
-int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *node_boxes, hipStream_t st);
+// and their unions per subtree (node_boxes[n_nodes]): leaves first, then the inner
+// nodes level by level from the deepest (levels: inner node ids grouped by depth,
+// level_off[i] = {offset, count} of level i, deepest first)
+int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *node_boxes, const uint32_t *levels,
+                    const uint32_t (*level_off)[2], int nlevels, hipStream_t st);
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks);
 void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks);
 // HIP events bracketing every trace launch (start, stop), recorded on the launch

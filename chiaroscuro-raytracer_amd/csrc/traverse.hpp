@@ -163,13 +163,14 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // per scalar load and tests a triangle only if some lane is inside its box; a divergent
 // lane reads its box (16 B) and, inside, the record (48 B).
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false, bool CULL = false>
+          bool UL2 = false, int CULL = 0>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr) {
-    static_assert(!CULL || (BF && SC && PF == 1 && !FULL && !UL2), "cull: lean BF + SC builds");
+    static_assert(!CULL || (BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "cull: lean BF + SC builds");
+    static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -222,6 +223,10 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         return k;
     };
     uint2 nd;
+    // CULL >= 2: a fetched node whose subtree box excludes the sample is treated as an
+    // empty leaf -- none of its triangles can accept, so the traversal would leave it
+    // without a hit and with tmax = its interval's end, which is exactly this state
+    bool culled = false;
     if (FAT) { // two levels per dependent load: a node's record carries its children's
         uint4 f0, f1;
         auto fetch = [&](uint32_t node) {
@@ -231,16 +236,22 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             } else {
                 load_fat<SC>(S, node, f0, f1);
             }
+            nd = make_uint2(f0.x, f0.y);
+            if (CULL >= 2) {
+                const float4 b = load_box<SC>(cull_node, node);
+                if (!(csx >= b.x && csx <= b.y && csy >= b.z && csy <= b.w)) {
+                    culled = true;
+                    nd = make_uint2(0xffffffffu, 3u); // an empty leaf no real leaf shares `first` with
+                }
+            }
         };
         fetch(T.node);
-        nd = make_uint2(f0.x, f0.y);
         while ((nd.y & 3u) != 3u) {
             const uint32_t k = step(nd);
             nd = k ? make_uint2(f1.x, f1.y) : make_uint2(f0.z, f0.w);
             if ((nd.y & 3u) == 3u) break;
             step(nd);
             fetch(T.node);
-            nd = make_uint2(f0.x, f0.y);
         }
     } else {
         nd = load_node<SC>(S, T.node);
@@ -255,8 +266,8 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
     }
     const uint32_t first = nd.x;
     uint32_t count = nd.y >> 2;
-    bool lin = true; // CULL: the sample lies in the leaf's box (the union of its references')
-    if (CULL) {
+    bool lin = !culled; // CULL: the sample lies in the leaf's box (the union of its references')
+    if (CULL && !culled) {
         const float4 lb = load_box<SC>(cull_node, T.node);
         lin = csx >= lb.x && csx <= lb.y && csy >= lb.z && csy <= lb.w;
     }

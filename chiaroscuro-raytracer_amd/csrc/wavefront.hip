@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // CULL (camera instantiation only): triangle tests skipped by the screen-space cull
 // boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, bool CULL = false>
+          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
@@ -583,13 +583,13 @@ struct WfVariant {
     void (*closest)(RenderArgs, WfArgs, uint32_t);
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd, tile;
-    bool cull; // the camera trace reads the cull boxes
+    int cull; // the camera trace reads the cull boxes (1: references and leaves, 2: also subtrees)
 };
 #define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU)                                                         \
     {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
      wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>,                                         \
      wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>, R, W, TL, CU}
-#define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, false)
+#define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, 0)
 #define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
 #define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
 #define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
@@ -605,11 +605,13 @@ static const WfVariant kWf[] = {
     CR_WF_T(4, 8, true, false, true, 1, true, 0),
     // 13: build 9 with a uniform leaf's records two per scalar-load wait
     CR_WF_U(8, 8, true, false, true, 1, true, 0, true),
-    // 14: build 9 whose camera trace skips triangle tests by the screen-space cull boxes
-    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, true)};
+    // 14: build 9 whose camera trace skips triangle tests and leaves by the screen-space cull boxes
+    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 1),
+    // 15: 14 that also skips the subtrees whose box excludes the sample (checked at each fat-record fetch)
+    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 2)};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
-                                   false};
+                                   0};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
 bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].cull; }
@@ -654,10 +656,25 @@ __global__ void __launch_bounds__(256) cam_cull_leaf_kernel(RenderArgs A, const 
     node_boxes[i] = u;
 }
 
-int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *node_boxes, hipStream_t st) {
+// One thread per inner node of one level: the union of its children's boxes.
+__global__ void __launch_bounds__(256) cam_cull_inner_kernel(RenderArgs A, const uint32_t *ids, uint32_t n,
+                                                             float4 *node_boxes) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = ids[i], ch = A.S.nodes[id].y >> 2;
+    const float4 a = node_boxes[ch], b = node_boxes[ch + 1];
+    node_boxes[id] = make_float4(fminf(a.x, b.x), fmaxf(a.y, b.y), fminf(a.z, b.z), fmaxf(a.w, b.w));
+}
+
+int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *node_boxes, const uint32_t *levels,
+                    const uint32_t (*level_off)[2], int nlevels, hipStream_t st) {
     const uint32_t n = nrefs + 3;
     hipLaunchKernelGGL(cam_cull_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, nrefs, boxes);
     hipLaunchKernelGGL(cam_cull_leaf_kernel, dim3((A.S.n_nodes + 255) / 256), dim3(256), 0, st, A, boxes, node_boxes);
+    for (int l = 0; l < nlevels; l++)
+        if (level_off[l][1])
+            hipLaunchKernelGGL(cam_cull_inner_kernel, dim3((level_off[l][1] + 255) / 256), dim3(256), 0, st, A,
+                               levels + level_off[l][0], level_off[l][1], node_boxes);
     return (int)hipGetLastError();
 }
 

@@ -55,7 +55,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
     wave-uniform nodes / leaves) renders the same bits."""
@@ -79,16 +79,17 @@ CULL_CAMS = {
 }
 
 
+@pytest.mark.parametrize("variant", [14, 15])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell", "cornell_box"])
-def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_mm, cfg):
-    """Trace build 14: the camera-ray trace skips Moller-Trumbore tests by per-render
-    screen-space cull boxes (camcull.hpp).  A skipped test could not have accepted, so
+def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_mm, cfg, variant):
+    """Trace builds 14 / 15: the camera-ray trace skips Moller-Trumbore tests, leaves
+    (14) and subtrees (15) by per-render screen-space cull boxes (camcull.hpp).  A skipped test could not have accepted, so
     the image and the per-query counters equal the oracle's -- at the config's camera,
     at an edge-on camera close to a surface and at a wide-angle camera inside the scene;
     also tile-split (global pixel coordinates) and at an odd frame size."""
     pair = {"sponza": sponza, "nanobox": nanobox, "cornell": cornell, "cornell_box": cornell_mm}[cfg]
     pair.dev.set_option("kernel", 2)
-    pair.dev.set_option("variant", 14)
+    pair.dev.set_option("variant", variant)
     try:
         for ci, spec in enumerate(CULL_CAMS[cfg]):
             for (x, y, s) in ((96, 54, 4), (61, 37, 3)):
