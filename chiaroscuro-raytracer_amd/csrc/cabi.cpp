@@ -4,6 +4,7 @@
 // kernels.hip header), the progressive accumulator, the counters and the
 // per-launch HIP events.  No C++ exception or hipError_t crosses the ABI.
 #include "ctx.hpp"
+#include "planecull.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -476,6 +477,26 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         q[1] = make_float4(p[3] - p[0], p[4] - p[1], p[5] - p[2], 0.f);
         q[2] = make_float4(p[6] - p[0], p[7] - p[1], p[8] - p[2], 0.f);
     }
+    // plane records (planecull.hpp) for rays of unit length inside the padded box: Db bounds
+    // every coordinate of an origin (a hit point + 0.001 * normal) or vertex, Tb the segment
+    std::vector<float4> planes((size_t)d->n_refs + 3, make_float4(0.f, 0.f, 0.f, 0.f));
+    {
+        double Db = 0.0, diag = 0.0;
+        for (int i = 0; i < 3; i++) {
+            Db = std::max(Db, std::max(std::fabs((double)d->box_min[i]), std::fabs((double)d->box_max[i])));
+            diag += ((double)d->box_max[i] - d->box_min[i]) * ((double)d->box_max[i] - d->box_min[i]);
+        }
+        Db += 1.0;
+        const double Tb = 1.01 * std::sqrt(diag) + 2.0;
+        for (uint32_t r = 0; r < d->n_refs; r++) {
+            const float4 *q = recs.data() + (size_t)cr::REC_STRIDE * r;
+            const float a[3] = {q[0].x, q[0].y, q[0].z}, e1[3] = {q[1].x, q[1].y, q[1].z},
+                        e2[3] = {q[2].x, q[2].y, q[2].z};
+            float o[4];
+            cr::plane_record(a, e1, e2, Db, Tb, o);
+            planes[r] = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
     std::vector<float4> tri((size_t)3 * nt), mn(nt), mkd(nt), mke(nt);
     std::vector<float2> muv((size_t)3 * nt);
     for (uint32_t t = 0; t < nt; t++) {
@@ -549,7 +570,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         free_scene(c);
         return rc;
     }
-    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, tri, &c->S.tri)) ||
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
         (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels))) {

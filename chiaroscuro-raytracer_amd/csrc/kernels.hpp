@@ -29,6 +29,9 @@ struct DevScene {
     // {e2 = C-A, 0} -- bitwise what the reference computes per test.  (A 40-B SoA
     // split measured 15% slower: three cache lines per test instead of one or two.)
     const float4 *recs;
+    // one per leaf reference (+ 3 padding): the triangle's plane scaled by its rounding
+    // margin (planecull.hpp), the exact pre-test of the secondary / shadow traces
+    const float4 *planes;
     const float4 *tri;    // 3 per triangle: A, B, C
     const float4 *mat_n;  // normal, w = emissive flag bits
     const float4 *mat_kd; // Kd, w = texture index (int bits, -1 none)

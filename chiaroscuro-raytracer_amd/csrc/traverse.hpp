@@ -157,13 +157,17 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // cr_upload_scene numbers breadth-first -- are read from the block's LDS copy
 // `tile` instead of through the vector-memory address path.
 // UL2 (BF + SC builds): a uniform leaf's records come two per scalar-load wait.
+// PLANE (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a triangle
+// test runs only when the lane's segment [0, tmax) is not proven to stay on one side of
+// the triangle's plane (S.planes, planecull.hpp) -- on one side the test cannot accept.
+// A uniform leaf reads four plane records per scalar load.
 // CULL (camera rays; BF + SC, PF 1): a triangle test runs only when the lane's sample
 // position (csx, csy) lies in the reference's cull box (camcull.hpp) -- outside it the
 // test cannot accept, so skipping it changes nothing.  A uniform leaf reads four boxes
 // per scalar load and tests a triangle only if some lane is inside its box; a divergent
 // lane reads its box (16 B) and, inside, the record (48 B).
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false, int CULL = 0>
+          bool UL2 = false, int CULL = 0, int PLANE = 0>
 __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
@@ -171,6 +175,7 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
                                                const float4 *cull_node = nullptr) {
     static_assert(!CULL || (BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "cull: lean BF + SC builds");
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
+    static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -344,7 +349,28 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             found = found || acc;
             return true;
         };
-        if (CULL) {
+        // PLANE: the test of a triangle every active lane's segment stays on one side of is skipped
+        auto needs = [&](float nx, float ny, float nz, float w) -> bool {
+            const float s0 = dot(mk(nx, ny, nz), o) - w;
+            const float s1 = s0 + T.tmax * dot(mk(nx, ny, nz), d);
+            return !((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f));
+        };
+        if (PLANE == 1) {
+            const float4 *pb = S.planes + uf;
+            bool go = true;
+            for (uint32_t j = 0; j < uc && go; j += 4) {
+                const cr_v16f pl = sload_box4(pb + j);
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    if (j + k >= uc) break;
+                    if (__ballot(needs(pl[4 * k], pl[4 * k + 1], pl[4 * k + 2], pl[4 * k + 3])) &&
+                        !utest(sload_rec(base + (size_t)REC_STRIDE * (j + k)), j + k)) {
+                        go = false;
+                        break;
+                    }
+                }
+            }
+        } else if (CULL) {
             const float4 *cb = cull + uf;
             for (uint32_t j = 0; j < uc && __ballot(lin); j += 4) {
                 const cr_v16f bx = sload_box4(cb + j);
@@ -383,6 +409,17 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             if (j + 2 < count) ra = load_rec(S, first + j + 2);
             tally_tri(first + j + 1);
             if (!test(rb)) break;
+        }
+    } else if (PLANE) { // plane records pipelined one ahead; a record only when the plane is crossed
+        float4 np = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (count) np = S.planes[first];
+        for (uint32_t j = 0; j < count; j++) {
+            const float4 pl = np;
+            if (j + 1 < count) np = S.planes[first + j + 1];
+            const float s0 = dot(mk(pl.x, pl.y, pl.z), o) - pl.w;
+            const float s1 = s0 + T.tmax * dot(mk(pl.x, pl.y, pl.z), d);
+            if (!((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f)))
+                if (!test(load_rec(S, first + j))) break;
         }
     } else if (CULL) { // boxes pipelined one ahead; a record only for a sample inside its box
         if (!lin) count = 0;

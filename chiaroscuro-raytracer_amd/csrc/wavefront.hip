@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // CULL (camera instantiation only): triangle tests skipped by the screen-space cull
 // boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0>
+          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0, int PLANE = 0>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL>(
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE>(
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
                 A.cull_node);
             if (r != busy_st) {
@@ -585,10 +585,11 @@ struct WfVariant {
     int ring, waves_per_simd, tile;
     int cull; // the camera trace reads the cull boxes (1: references and leaves, 2: also subtrees)
 };
-#define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU)                                                         \
+#define CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, PL)                                                     \
     {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
-     wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>,                                         \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2>, R, W, TL, CU}
+     wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>,                                  \
+     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>, R, W, TL, CU}
+#define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU) CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, 0)
 #define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, 0)
 #define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
 #define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
@@ -608,7 +609,10 @@ static const WfVariant kWf[] = {
     // 14: build 9 whose camera trace skips triangle tests and leaves by the screen-space cull boxes
     CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 1),
     // 15: 14 that also skips the subtrees whose box excludes the sample (checked at each fat-record fetch)
-    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 2)};
+    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 2),
+    // 16: 15 whose secondary closest and shadow traces skip the tests their segment cannot
+    // pass by the triangle's plane (planecull.hpp)
+    CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1)};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
                                    0};

@@ -55,7 +55,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
     wave-uniform nodes / leaves) renders the same bits."""
@@ -79,11 +79,13 @@ CULL_CAMS = {
 }
 
 
-@pytest.mark.parametrize("variant", [14, 15])
+@pytest.mark.parametrize("variant", [14, 15, 16])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell", "cornell_box"])
 def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_mm, cfg, variant):
-    """Trace builds 14 / 15: the camera-ray trace skips Moller-Trumbore tests, leaves
-    (14) and subtrees (15) by per-render screen-space cull boxes (camcull.hpp).  A skipped test could not have accepted, so
+    """Trace builds 14 / 15 / 16: the camera-ray trace skips Moller-Trumbore tests, leaves
+    (14) and subtrees (15) by per-render screen-space cull boxes (camcull.hpp); build 16's
+    secondary and shadow traces also skip the tests whose segment stays on one side of the
+    triangle's plane (planecull.hpp).  A skipped test could not have accepted, so
     the image and the per-query counters equal the oracle's -- at the config's camera,
     at an edge-on camera close to a surface and at a wide-angle camera inside the scene;
     also tile-split (global pixel coordinates) and at an odd frame size."""
