@@ -17,8 +17,10 @@ touches the GPU) and exits with their status; under torch.distributed.run the
 world size must equal N.
 
 Prints ONE JSON line on rank 0 with the contract fields plus
-  "roofline"      the dominant kernel (the camera-ray trace) against the ceiling
-                  that binds it: instruction issue (VALU / SALU wave-instructions
+  "roofline"      the dominant kernel (the trace kind with the most standalone
+                  time per pass: the shadow-ray trace on the sponza stand-in since
+                  the camera-ray cull of build 15) against the ceiling that binds
+                  it: instruction issue (VALU / SALU wave-instructions
                   per launch from the committed rocprofv3 PMC summary
                   profiles/pmc_issue_<config>.json, divided by this run's live
                   HIP-event launch time, against 1024 SIMDs x 2.4 GHz / 2 cycles
@@ -115,7 +117,7 @@ def cpu_baseline(pair_tris, textures, info, leaf, cam, xres, yres, spp, k, seed,
                       "1 thread: %s" % (threads, s_all, s_1t)}
 
 
-def issue_roofline(dom, iss, views, issue, pass_view):
+def issue_roofline(dom, iss, views, issue, pass_view, kind):
     """Roofline of the dominant trace kernel against the ceiling that binds it.
 
     The trace kernels' working set (kd nodes + triangle records, ~65 MB for the
@@ -132,8 +134,11 @@ def issue_roofline(dom, iss, views, issue, pass_view):
     bytes_view = {"algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"], "achieved_gbs": dom["achieved"],
                   "frac_of_hbm": round(dom["achieved"] / HBM_PEAK_GBS, 4),
                   "frac_of_l2_aggregate": round(dom["achieved"] / L2_PEAK_GBS, 4),
-                  "fabric_bytes_per_launch": dom["traffic"]}
-    base = {"kernel": dom["kernel"] + " (camera-ray kd traversal, wavefront.hip)",
+                  "fabric_bytes_per_launch": dom["traffic"],
+                  "note": "SURVEY 8d bytes of the reference algorithm's work (counting build); the cull boxes of the "
+                          "camera trace skip most of that work exactly, so its rate is an effective one"}
+    what = {"camera": "camera-ray", "closest": "secondary closest-hit", "shadow": "shadow-ray"}[kind]
+    base = {"kernel": dom["kernel"] + " (%s kd traversal, wavefront.hip)" % what,
             "avg_launch_ms": dom["avg_launch_ms"], "launches": dom["launches"],
             "rocprof_avg_launch_ms": dom["rocprof_avg_launch_ms"], "bytes": bytes_view,
             "other_traces": {k: v for k, v in views.items() if v is not None and v is not dom},
@@ -149,12 +154,14 @@ def issue_roofline(dom, iss, views, issue, pass_view):
             "salu": {"achieved": round(salu, 2), "peak": SALU_PEAK_GIPS, "frac": round(salu / SALU_PEAK_GIPS, 4),
                      "insts_per_launch": iss["salu_insts_per_launch"]},
             "ta_busy_profiled": iss.get("ta_busy"),
+            "ta_note": "vector-memory address path busy fraction from the rocprofv3 PMC pass (no live "
+                       "counterpart): the trace kernels are co-limited by issue and the address path",
             "hbm_bytes": {"frac": bytes_view["frac_of_hbm"], "note": "algorithmic bytes, cache resident"}}
     bound = max(("valu", "salu"), key=lambda k: ceil[k]["frac"])
     b = ceil[bound]
     return {"bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": "Gwave-inst/s", "frac": b["frac"],
             "traffic": dom["traffic"], "ceilings": ceil,
-            "profile": "profiles/pmc_issue_<config>.json kinds[camera] (%s)" % iss["kernel"], **base}
+            "profile": "profiles/pmc_issue_<config>.json kinds[%s] (%s)" % (kind, iss["kernel"]), **base}
 
 
 def spawn_ranks(n: int) -> int:
@@ -337,9 +344,8 @@ def main():
                      "algorithmic_bytes": int(pass_bytes), "achieved": round(pass_gbs, 2),
                      "traffic": pj.get("hbm_bytes_per_launch") if pj else None}
         if wavefront:
-            # Dominant kernel: the camera-ray trace (wf_trace, generation-1 closest queries), the
-            # largest launch of a pass and the only trace that never runs beside another one.
-            # Algorithmic bytes (8 per inner node, 8 per leaf, 40 per triangle test)
+            # Per trace kind (camera = generation-1 closest queries, closest = later generations,
+            # shadow): algorithmic bytes (8 per inner node, 8 per leaf, 40 per triangle test)
             # per kind from the counting pass; launch times from HIP event pairs around every
             # launch of the timed passes, on the launch's stream.
             def kind_view(kind):
@@ -369,9 +375,24 @@ def main():
                         issue = ij.get("kinds")
                 except Exception:
                     issue = None
-            dom = views["camera"] or views["closest"]
-            dom_kind = "camera" if views["camera"] else "closest"
-            roofline = issue_roofline(dom, (issue or {}).get(dom_kind), views, issue, pass_view)
+            # Dominant kernel: the trace kind with the most kernel time per pass.  Closest traces of
+            # generation >= 2 run beside a shadow trace on a second stream, so their live event
+            # times include the other kernel's share of the GPU; the ranking therefore uses the
+            # standalone durations of the committed PMC pass (rocprofv3 serializes kernels there)
+            # when it exists, else the live times.  (Sponza stand-in, build 15: shadow 249 ms,
+            # camera 70, closest 69 per pass -- the shadow trace, whose live time equals its
+            # standalone one: it is launched first and owns the GPU.)
+            def per_pass_ms(kind):
+                k = (issue or {}).get(kind)
+                if k and k.get("avg_launch_ms") and k.get("dispatches"):
+                    return k["avg_launch_ms"] * k["dispatches"], "standalone"
+                v = views.get(kind)
+                return ((v["avg_launch_ms"] * v["launches"] / max(totals["launches"], 1)) if v else 0.0), "live"
+            ranked = {k: per_pass_ms(k) for k in ("camera", "closest", "shadow") if views.get(k)}
+            dom_kind = max(ranked, key=lambda k: ranked[k][0])
+            dom = views[dom_kind]
+            roofline = issue_roofline(dom, (issue or {}).get(dom_kind), views, issue, pass_view, dom_kind)
+            roofline["dominant_by"] = {k: {"ms_per_pass": round(v[0], 3), "from": v[1]} for k, v in ranked.items()}
         else:
             roofline = {"bound": "hbm", "achieved": round(pass_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(pass_gbs / HBM_PEAK_GBS, 5), "traffic": pass_view["traffic"],
