@@ -234,7 +234,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         // computed inside the timed region of every render
         const bool cull = wf && !c->full_counters && cr::wf_variant_culls(A.variant) && c->n_refs > 0;
         if (cull) {
-            if (int r = grow(c, &c->d_cull, c->cull_bytes, 16 * ((size_t)c->n_refs + 3))) return r;
+            if (int r = grow(c, &c->d_cull, c->cull_bytes, 16 * ((size_t)c->n_refs + 4))) return r;
             if (int r = grow(c, &c->d_cull_node, c->cull_node_bytes, 16 * (size_t)c->S.n_nodes)) return r;
         }
         A.cull = cull ? (const float4 *)c->d_cull : nullptr;

@@ -42,7 +42,7 @@ struct cr_ctx {
     size_t accum_elems = 0;
     void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
     size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
-    void *d_cull = nullptr;  // camera-ray cull boxes, one per leaf reference (+ 3), per render
+    void *d_cull = nullptr;  // camera-ray cull boxes, one per leaf reference (+ 4), per render
     size_t cull_bytes = 0;
     void *d_cull_node = nullptr; // ... their per-leaf unions, one per kd node
     size_t cull_node_bytes = 0;

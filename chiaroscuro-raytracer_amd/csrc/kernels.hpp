@@ -152,7 +152,7 @@ struct WfStreams {
 int num_wf_variants();
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
-// cull boxes of this render's camera for the nrefs leaf references (+ 3 padding boxes)
+// cull boxes of this render's camera for the nrefs leaf references (+ 4 padding boxes)
 // and their unions per subtree (node_boxes[n_nodes]): leaves first, then the inner
 // nodes level by level from the deepest (levels: inner node ids grouped by depth,
 // level_off[i] = {offset, count} of level i, deepest first)

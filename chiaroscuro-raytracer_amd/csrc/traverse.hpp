@@ -120,6 +120,17 @@ __device__ __forceinline__ float4 sload_box(const float4 *p) {
     asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
     return make_float4(r[0], r[1], r[2], r[3]);
 }
+// A fat record and its subtree box (CULL >= 2) under one scalar-load wait.
+__device__ __forceinline__ void sload_fat_box(const uint4 *p, const float4 *q, uint4 &a, uint4 &b, float4 &box) {
+    cr_v8u r;
+    cr_v4f x;
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(r), "=s"(x)
+                 : "s"(p), "s"(q));
+    a = make_uint4(r[0], r[1], r[2], r[3]);
+    b = make_uint4(r[4], r[5], r[6], r[7]);
+    box = make_float4(x[0], x[1], x[2], x[3]);
+}
 template <bool SC> __device__ __forceinline__ float4 load_box(const float4 *b, uint32_t i) {
     if (SC && wave_uniform(i)) return sload_box(b + __builtin_amdgcn_readfirstlane(i));
     return b[i];
@@ -238,6 +249,23 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             if (TILE && node < (uint32_t)TILE) {
                 f0 = tile[2 * node];
                 f1 = tile[2 * node + 1];
+            } else if (CULL >= 2) { // the record and the subtree box, loads issued together
+                float4 b;
+                if (SC && wave_uniform(node)) {
+                    const uint32_t un = __builtin_amdgcn_readfirstlane(node);
+                    sload_fat_box(S.fat + 2u * un, cull_node + un, f0, f1, b);
+                } else {
+                    const uint4 *p = (const uint4 *)((const char *)S.fat + node * 32u);
+                    f0 = p[0];
+                    f1 = p[1];
+                    b = cull_node[node];
+                }
+                nd = make_uint2(f0.x, f0.y);
+                if (!(csx >= b.x && csx <= b.y && csy >= b.z && csy <= b.w)) {
+                    culled = true;
+                    nd = make_uint2(0xffffffffu, 3u); // an empty leaf no real leaf shares `first` with
+                }
+                return;
             } else {
                 load_fat<SC>(S, node, f0, f1);
             }

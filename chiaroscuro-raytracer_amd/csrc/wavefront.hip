@@ -622,11 +622,11 @@ bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && 
 
 // One thread per leaf reference: its cull box for this render's camera (camcull.hpp),
 // from the record's A, e1, e2 -- the floats the triangle test uses.  Boxes
-// nrefs..nrefs+2 are empty (the four-box scalar loads of uniform leaves read past a
-// leaf's end).  Samples lie in [0, xres] x [0, yres] (global pixel coordinates).
+// nrefs..nrefs+3 are empty (the four-box scalar loads of uniform leaves read past a
+// leaf's end, also from an empty leaf's `first` == nrefs).  Samples lie in [0, xres] x [0, yres] (global pixel coordinates).
 __global__ void __launch_bounds__(256) cam_cull_kernel(RenderArgs A, uint32_t nrefs, float4 *boxes) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrefs + 3) return;
+    if (r >= nrefs + 4) return;
     if (r >= nrefs) {
         boxes[r] = make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
         return;
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(256) cam_cull_inner_kernel(RenderArgs A, const
 
 int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *node_boxes, const uint32_t *levels,
                     const uint32_t (*level_off)[2], int nlevels, hipStream_t st) {
-    const uint32_t n = nrefs + 3;
+    const uint32_t n = nrefs + 4;
     hipLaunchKernelGGL(cam_cull_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, nrefs, boxes);
     hipLaunchKernelGGL(cam_cull_leaf_kernel, dim3((A.S.n_nodes + 255) / 256), dim3(256), 0, st, A, boxes, node_boxes);
     for (int l = 0; l < nlevels; l++)
