@@ -109,7 +109,7 @@ _host = None
 
 # Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
-               "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_intersect",
+               "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_tile_origin", "cr_intersect",
                "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize",
                "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap",
                "cr_comm_unique_id", "cr_comm_init", "cr_comm_destroy", "cr_render_dist_device",
@@ -165,6 +165,8 @@ def libs():
     _sig(hip, "cr_render_tiles_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
     _sig(hip, "cr_blend_tiles_device", C.c_int, [P, C.POINTER(CrRenderParams), P, P, P])
     _sig(hip, "cr_tiles_for_rank", C.c_uint32, [C.POINTER(CrRenderParams), C.c_uint32])
+    _sig(hip, "cr_tile_origin", C.c_int, [C.POINTER(CrRenderParams), C.c_uint32, C.c_uint32,
+                                          C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)])
     _sig(hip, "cr_intersect", C.c_int, [P, C.c_uint32, FP, FP, UP, UP, FP, FP])
     _sig(hip, "cr_intersect_shadow", C.c_int, [P, C.c_uint32, FP, FP, FP, UP, UP])
     _sig(hip, "cr_get_counters", C.c_int, [P, C.POINTER(CrCounters)])
@@ -427,6 +429,13 @@ class Device:
     @staticmethod
     def tiles_for_rank(p: CrRenderParams, rank: int) -> int:
         return int(libs()[0].cr_tiles_for_rank(C.byref(p), int(rank)))
+
+    @staticmethod
+    def tile_origin(p: CrRenderParams, rank: int, local: int):
+        x0, y0 = C.c_uint32(0), C.c_uint32(0)
+        if libs()[0].cr_tile_origin(C.byref(p), int(rank), int(local), C.byref(x0), C.byref(y0)):
+            raise ValueError("cr_tile_origin: no such tile")
+        return x0.value, y0.value
 
     def intersect(self, orig: np.ndarray, dirs: np.ndarray) -> dict:
         orig = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)

@@ -1,7 +1,8 @@
 """Multi-GPU frame protocol: tile split + one gather per layer.
 
-The frame is cut into `tile`×`tile` tiles, row-major; tile t belongs to rank
-t % nranks.  Each rank renders its tiles' batch means into a compact
+The frame is cut into `tile`×`tile` tiles, numbered in row-major slots (each row
+rotated by its index when nranks > 1, TileLayout.tile_origin); slot s belongs to
+rank s % nranks.  Each rank renders its tiles' batch means into a compact
 [ntiles_r][tile][tile][3] buffer (cr_render_tiles_device), rank 0 gathers the
 buffers over torch.distributed (RCCL over xGMI on GPUs, gloo in the CPU tests)
 and unpermutes + blends the layer on the device (cr_blend_tiles_device):
@@ -43,9 +44,14 @@ class TileLayout:
         return self.tiles_for_rank(0)
 
     def tile_origin(self, rank: int, local: int):
-        """Pixel origin (x0, y0) of the rank's local tile `local`."""
-        t = rank + local * self.nranks
-        return (t % self.tiles_x) * self.tile, (t // self.tiles_x) * self.tile
+        """Pixel origin (x0, y0) of the rank's local tile `local` (== cr_tile_origin):
+        slot s = rank + local * nranks; with nranks > 1 tile row s // tiles_x is rotated
+        by its index, so a rank's tiles cycle through every column class."""
+        s = rank + local * self.nranks
+        row, c = divmod(s, self.tiles_x)
+        if self.nranks > 1:
+            c = (c + row) % self.tiles_x
+        return c * self.tile, row * self.tile
 
 
 class DistributedFrame:

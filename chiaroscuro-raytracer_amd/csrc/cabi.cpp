@@ -589,6 +589,14 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     return CR_OK;
 }
 
+int cr_tile_origin(const cr_render_params *p, uint32_t rank, uint32_t local, uint32_t *x0, uint32_t *y0) {
+    if (!p || !x0 || !y0 || local >= cr_tiles_for_rank(p, rank)) return CR_E_INVALID;
+    const uint32_t T = tile_of(p), tx = (p->xres + T - 1) / T, s = rank + local * p->nranks;
+    *x0 = cr::tile_slot_column(s, tx, p->nranks) * T;
+    *y0 = s / tx * T;
+    return CR_OK;
+}
+
 uint32_t cr_tiles_for_rank(const cr_render_params *p, uint32_t rank) {
     if (!p || p->nranks == 0 || rank >= p->nranks || p->xres == 0 || p->yres == 0) return 0;
     const uint32_t T = tile_of(p);

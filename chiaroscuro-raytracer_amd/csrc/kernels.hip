@@ -225,8 +225,8 @@ __global__ void __launch_bounds__(256) blend_tiles_kernel(BlendArgs B) {
     if (i >= B.xres * B.yres) return;
     const uint32_t y = i / B.xres, x = i - y * B.xres;
     const uint32_t T = B.tile;
-    const uint32_t gt = (y / T) * B.tiles_x + (x / T);
-    const uint32_t r = gt % B.nranks, lt = gt / B.nranks;
+    const uint32_t s = tile_slot(x / T, y / T, B.tiles_x, B.nranks);
+    const uint32_t r = s % B.nranks, lt = s / B.nranks;
     const size_t src = ((size_t)r * B.max_tiles + lt) * T * T + (y % T) * T + (x % T);
     const f3 m = mk(B.gathered[3 * src], B.gathered[3 * src + 1], B.gathered[3 * src + 2]);
     float *o = B.frame + 3 * (size_t)i;

@@ -22,6 +22,22 @@ enum { CTR_TRACE = 24 };
 // bytes for 1-channel images; the pad makes that read defined (zeros).
 __host__ __device__ inline uint64_t tex_pad(int w, int nc) { return (uint64_t)(w + 1) * nc + 4; }
 
+// Tile split (nranks > 1): slot s = rank + lt * nranks of the frame's row-major tile
+// slots belongs to the rank; slot s is tile (column (s % tiles_x + row) % tiles_x, row
+// s / tiles_x) -- each tile row rotated by its index, so a rank's tiles cycle through
+// every column class mod nranks instead of forming vertical stripes (cost varies
+// across the frame: plain t % nranks left 2.6% imbalance at 8 ranks).  One rank: the
+// identity.  cr_tile_origin and chiaroscuro_amd.tiles.TileLayout are the same map.
+__host__ __device__ inline uint32_t tile_slot_column(uint32_t slot, uint32_t tiles_x, uint32_t nranks) {
+    const uint32_t row = slot / tiles_x, c = slot - row * tiles_x;
+    return nranks > 1 ? (c + row % tiles_x) % tiles_x : c;
+}
+// ... and back: the slot of tile (column gx, row gy)
+__host__ __device__ inline uint32_t tile_slot(uint32_t gx, uint32_t gy, uint32_t tiles_x, uint32_t nranks) {
+    const uint32_t c = nranks > 1 ? (gx + tiles_x - gy % tiles_x) % tiles_x : gx;
+    return gy * tiles_x + c;
+}
+
 struct DevScene {
     const uint2 *nodes;   // {split bits | first ref, axis | child<<2 ; leaf: 3 | count<<2}
     const uint4 *fat;     // 2 per node: {self, child 0}, {child 1, 0, 0} (two-level descent)

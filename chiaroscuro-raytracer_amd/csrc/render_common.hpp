@@ -151,12 +151,12 @@ __device__ __forceinline__ f3 camera_dir(const RenderArgs &A, uint32_t x, uint32
     return add(add(lu, muls(dx, sx)), muls(dy, sy));
 }
 
-// Work item -> pixel: this rank's tiles (tile t -> rank t % nranks), row-major in a tile.
+// Work item -> pixel: this rank's tiles (slot s -> rank s % nranks), row-major in a tile.
 __device__ __forceinline__ bool item_pixel(const RenderArgs &A, uint32_t item, uint32_t &x, uint32_t &y) {
     const uint32_t T = A.tile, TT = A.tile * A.tile;
     const uint32_t lt = item / TT, o = item - lt * TT;
-    const uint32_t gt = A.rank + lt * A.nranks;
-    const uint32_t gy = gt / A.tiles_x, gx = gt - gy * A.tiles_x;
+    const uint32_t s = A.rank + lt * A.nranks;
+    const uint32_t gy = s / A.tiles_x, gx = tile_slot_column(s, A.tiles_x, A.nranks);
     x = gx * T + (o % T);
     y = gy * T + (o / T);
     return x < A.xres && y < A.yres;

@@ -117,7 +117,7 @@ typedef struct {
     float background[3];  /* Scene::background */
     uint32_t seed;        /* RNG stream key (DESIGN.md "RNG") */
     uint32_t layer;       /* progressive layer L >= 1 (src/rayTracer.cpp:18-33) */
-    uint32_t rank, nranks;/* tile partition: tile t belongs to rank t % nranks */
+    uint32_t rank, nranks;/* tile partition: tile slot s belongs to rank s % nranks (cr_tile_origin) */
     uint32_t tile;        /* tile edge in pixels, 0 -> 32 */
 } cr_render_params;
 
@@ -205,6 +205,10 @@ int cr_render_tiles_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_pa
 int cr_blend_tiles_device(cr_ctx *ctx, const cr_render_params *p, const float *d_gathered, float *d_frame,
                           void *stream);
 uint32_t cr_tiles_for_rank(const cr_render_params *p, uint32_t rank);
+/* Pixel origin of rank's local tile `local` (slot rank + local * nranks of the frame's
+ * row-major tile slots; with nranks > 1 each tile row is rotated by its index, so a
+ * rank's tiles spread over every column class). */
+int cr_tile_origin(const cr_render_params *p, uint32_t rank, uint32_t local, uint32_t *x0, uint32_t *y0);
 
 /* Ray queries (host arrays). dir need not be normalised (the reference does not). */
 int cr_intersect(cr_ctx *ctx, uint32_t n, const float *orig, const float *dir, uint32_t *hit, uint32_t *tri,
@@ -241,7 +245,7 @@ int cr_synchronize(cr_ctx *ctx);
 
 /* ---------------------------------------------------------- multi-GPU --
  * The frame split of SURVEY §8e behind the C-ABI, RCCL inside (csrc/group.cpp):
- * tile t of the frame belongs to rank t % nranks; each rank renders its tiles'
+ * tile slot s of the frame belongs to rank s % nranks (cr_tile_origin); each rank renders its tiles'
  * batch means, the root (rank 0) gathers them over RCCL (xGMI) and blends the
  * layer into its frame ((old*(L-1) + mean)/L, src/rayTracer.cpp:64) on the
  * device.  The image equals the single-GPU render bit for bit. */

@@ -158,9 +158,16 @@ def test_tile_layout_matches_cabi(ca):
         counts = [ca.Device.tiles_for_rank(p, r) for r in range(n)]
         assert counts == [lay.tiles_for_rank(r) for r in range(n)]
         assert sum(counts) == lay.ntiles
-        # every tile owned exactly once
+        # every tile owned exactly once, at the same origin in the C-ABI and in TileLayout
         owned = sorted(r + lt * n for r in range(n) for lt in range(lay.tiles_for_rank(r)))
         assert owned == list(range(lay.ntiles))
+        origins = [lay.tile_origin(r, lt) for r in range(n) for lt in range(lay.tiles_for_rank(r))]
+        assert origins == [ca.Device.tile_origin(p, r, lt) for r in range(n) for lt in range(lay.tiles_for_rank(r))]
+        assert sorted(origins) == sorted((tx * t, ty * t) for ty in range(lay.tiles_y) for tx in range(lay.tiles_x))
+    # rows rotated by their index (n > 1): rank 0 of 8 at 1920 px sees every column class mod 8
+    lay = TileLayout(1920, 1080, 8, 32)
+    cols = {lay.tile_origin(0, lt)[0] // 32 % 8 for lt in range(lay.tiles_for_rank(0))}
+    assert cols == set(range(8))
 
 
 def test_gloo_tile_gather_matches_single_process():
