@@ -688,15 +688,6 @@ void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &bloc
     blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)v.waves_per_simd; // 4 SIMDs, 4 waves/block
 }
 
-// Length of a queue (device counter -> host; waits for the stream).
-static uint32_t queue_len(const uint32_t *dcount, hipStream_t st, int &err) {
-    uint32_t n = 0;
-    if ((err = (int)hipMemcpyAsync(&n, dcount, sizeof(n), hipMemcpyDeviceToHost, st)) ||
-        (err = (int)hipStreamSynchronize(st)))
-        return 0;
-    return n;
-}
-
 // Sorts the queue of n rays whose keys wf_shade wrote into key / perm set `set`
 // (0 shadow, 1 closest); returns the permutation for the trace kernel (nullptr:
 // trace in queue order).

@@ -116,6 +116,38 @@ def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_
         pair.dev.set_option("variant", -1)
 
 
+@pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell"])
+def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg):
+    """The default build (camera-ray cull boxes) at 12 random cameras per scene: eyes
+    inside and outside the scene box, any view direction and up vector, fields of view
+    from 6 to 170 degrees, odd frame sizes -- every image and per-query counter equal to
+    the oracle's.  Seeded, so a failure reproduces."""
+    pair = {"sponza": sponza, "nanobox": nanobox, "cornell": cornell}[cfg]
+    rng = np.random.default_rng({"sponza": 11, "nanobox": 12, "cornell": 13}[cfg])
+    lo, hi = np.array(list(pair.desc.box_min), np.float64), np.array(list(pair.desc.box_max), np.float64)
+    ext = hi - lo
+    pair.dev.set_option("kernel", 2)
+    pair.dev.set_option("counters", 0)
+    try:
+        for i in range(12):
+            eye = lo + ext * rng.uniform(-0.2 if i % 3 == 0 else 0.05, 1.2 if i % 3 == 0 else 0.95, 3)
+            look = lo + ext * rng.uniform(0, 1, 3)
+            up = rng.normal(size=3)
+            yview = float(rng.uniform(0.1, 20.0) if i % 4 == 3 else rng.uniform(0.3, 2.5))
+            x, y = int(rng.integers(17, 70)), int(rng.integers(11, 50))
+            cam = ca.camera(eye, look, up, yview, x, y)
+            g = pair.dev.render(cam, ca.render_params(x, y, 2, 6, 0xC41A05C0 + i))
+            lc = pair.dev.counters()
+            o, oc = pair.oracle.render(cam.as_array(), x, y, 2, 6, 0xC41A05C0 + i)
+            what = "%s fuzz camera %d (%dx%d, yview %.2f)" % (cfg, i, x, y, yview)
+            assert pair.dev.trace_stats()["camera"]["launches"] == 1, what  # the culling camera trace ran
+            assert_bitwise(g, o, what)
+            assert {k: lc[k] for k in ("closest", "shadow", "hit", "texhit", "paths")} == \
+                {k: oc[k] for k in ("closest", "shadow", "hit", "texhit", "paths")}, what
+    finally:
+        pair.dev.set_option("counters", 1)
+
+
 @pytest.mark.parametrize("lanes", [1, 2])
 def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
     """Two chunks in flight (wf_lanes 2: the frame's paths split in two, the second
