@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--spp", type=int, default=0)
     ap.add_argument("--nranks", default="1,2,4,8")
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE", help="cr_set_option (experiments)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -34,6 +35,9 @@ def main():
     dev = ca.Device(0)
     dev.upload(ca.KDTree(m, sc).describe())
     dev.set_option("counters", 0)
+    for kv in args.opt:
+        key, val = kv.split("=", 1)
+        dev.set_option(key, int(val, 0))
     spp = args.spp or i["samples"]
     cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], i["xres"], i["yres"])
     res = {}
