@@ -115,6 +115,9 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 15 = 14 that also skips every fetched subtree whose box excludes the sample:
     // camera trace 118 -> 70 ms, 488 -> 439 ms per pass
     A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 15 : 0);
+    A.eye_on_split = 0;
+    for (int a = 0; a < 3; a++)
+        if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
@@ -583,6 +586,10 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     c->S.bmax = make_float3(d->box_max[0], d->box_max[1], d->box_max[2]);
     c->stack_depth = d->max_depth > 0 ? d->max_depth : 1;
     c->n_refs = d->n_refs;
+    for (int a = 0; a < 3; a++) c->splits[a].clear();
+    for (uint32_t i = 0; i < NN; i++)
+        if (d->nodes[i].axis < 3) c->splits[d->nodes[i].axis].push_back(d->nodes[i].split);
+    for (int a = 0; a < 3; a++) std::sort(c->splits[a].begin(), c->splits[a].end());
     c->d_levels = levels_dev;
     c->levels = std::move(level_off);
     c->has_scene = true;

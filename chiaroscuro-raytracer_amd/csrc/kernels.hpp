@@ -98,6 +98,9 @@ struct RenderArgs {
     // accept a camera ray of this camera (null: no cull)
     const float4 *cull;
     const float4 *cull_node;      // [n_nodes] the union of the boxes of the node's subtree
+    // 1: the eye lies exactly on a split plane of its axis, where camera rays may disagree on
+    // a node's near child -- the packet camera trace (build 18) is not used for this render
+    int eye_on_split;
 };
 int num_persistent_variants();
 

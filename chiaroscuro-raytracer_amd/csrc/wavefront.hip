@@ -577,6 +577,178 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
     flush_tallies(A, tl);
 }
 
+// ------------------------------------------------- packet camera-ray trace --
+// Trace build 18's camera-ray trace.  A wave's 64 camera rays -- 64 samples of one
+// pixel, taken in lock-step -- traverse the kd tree as ONE packet: the node is
+// wave-uniform (scalar loads, uniform control flow), and every lane keeps its own
+// interval and an active flag.  All camera rays start at the eye, so a node's near
+// child (kdtree.cpp:262, `belowFirst` from the origin's side of the split) is the same
+// for every lane; the packet visits nodes depth-first, near child first, and a lane
+// is active exactly at the nodes its own traversal (kdtree.cpp:248-281) visits, with
+// the same interval and in the same order:
+//   near only   (tsplit >= tmax or < 0)  near with [tmin, tmax]
+//   far only    (tsplit <= tmin)         far  with [tmin, tmax]
+//   both                                 near with [tmin, tsplit], then far with [tsplit, tmax]
+// A lane that finds a hit in a leaf is done (the first leaf with a hit ends its query),
+// the others go on; cull boxes (camcull.hpp) deactivate a lane for a subtree / leaf /
+// triangle exactly as in build 15.  The stack: per entry the node (per wave, LDS) and
+// each lane's interval or an inactive mark (the ring [R][thread] in LDS, deeper entries
+// spilled to gstack as in trav_round).  If the eye lies exactly on a split plane of its
+// axis the near child could differ between lanes; the host then uses build 15's camera
+// trace for that render (RenderArgs::eye_on_split).
+enum : uint32_t { PACKET_DEPTH = 256 }; // >= the deepest tree cr_upload_scene accepts
+template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W, uint32_t g) {
+    extern __shared__ uint2 ring_lds[]; // [R][blockDim] per-lane {tmin, tmax} bits of an entry
+    __shared__ uint32_t pnode[4][PACKET_DEPTH];
+    const DevScene &S = A.S;
+    const uint32_t tid = threadIdx.x, wv = tid >> 6, lane = tid & 63u, bdim = blockDim.x;
+    const uint32_t gid = blockIdx.x * bdim + tid, gstride = W.gstride;
+    uint2 *ring = ring_lds, *gstk = W.gstack;
+    const uint32_t n = *cnt_closest(W, 1);
+    uint32_t *work = work_closest(W, 1);
+    const float4 *rays = W.ray[1];
+    uint4 *hits = W.hit[1];
+    const f3 eye = mk(A.cam[0], A.cam[1], A.cam[2]); // every camera ray's origin (wf_camera)
+    const float4 *cnode = A.cull_node, *cref = A.cull;
+    const uint32_t INACTIVE = 0xffffffffu;
+    Ctr c = {};
+    uint32_t issued = 0;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(work, 64u);
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+        if (base >= n) break;
+        const uint32_t idx = base + lane;
+        bool live = idx < n;
+        f3 d = mk(0.f, 0.f, 1.f);
+        float tmin = 0.f, tmax = 0.f, csx = 0.f, csy = 0.f;
+        if (live) {
+            const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
+            d = ld3(r1);
+            if (__float_as_uint(r0.w) == NO_PATH) { // partial-tile slot: no query
+                hits[idx] = make_uint4(0u, 0u, 0u, 0u);
+                live = false;
+            } else {
+                const float2 q = W.cxy[idx];
+                csx = q.x;
+                csy = q.y;
+                issued++;
+                Trav T;
+                if (trav_begin(S, eye, d, false, 0.f, T)) {
+                    tmin = T.tmin;
+                    tmax = T.tmax;
+                } else {
+                    hits[idx] = make_uint4(0u, 0u, 0u, 0u);
+                    live = false;
+                }
+            }
+        }
+        bool active = live, found = false;
+        uint32_t tri = 0;
+        float bx = 0.f, by = 0.f;
+        uint32_t cn = 0, sp = 0, nl = 0; // wave-uniform
+        auto inb = [&](float4 b) { return csx >= b.x && csx <= b.y && csy >= b.z && csy <= b.w; };
+        auto push = [&](uint32_t node, bool act, float t0, float t1) {
+            const uint32_t slot = (sp & (R - 1)) * bdim + tid;
+            if (nl == (uint32_t)R) gstk[(size_t)(sp - R) * gstride + gid] = ring[slot]; // spill the oldest
+            else nl++;
+            ring[slot] = act ? make_uint2(__float_as_uint(t0), __float_as_uint(t1)) : make_uint2(INACTIVE, INACTIVE);
+            pnode[wv][sp] = node;
+            sp++;
+        };
+        // the next entry with an active lane; false: the packet's traversal is over
+        auto pop = [&]() -> bool {
+            while (sp) {
+                sp--;
+                uint2 e;
+                if (nl) {
+                    e = ring[(sp & (R - 1)) * bdim + tid];
+                    nl--;
+                } else {
+                    e = gstk[(size_t)sp * gstride + gid];
+                }
+                cn = __builtin_amdgcn_readfirstlane(pnode[wv][sp]);
+                active = live && !found && !(e.x == INACTIVE && e.y == INACTIVE);
+                tmin = __uint_as_float(e.x);
+                tmax = __uint_as_float(e.y);
+                if (__ballot(active)) return true;
+            }
+            return false;
+        };
+        // a leaf reached with record nd; boxed: its box was read with its fat record
+        auto leaf = [&](uint2 nd, bool boxed) {
+            const uint32_t first = nd.x, count = nd.y >> 2;
+            if (!boxed) active = active && inb(sload_box(cnode + cn));
+            if (!__ballot(active) || !count) return;
+            const float4 *rb = S.recs + (size_t)REC_STRIDE * first;
+            for (uint32_t j = 0; j < count; j += 4) {
+                const cr_v16f bb = sload_box4(cref + first + j);
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    if (j + k >= count) break;
+                    const bool in = active && csx >= bb[4 * k] && csx <= bb[4 * k + 1] && csy >= bb[4 * k + 2] &&
+                                    csy <= bb[4 * k + 3];
+                    if (!__ballot(in)) continue;
+                    const TriRec r = sload_rec(rb + (size_t)REC_STRIDE * (j + k));
+                    float ux, uy, t;
+                    const bool acc = in && tri_test_wave(eye, d, r, tmax, ux, uy, t);
+                    bx = acc ? ux : bx;
+                    by = acc ? uy : by;
+                    tmax = acc ? t : tmax;
+                    tri = acc ? rec_id(r) : tri;
+                    found = found || acc;
+                }
+            }
+        };
+        bool go = __ballot(active) != 0;
+        while (go) {
+            // fetch node cn: its record, both children's records and its subtree box
+            uint4 f0, f1;
+            float4 b;
+            sload_fat_box(S.fat + 2u * cn, cnode + cn, f0, f1, b);
+            active = active && inb(b);
+            uint2 nd = make_uint2(f0.x, f0.y);
+            bool popit = true;
+            // one fat record serves two levels: the fetched node (lvl 0, its children's
+            // records at hand) and the child stepped into (lvl 1, its children fetched next)
+            for (uint32_t lvl = 0;; lvl++) {
+                if (!__ballot(active)) break;
+                if ((nd.y & 3u) == 3u) {
+                    leaf(nd, lvl == 0);
+                    break;
+                }
+                const uint32_t a = nd.y & 3u, child = nd.y >> 2;
+                const float split = __uint_as_float(nd.x);
+                const float oa = comp(eye, a), da = comp(d, a);
+                const float tsplit = split_distance(split, oa, da);
+                const uint32_t below = oa < split ? 1u : 0u; // uniform: the eye is not on the plane
+                const bool near_only = tsplit >= tmax || tsplit < 0;
+                const bool far_only = !near_only && tsplit <= tmin;
+                const bool both = !near_only && !far_only;
+                const uint32_t nearc = child + (1u - below), farc = child + below;
+                if (!__ballot(active && !far_only)) { // every active lane goes to the far child only
+                    cn = farc;
+                } else {
+                    if (__ballot(active && !near_only)) push(farc, active && !near_only, both ? tsplit : tmin, tmax);
+                    active = active && !far_only;
+                    tmax = both ? tsplit : tmax;
+                    cn = nearc;
+                }
+                if (lvl == 1) { // cn's record is not in this fat record: fetch it
+                    popit = false;
+                    break;
+                }
+                nd = cn == child ? make_uint2(f0.z, f0.w) : make_uint2(f1.x, f1.y);
+            }
+            go = popit ? pop() : true;
+        }
+        if (live) hits[idx] = found ? make_uint4(tri, __float_as_uint(bx), __float_as_uint(by), 1u)
+                                    : make_uint4(0u, 0u, 0u, 0u);
+    }
+    c.closest = issued;
+    flush_counters(A.counters, c, 0u);
+}
+
 // --------------------------------------------------------------- launch --
 struct WfVariant {
     void (*camera)(RenderArgs, WfArgs, uint32_t);
@@ -612,12 +784,21 @@ static const WfVariant kWf[] = {
     CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 2),
     // 16: 15 whose secondary closest and shadow traces skip the tests their segment cannot
     // pass by the triangle's plane (planecull.hpp)
-    CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1)};
+    CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1),
+    // 17: 15 whose camera rays traverse as one packet per wave (wf_trace_packet)
+    {wf_trace_packet<8>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2}};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
                                    0};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
+// The camera-ray trace of a variant; the packet trace (build 17) needs a near child common
+// to all camera rays, which an eye lying exactly on a split plane breaks: build 15's then.
+static void (*camera_kernel(const WfVariant &v, const RenderArgs &A))(RenderArgs, WfArgs, uint32_t) {
+    return (v.camera == (void (*)(RenderArgs, WfArgs, uint32_t))wf_trace_packet<8> && A.eye_on_split) ? kWf[15].camera
+                                                                                                       : v.camera;
+}
 bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].cull; }
 
 // One thread per leaf reference: its cull box for this render's camera (camcull.hpp),
@@ -770,7 +951,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         Wc.gstack = gstack;
         const int kind = g == 1 ? TK_CAMERA : TK_CLOSEST;
         if ((err = trace_event(te, s, kind, true))) return;
-        hipLaunchKernelGGL(g == 1 ? v.camera : v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
+        hipLaunchKernelGGL(g == 1 ? camera_kernel(v, A) : v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
         err = trace_event(te, s, kind, false);
     };
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
@@ -844,7 +1025,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         Wc.gstack = gstack;
         const int kind = g == 1 ? TK_CAMERA : TK_CLOSEST;
         if ((err = trace_event(te, s, kind, true))) return;
-        hipLaunchKernelGGL(g == 1 ? v.camera : v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
+        hipLaunchKernelGGL(g == 1 ? camera_kernel(v, A) : v.closest, dim3(blocks), dim3(blk), lds, s, A, Wc, g);
         err = trace_event(te, s, kind, false);
     };
     auto shade = [&](WfLane &ln, Run &r) { // wf_shade(g), then the queue lengths to the host, async

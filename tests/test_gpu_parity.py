@@ -55,7 +55,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
     wave-uniform nodes / leaves) renders the same bits."""
@@ -79,7 +79,7 @@ CULL_CAMS = {
 }
 
 
-@pytest.mark.parametrize("variant", [14, 15, 16])
+@pytest.mark.parametrize("variant", [14, 15, 16, 17])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell", "cornell_box"])
 def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_mm, cfg, variant):
     """Trace builds 14 / 15 / 16: the camera-ray trace skips Moller-Trumbore tests, leaves
@@ -116,8 +116,9 @@ def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_
         pair.dev.set_option("variant", -1)
 
 
+@pytest.mark.parametrize("variant", [15, 17])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell"])
-def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg):
+def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg, variant):
     """The default build (camera-ray cull boxes) at 12 random cameras per scene: eyes
     inside and outside the scene box, any view direction and up vector, fields of view
     from 6 to 170 degrees, odd frame sizes -- every image and per-query counter equal to
@@ -128,6 +129,7 @@ def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg):
     ext = hi - lo
     pair.dev.set_option("kernel", 2)
     pair.dev.set_option("counters", 0)
+    pair.dev.set_option("variant", variant)
     try:
         for i in range(12):
             eye = lo + ext * rng.uniform(-0.2 if i % 3 == 0 else 0.05, 1.2 if i % 3 == 0 else 0.95, 3)
@@ -146,6 +148,35 @@ def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg):
                 {k: oc[k] for k in ("closest", "shadow", "hit", "texhit", "paths")}, what
     finally:
         pair.dev.set_option("counters", 1)
+        pair.dev.set_option("variant", -1)
+
+
+def test_packet_camera_eye_on_split_plane(ca, sponza, cornell):
+    """Build 17's packet camera trace needs every camera ray to agree on a node's near
+    child; an eye exactly on a split plane breaks that (kdtree.cpp:262 then decides by
+    the ray's direction), and the render falls back to build 15's camera trace.  Eyes
+    placed exactly on split planes of each axis render bit-exact either way."""
+    for pair in (sponza, cornell):
+        e = pair.kd.export()
+        lo, hi = np.array(list(pair.desc.box_min)), np.array(list(pair.desc.box_max))
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("counters", 0)
+        pair.dev.set_option("variant", 17)
+        try:
+            for axis in range(3):
+                inner = np.nonzero((e["is_leaf"] == 0) & (e["axis"] == axis))[0]
+                split = float(e["split"][inner[len(inner) // 2]])
+                eye = (lo + hi) / 2
+                eye[axis] = split
+                look = eye + np.array([0.31, -0.2, 0.93]) * (hi - lo).max()
+                cam = ca.camera(eye.astype(np.float32), look, (0, 1, 0), 1.4, 48, 40)
+                assert cam.as_array()[axis] == np.float32(split)
+                g = pair.dev.render(cam, ca.render_params(48, 40, 2, 6, 77 + axis))
+                o, _ = pair.oracle.render(cam.as_array(), 48, 40, 2, 6, 77 + axis)
+                assert_bitwise(g, o, "eye on a split plane of axis %d" % axis)
+        finally:
+            pair.dev.set_option("counters", 1)
+            pair.dev.set_option("variant", -1)
 
 
 @pytest.mark.parametrize("lanes", [1, 2])
