@@ -113,8 +113,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 14 = 9 whose camera-ray trace skips triangle tests (and whole leaves) outside their
     // screen-space cull boxes (camcull.hpp): camera trace 193 -> 119 ms, 565 -> 489 ms per pass;
     // 15 = 14 that also skips every fetched subtree whose box excludes the sample:
-    // camera trace 118 -> 70 ms, 488 -> 439 ms per pass
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 15 : 0);
+    // camera trace 118 -> 70 ms, 488 -> 439 ms per pass;
+    // 17 = 15 whose camera rays traverse one packet (one pixel's 64 samples) per wave:
+    // 429.3 vs 435.1 ms per pass (2 interleaved rounds), 416.5 vs 423.1 ms with wf_xcd 7
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 17 : 0);
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
@@ -211,6 +213,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.world_keys = nworld <= (1ull << 32) ? c->wf_world_keys : 0;
                 W.world_bits = c->wf_world_bits;
                 W.tail_min = c->wf_tail_min;
+                W.xcd = c->wf_xcd;
                 if (c->wf_sort) {
                     for (int q = 0; q < 2; q++)
                         for (int i = 0; i < 2; i++) {
@@ -822,6 +825,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
     else if (!std::strcmp(key, "wf_sort_lib") && (v == 0 || v == 1)) c->wf_sort_lib = (int)v;
     else if (!std::strcmp(key, "wf_lanes") && (v == 1 || v == 2)) c->wf_lanes = (int)v;
+    else if (!std::strcmp(key, "wf_xcd") && v >= 0 && v <= 7) c->wf_xcd = (uint32_t)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);

@@ -83,6 +83,10 @@ struct cr_ctx {
     uint64_t sample_buf = cr::SAMPLE_BUF_BYTES;
     int wf_sort_lib = 0;              // 1: hipcub's radix sort for the queues (comparison)
     int wf_lanes = 1;                 // wavefront chunks in flight at once (1 or 2)
+    // XCD-partitioned queues (WfArgs::xcd bits: 1 shadow, 2 secondary closest, 4 camera rays);
+    // sponza 1080p x 128 spp, 2 interleaved rounds: 0 / 1 / 3 / 7 -> 435.1 / 432.4 / 431.4 / 423.1 ms
+    // per pass (build 15); build 17: 429.3 -> 416.5 ms with 7
+    uint32_t wf_xcd = 7;
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

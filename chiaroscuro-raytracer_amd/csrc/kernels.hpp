@@ -123,8 +123,11 @@ int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t s
 // work items [w0, w0 + P) advance one bounce per generation through separate
 // kernels (camera, closest trace, shade, shadow trace, bounce) that exchange
 // rays through queues in HBM.
-// counters: closest count [g], shadow count [WF_G+g], work [2*WF_G+g], [3*WF_G+g]; g <= K + 1 <= 65
-enum : uint32_t { WF_G = 66, WF_CNT = 4 * WF_G };
+// counters: closest count [g], shadow count [WF_G+g], work [2*WF_G+g], [3*WF_G+g]; g <= K + 1 <= 65;
+// then the per-XCD work counters of the partitioned queues (WfArgs::xcd), WF_XSTRIDE apart
+// (one 64-B line each): closest [WF_XBASE + (g*8 + x)*WF_XSTRIDE], shadow after WF_G*8 of those
+enum : uint32_t { WF_G = 66, WF_XCDS = 8, WF_XSTRIDE = 16, WF_XBASE = 4 * WF_G,
+                  WF_CNT = WF_XBASE + 2 * WF_G * WF_XCDS * WF_XSTRIDE };
 enum { WF_STATE = 5 };            // path-state float4 slots per path
 struct WfArgs {
     uint32_t P;       // path slots of this chunk
@@ -159,6 +162,11 @@ struct WfArgs {
     uint32_t world_bits; // bits per axis of the origin's Morton code
     uint32_t tail_min;   // a closest queue shorter than this hands the rest of the chunk to wf_tail (0: never)
     float2 *cxy;         // [P] screen position (sx, sy) of path p's camera sample (written when A.cull)
+    // XCD-partitioned queues (bit 0 shadow, bit 1 secondary closest, bit 2 camera rays): the
+    // queue's (sorted) order is cut into WF_XCDS contiguous ranges and a block of XCD
+    // blockIdx % WF_XCDS (the dispatcher's round-robin) takes rays from its own range first,
+    // then from the others' -- each XCD's L2 then holds the data of one region of key space
+    uint32_t xcd;
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

@@ -200,21 +200,36 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
     const uint32_t busy_st = SHADOW ? ST_SHADOW : ST_CLOSEST;
     const uint32_t refill = SHADOW ? A.refill_shadow : (g == 1 ? A.refill_camera : A.refill);
+    // XCD partition (WfArgs::xcd): wave-uniform range `part`, WF_XCDS ranges tried in turn
+    const bool xp = (W.xcd >> (SHADOW ? 0 : (g == 1 ? 2 : 1))) & 1u;
+    uint32_t part = blockIdx.x % WF_XCDS, tried = 0;
+    uint32_t *xwork = W.cnt + WF_XBASE + ((SHADOW ? WF_G : 0u) + g) * WF_XCDS * WF_XSTRIDE;
     for (;;) {
         const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
         if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= refill)) {
             for (;;) { // refill; a ray culled by the root box is answered at once and refetched
                 const uint64_t m = __ballot(state == ST_NEED_WORK);
                 if (!m) break;
+                if (xp && tried == WF_XCDS) { // every range drained
+                    if (state == ST_NEED_WORK) state = ST_DONE;
+                    break;
+                }
                 const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1u;
+                const uint32_t lo = xp ? (uint32_t)((uint64_t)n * part / WF_XCDS) : 0u;
+                const uint32_t hi = xp ? (uint32_t)((uint64_t)n * (part + 1) / WF_XCDS) : n;
                 uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(work, (uint32_t)__popcll(m));
-                base = __shfl(base, (int)leader, 64);
+                if (lane == leader)
+                    base = atomicAdd(xp ? xwork + part * WF_XSTRIDE : work, (uint32_t)__popcll(m));
+                base = lo + __shfl(base, (int)leader, 64);
+                if (xp && base + (uint32_t)__popcll(m) > hi) { // this range is drained: the next one
+                    part = (part + 1) % WF_XCDS;
+                    tried++;
+                }
                 if (state == ST_NEED_WORK) {
                     idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (idx >= n) {
-                        state = ST_DONE;
+                    if (idx >= hi) {
+                        if (!xp) state = ST_DONE; // else: stays idle and takes a ray of the next range
                     } else {
                         if (W.order) idx = W.order[idx]; // sorted queue: results still go to slot idx
                         const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
@@ -613,13 +628,23 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
     const uint32_t INACTIVE = 0xffffffffu;
     Ctr c = {};
     uint32_t issued = 0;
+    // XCD partition (WfArgs::xcd bit 2), as in wf_trace: own range first, then the others
+    const bool xp = (W.xcd >> 2) & 1u;
+    uint32_t part = blockIdx.x % WF_XCDS, tried = 0;
+    uint32_t *xwork = W.cnt + WF_XBASE + g * WF_XCDS * WF_XSTRIDE;
     for (;;) {
+        const uint32_t lo = xp ? (uint32_t)((uint64_t)n * part / WF_XCDS) : 0u;
+        const uint32_t hi = xp ? (uint32_t)((uint64_t)n * (part + 1) / WF_XCDS) : n;
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(work, 64u);
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
-        if (base >= n) break;
+        if (lane == 0) base = atomicAdd(xp ? xwork + part * WF_XSTRIDE : work, 64u);
+        base = __builtin_amdgcn_readfirstlane(lo + __shfl(base, 0, 64));
+        if (base >= hi) {
+            if (!xp || ++tried == WF_XCDS) break;
+            part = (part + 1) % WF_XCDS;
+            continue;
+        }
         const uint32_t idx = base + lane;
-        bool live = idx < n;
+        bool live = idx < hi;
         f3 d = mk(0.f, 0.f, 1.f);
         float tmin = 0.f, tmax = 0.f, csx = 0.f, csy = 0.f;
         if (live) {

@@ -26,7 +26,7 @@ def main():
             n = r["Kernel_Name"]
             ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
             tot += ms
-            if "wf_trace<false" in n:
+            if "wf_trace<false" in n or "wf_trace_packet" in n:  # the packet build's camera trace
                 g += 1
                 k = "g%d closest" % g
                 counting |= re.search(r"wf_trace<false, true,", n) is not None

@@ -51,12 +51,15 @@ def main(src, dst, spp=128):
     kinds = {}
     for k, v in out.items():
         m = re.search(r"wf_trace<([^>]*)>", k)
-        if not m:
+        if "wf_trace_packet" in k:  # the packet build's camera-ray trace (lean)
+            kind = "camera"
+        elif not m:
             continue
-        a = [x.strip() for x in m.group(1).split(",")]
-        if a[1] != "false":
-            continue
-        kind = "shadow" if a[0] == "true" else ("camera" if len(a) > 8 and a[8] == "true" else "closest")
+        else:
+            a = [x.strip() for x in m.group(1).split(",")]
+            if a[1] != "false":
+                continue
+            kind = "shadow" if a[0] == "true" else ("camera" if len(a) > 8 and a[8] == "true" else "closest")
         d = v["dispatches"]
         kinds[kind] = {"kernel": k, "valu_issue_busy": v["valu_issue_busy"], "salu_issue_busy": v["salu_issue_busy"],
                        "ta_busy": v.get("ta_busy"), "shader_clock_ghz": v["shader_clock_ghz"],

@@ -80,11 +80,13 @@ def main():
     trace = {}
     for n, e in summary.items():
         m = re.search(r"wf_trace<([^>]*)>", n)
-        if not m or "fabric_bytes_total" not in e:
+        packet = "wf_trace_packet" in n  # the packet build's camera-ray trace (lean)
+        if not (m or packet) or "fabric_bytes_total" not in e:
             continue
-        targs = [a.strip() for a in m.group(1).split(",")]  # SHADOW, FULL, R, MINW, SC, FD, FAT, PF, CAM[, BF]
+        # SHADOW, FULL, R, MINW, SC, FD, FAT, PF, CAM[, BF]
+        targs = ["false", "false"] if packet else [a.strip() for a in m.group(1).split(",")]
         if targs[1] == "false":  # lean builds (the timed ones)
-            cam = len(targs) > 8 and targs[8] == "true"
+            cam = packet or (len(targs) > 8 and targs[8] == "true")
             kind = "shadow" if targs[0] == "true" else ("camera" if cam else "closest")
             trace[kind] = {
                 "kernel": n, "calls": e["calls"], "avg_ns": e["avg_ns"],

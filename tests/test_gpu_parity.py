@@ -55,6 +55,29 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
+@pytest.mark.parametrize("xcd,sort_min,variant", [(7, 0, 15), (7, 1 << 20, 15), (1, 0, 15), (2, 0, 15), (4, 0, 17),
+                                                   (7, 0, 17)])
+def test_wavefront_xcd_partition_bitexact(ca, sponza, nanobox, xcd, sort_min, variant):
+    """XCD-partitioned queues (wf_xcd bits: shadow, secondary closest, camera) change which
+    block traces which ray only: every ray is traced once, whatever the queue length
+    (queues shorter than the eight ranges included: the tiny frame)."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4)), (nanobox, (3, 2, 1))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("variant", variant)
+        pair.dev.set_option("wf_xcd", xcd)
+        pair.dev.set_option("wf_sort_min", sort_min)
+        pair.dev.set_option("wf_tail_min", 0)  # every generation through wf_trace
+        try:
+            g, gc, o, oc = _render_both(ca, pair, x, y, s)
+        finally:
+            pair.dev.set_option("wf_xcd", 0)
+            pair.dev.set_option("wf_tail_min", 1 << 20)
+            pair.dev.set_option("variant", -1)
+            pair.dev.set_option("wf_sort_min", 1 << 20)
+        assert_bitwise(g, o, "xcd-partitioned wavefront %d %dx%dx%d" % (xcd, x, y, s))
+        assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
