@@ -56,7 +56,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
 
 
 @pytest.mark.parametrize("xcd,sort_min,variant", [(7, 0, 15), (7, 1 << 20, 15), (1, 0, 15), (2, 0, 15), (4, 0, 17),
-                                                   (7, 0, 17)])
+                                                   (7, 0, 17), (0, 0, 17)])
 def test_wavefront_xcd_partition_bitexact(ca, sponza, nanobox, xcd, sort_min, variant):
     """XCD-partitioned queues (wf_xcd bits: shadow, secondary closest, camera) change which
     block traces which ray only: every ray is traced once, whatever the queue length
@@ -66,12 +66,10 @@ def test_wavefront_xcd_partition_bitexact(ca, sponza, nanobox, xcd, sort_min, va
         pair.dev.set_option("variant", variant)
         pair.dev.set_option("wf_xcd", xcd)
         pair.dev.set_option("wf_sort_min", sort_min)
-        pair.dev.set_option("wf_tail_min", 0)  # every generation through wf_trace
-        try:
+        try:  # (Pair sets wf_tail_min 0: every generation through wf_trace)
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
         finally:
-            pair.dev.set_option("wf_xcd", 0)
-            pair.dev.set_option("wf_tail_min", 1 << 20)
+            pair.dev.set_option("wf_xcd", 7)
             pair.dev.set_option("variant", -1)
             pair.dev.set_option("wf_sort_min", 1 << 20)
         assert_bitwise(g, o, "xcd-partitioned wavefront %d %dx%dx%d" % (xcd, x, y, s))
