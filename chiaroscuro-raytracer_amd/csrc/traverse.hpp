@@ -131,6 +131,19 @@ __device__ __forceinline__ void sload_fat_box(const uint4 *p, const float4 *q, u
     b = make_uint4(r[4], r[5], r[6], r[7]);
     box = make_float4(x[0], x[1], x[2], x[3]);
 }
+// The same for node n with the byte offsets in SGPRs (s_load's soffset form): no 64-bit
+// address arithmetic on the scalar unit, which bounds the packet trace.
+__device__ __forceinline__ void sload_fat_box_n(const uint4 *fat, const float4 *boxes, uint32_t n, uint4 &a, uint4 &b,
+                                                float4 &box) {
+    cr_v8u r;
+    cr_v4f x;
+    asm volatile("s_load_dwordx8 %0, %2, %4\n\ts_load_dwordx4 %1, %3, %5\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(r), "=s"(x)
+                 : "s"(fat), "s"(boxes), "s"(n * 32u), "s"(n * 16u));
+    a = make_uint4(r[0], r[1], r[2], r[3]);
+    b = make_uint4(r[4], r[5], r[6], r[7]);
+    box = make_float4(x[0], x[1], x[2], x[3]);
+}
 template <bool SC> __device__ __forceinline__ float4 load_box(const float4 *b, uint32_t i) {
     if (SC && wave_uniform(i)) return sload_box(b + __builtin_amdgcn_readfirstlane(i));
     return b[i];

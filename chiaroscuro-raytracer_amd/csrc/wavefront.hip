@@ -200,17 +200,19 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
     const uint32_t busy_st = SHADOW ? ST_SHADOW : ST_CLOSEST;
     const uint32_t refill = SHADOW ? A.refill_shadow : (g == 1 ? A.refill_camera : A.refill);
-    // XCD partition (WfArgs::xcd): wave-uniform range `part`, WF_XCDS ranges tried in turn
-    const bool xp = (W.xcd >> (SHADOW ? 0 : (g == 1 ? 2 : 1))) & 1u;
-    uint32_t part = blockIdx.x % WF_XCDS, tried = 0;
-    uint32_t *xwork = W.cnt + WF_XBASE + ((SHADOW ? WF_G : 0u) + g) * WF_XCDS * WF_XSTRIDE;
+    // XCD partition (WfArgs::xcd): wave-uniform range part = xs % 256, WF_XCDS ranges tried
+    // in turn (xs / 256 of them drained); one register, the rest is derived at refill
+    uint32_t xs = blockIdx.x % WF_XCDS;
     for (;;) {
         const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
         if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= refill)) {
+            const bool xp = (W.xcd >> (SHADOW ? 0 : (g == 1 ? 2 : 1))) & 1u;
+            uint32_t *xwork = W.cnt + WF_XBASE + ((SHADOW ? WF_G : 0u) + g) * WF_XCDS * WF_XSTRIDE;
             for (;;) { // refill; a ray culled by the root box is answered at once and refetched
                 const uint64_t m = __ballot(state == ST_NEED_WORK);
                 if (!m) break;
-                if (xp && tried == WF_XCDS) { // every range drained
+                const uint32_t part = xs & 255u;
+                if (xp && (xs >> 8) == WF_XCDS) { // every range drained
                     if (state == ST_NEED_WORK) state = ST_DONE;
                     break;
                 }
@@ -221,10 +223,8 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                 if (lane == leader)
                     base = atomicAdd(xp ? xwork + part * WF_XSTRIDE : work, (uint32_t)__popcll(m));
                 base = lo + __shfl(base, (int)leader, 64);
-                if (xp && base + (uint32_t)__popcll(m) > hi) { // this range is drained: the next one
-                    part = (part + 1) % WF_XCDS;
-                    tried++;
-                }
+                if (xp && base + (uint32_t)__popcll(m) > hi) // this range is drained: the next one
+                    xs = (xs & ~255u) + 256u + (part + 1) % WF_XCDS;
                 if (state == ST_NEED_WORK) {
                     idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
 }
 
 // ------------------------------------------------- packet camera-ray trace --
-// Trace build 18's camera-ray trace.  A wave's 64 camera rays -- 64 samples of one
+// Trace build 17's camera-ray trace.  A wave's 64 camera rays -- 64 samples of one
 // pixel, taken in lock-step -- traverse the kd tree as ONE packet: the node is
 // wave-uniform (scalar loads, uniform control flow), and every lane keeps its own
 // interval and an active flag.  All camera rays start at the eye, so a node's near
@@ -672,7 +672,8 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
         uint32_t tri = 0;
         float bx = 0.f, by = 0.f;
         uint32_t cn = 0, sp = 0, nl = 0; // wave-uniform
-        auto inb = [&](float4 b) { return csx >= b.x && csx <= b.y && csy >= b.z && csy <= b.w; };
+        // (bitwise &: four compares and three mask ands, no short-circuit branches)
+        auto inb = [&](float4 b) { return (csx >= b.x) & (csx <= b.y) & (csy >= b.z) & (csy <= b.w); };
         auto push = [&](uint32_t node, bool act, float t0, float t1) {
             const uint32_t slot = (sp & (R - 1)) * bdim + tid;
             if (nl == (uint32_t)R) gstk[(size_t)(sp - R) * gstride + gid] = ring[slot]; // spill the oldest
@@ -693,7 +694,7 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
                     e = gstk[(size_t)sp * gstride + gid];
                 }
                 cn = __builtin_amdgcn_readfirstlane(pnode[wv][sp]);
-                active = live && !found && !(e.x == INACTIVE && e.y == INACTIVE);
+                active = live & !found & !((e.x == INACTIVE) & (e.y == INACTIVE));
                 tmin = __uint_as_float(e.x);
                 tmax = __uint_as_float(e.y);
                 if (__ballot(active)) return true;
@@ -703,7 +704,7 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
         // a leaf reached with record nd; boxed: its box was read with its fat record
         auto leaf = [&](uint2 nd, bool boxed) {
             const uint32_t first = nd.x, count = nd.y >> 2;
-            if (!boxed) active = active && inb(sload_box(cnode + cn));
+            if (!boxed) active = active & inb(sload_box(cnode + cn));
             if (!__ballot(active) || !count) return;
             const float4 *rb = S.recs + (size_t)REC_STRIDE * first;
             for (uint32_t j = 0; j < count; j += 4) {
@@ -711,17 +712,17 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) {
                     if (j + k >= count) break;
-                    const bool in = active && csx >= bb[4 * k] && csx <= bb[4 * k + 1] && csy >= bb[4 * k + 2] &&
-                                    csy <= bb[4 * k + 3];
+                    const bool in = active & (csx >= bb[4 * k]) & (csx <= bb[4 * k + 1]) & (csy >= bb[4 * k + 2]) &
+                                    (csy <= bb[4 * k + 3]);
                     if (!__ballot(in)) continue;
                     const TriRec r = sload_rec(rb + (size_t)REC_STRIDE * (j + k));
                     float ux, uy, t;
-                    const bool acc = in && tri_test_wave(eye, d, r, tmax, ux, uy, t);
+                    const bool acc = in & tri_test_wave(eye, d, r, tmax, ux, uy, t);
                     bx = acc ? ux : bx;
                     by = acc ? uy : by;
                     tmax = acc ? t : tmax;
                     tri = acc ? rec_id(r) : tri;
-                    found = found || acc;
+                    found = found | acc;
                 }
             }
         };
@@ -730,8 +731,8 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
             // fetch node cn: its record, both children's records and its subtree box
             uint4 f0, f1;
             float4 b;
-            sload_fat_box(S.fat + 2u * cn, cnode + cn, f0, f1, b);
-            active = active && inb(b);
+            sload_fat_box_n(S.fat, cnode, cn, f0, f1, b);
+            active = active & inb(b);
             uint2 nd = make_uint2(f0.x, f0.y);
             bool popit = true;
             // one fat record serves two levels: the fetched node (lvl 0, its children's
@@ -747,15 +748,18 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
                 const float oa = comp(eye, a), da = comp(d, a);
                 const float tsplit = split_distance(split, oa, da);
                 const uint32_t below = oa < split ? 1u : 0u; // uniform: the eye is not on the plane
-                const bool near_only = tsplit >= tmax || tsplit < 0;
-                const bool far_only = !near_only && tsplit <= tmin;
-                const bool both = !near_only && !far_only;
+                // (bitwise logic on the lane masks: no short-circuit branches)
+                const bool crosses = !(tsplit >= tmax) & !(tsplit < 0.f); // !near_only
+                const bool after = !(tsplit <= tmin);                     // far_only = crosses & !after
+                const bool both = crosses & after;
+                const bool to_near = active & (!crosses | after);
                 const uint32_t nearc = child + (1u - below), farc = child + below;
-                if (!__ballot(active && !far_only)) { // every active lane goes to the far child only
+                if (!__ballot(to_near)) { // every active lane goes to the far child only
                     cn = farc;
                 } else {
-                    if (__ballot(active && !near_only)) push(farc, active && !near_only, both ? tsplit : tmin, tmax);
-                    active = active && !far_only;
+                    const bool to_far = active & crosses;
+                    if (__ballot(to_far)) push(farc, to_far, both ? tsplit : tmin, tmax);
+                    active = to_near;
                     tmax = both ? tsplit : tmax;
                     cn = nearc;
                 }
