@@ -360,6 +360,7 @@ def main():
                 tr = (pj or {}).get("trace", {}).get(kind)
                 return {"kernel": "wf_trace<%s>" % kind, "avg_launch_ms": round(avg_ms, 3), "launches": launches,
                         "algorithmic_bytes_per_launch": int(kb),
+                        "work_per_launch": {w: int(t[w] / max(per_pass, 1e-9)) for w in ("inner", "leaf", "tritest")},
                         "achieved": round(kb / (avg_ms / 1e3) / 1e9, 2) if avg_ms > 0 else 0.0,
                         "traffic": tr["fabric_bytes_per_launch"] if tr else None,
                         "rocprof_avg_launch_ms": round(tr["avg_ns"] / 1e6, 3) if tr else None}

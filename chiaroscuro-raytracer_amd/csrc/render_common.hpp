@@ -102,19 +102,20 @@ __device__ __forceinline__ bool tri_test_wave(f3 o, f3 d, const TriRec &r, float
     const f3 v0 = ld3(r.a), e1 = ld3(r.b), e2 = ld3(r.c);
     const f3 p = cross(d, e2);
     const float aa = dot(e1, p);
-    bool ok = !(aa < 1.19209290e-7F && aa > -1.19209290e-7F);
+    // (bitwise logic on the lane masks: no short-circuit exec branches)
+    bool ok = !((aa < 1.19209290e-7F) & (aa > -1.19209290e-7F));
     if (!__ballot(ok)) return false;
     const float f = rcp_rn_wave(aa);
     const f3 sv = sub(o, v0);
     ux = f * dot(sv, p);
-    ok = ok && !(ux < 0.f || ux > 1.f);
+    ok = ok & !((ux < 0.f) | (ux > 1.f));
     if (!__ballot(ok)) return false;
     const f3 q = cross(sv, e1);
     uy = f * dot(d, q);
-    ok = ok && !(uy < 0.f || uy + ux > 1.f);
+    ok = ok & !((uy < 0.f) | (uy + ux > 1.f));
     if (!__ballot(ok)) return false;
     t = f * dot(e2, q);
-    return ok && t >= 0.f && t < tmax;
+    return ok & (t >= 0.f) & (t < tmax);
 }
 
 // tsplit = (split - oa) / da of a kd node (kdtree.cpp:266), correctly rounded.

@@ -221,10 +221,10 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         const uint32_t below = (oa < split) || (oa == split && da <= 0);
         const uint32_t child = nd.y >> 2;
         uint32_t k;
-        if (BF) {
-            const bool near_only = tsplit >= T.tmax || tsplit < 0;
-            const bool far_only = !near_only && tsplit <= T.tmin;
-            const bool push = !near_only && !far_only;
+        if (BF) { // (bitwise logic on the lane masks: no short-circuit exec branches)
+            const bool near_only = (tsplit >= T.tmax) | (tsplit < 0);
+            const bool far_only = !near_only & (tsplit <= T.tmin);
+            const bool push = !near_only & !far_only;
             k = far_only ? below : 1u - below;
             if (push) {
                 const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
@@ -326,7 +326,8 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         if (shadow && id == exclude) return true;
         if (FULL) c.tritest++;
         float ux, uy, t;
-        if (tri_test(o, d, r, T.tmax, ux, uy, t)) {
+        // BF: the lanes that failed an early test compute on (wave-uniform exits, no exec bookkeeping)
+        if (BF ? tri_test_wave(o, d, r, T.tmax, ux, uy, t) : tri_test(o, d, r, T.tmax, ux, uy, t)) {
             if (shadow) {
                 occluded = true;
                 return false;
@@ -375,19 +376,19 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         auto utest = [&](const TriRec &r, uint32_t j) -> bool {
             tally_tri(uf + j);
             const uint32_t id = rec_id(r);
-            const bool live = !(shadow && (occluded || id == exclude));
+            const bool live = !(shadow & (occluded | (id == exclude)));
             if (FULL) c.tritest += live ? 1u : 0u;
             float ux, uy, t;
-            const bool acc = live && tri_test_wave(o, d, r, T.tmax, ux, uy, t);
+            const bool acc = live & tri_test_wave(o, d, r, T.tmax, ux, uy, t);
             if (shadow) {
-                occluded = occluded || acc;
+                occluded = occluded | acc;
                 return __ballot(!occluded) != 0;
             }
             bx = acc ? ux : bx;
             by = acc ? uy : by;
             T.tmax = acc ? t : T.tmax;
             tri = acc ? id : tri;
-            found = found || acc;
+            found = found | acc;
             return true;
         };
         // PLANE: the test of a triangle every active lane's segment stays on one side of is skipped
