@@ -99,7 +99,7 @@ struct RenderArgs {
     const float4 *cull;
     const float4 *cull_node;      // [n_nodes] the union of the boxes of the node's subtree
     // 1: the eye lies exactly on a split plane of its axis, where camera rays may disagree on
-    // a node's near child -- the packet camera trace (build 18) is not used for this render
+    // a node's near child -- the packet camera trace (build 17) is not used for this render
     int eye_on_split;
 };
 int num_persistent_variants();
