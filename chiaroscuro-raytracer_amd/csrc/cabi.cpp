@@ -115,8 +115,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 15 = 14 that also skips every fetched subtree whose box excludes the sample:
     // camera trace 118 -> 70 ms, 488 -> 439 ms per pass;
     // 17 = 15 whose camera rays traverse one packet (one pixel's 64 samples) per wave:
-    // 429.3 vs 435.1 ms per pass (2 interleaved rounds), 416.5 vs 423.1 ms with wf_xcd 7
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 17 : 0);
+    // 429.3 vs 435.1 ms per pass (2 interleaved rounds), 416.5 vs 423.1 ms with wf_xcd 7;
+    // 18 = 17 with two camera rays per lane (128-ray packets): camera trace 44.1 -> 40.5 ms,
+    // 409.7 -> 406.9 ms per pass
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 18 : 0);
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;

@@ -612,13 +612,25 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
 // axis the near child could differ between lanes; the host then uses build 15's camera
 // trace for that render (RenderArgs::eye_on_split).
 enum : uint32_t { PACKET_DEPTH = 256 }; // >= the deepest tree cr_upload_scene accepts
-template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W, uint32_t g) {
-    extern __shared__ uint2 ring_lds[]; // [R][blockDim] per-lane {tmin, tmax} bits of an entry
+// S rays per lane (S = 2: a packet of 128 rays -- at 128 spp exactly one pixel's samples --
+// so the per-node scalar control work is shared by twice the rays).
+// The stack keeps per ray only the tmax at push (or INACTIVE): on pop a reactivated ray's
+// tmin is its current tmax (the kd stack invariant).  It holds for every
+// ray that pushed the entry: a ray crossing both children went near with tmax = tsplit,
+// and a near subtree finished without a hit (or left by a cull) ends at its interval's
+// end; a ray going to the far child only is parked with tmax = its tmin.  Only active
+// rays' intervals change, so an inactive ray's tmax still holds its value for the next
+// entry it owns.
+template <int R, int S>
+__global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W, uint32_t g) {
+    extern __shared__ uint32_t pring_lds[]; // [R][blockDim][S] per-ray tmax bits at push
     __shared__ uint32_t pnode[4][PACKET_DEPTH];
-    const DevScene &S = A.S;
+    static_assert(S == 1 || S == 2, "one or two rays per lane");
+    const DevScene &Sc = A.S;
     const uint32_t tid = threadIdx.x, wv = tid >> 6, lane = tid & 63u, bdim = blockDim.x;
     const uint32_t gid = blockIdx.x * bdim + tid, gstride = W.gstride;
-    uint2 *ring = ring_lds, *gstk = W.gstack;
+    uint32_t *ring = pring_lds;
+    uint2 *gstk = W.gstack;
     const uint32_t n = *cnt_closest(W, 1);
     uint32_t *work = work_closest(W, 1);
     const float4 *rays = W.ray[1];
@@ -636,131 +648,185 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
         const uint32_t lo = xp ? (uint32_t)((uint64_t)n * part / WF_XCDS) : 0u;
         const uint32_t hi = xp ? (uint32_t)((uint64_t)n * (part + 1) / WF_XCDS) : n;
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(xp ? xwork + part * WF_XSTRIDE : work, 64u);
+        if (lane == 0) base = atomicAdd(xp ? xwork + part * WF_XSTRIDE : work, 64u * S);
         base = __builtin_amdgcn_readfirstlane(lo + __shfl(base, 0, 64));
         if (base >= hi) {
             if (!xp || ++tried == WF_XCDS) break;
             part = (part + 1) % WF_XCDS;
             continue;
         }
-        const uint32_t idx = base + lane;
-        bool live = idx < hi;
-        f3 d = mk(0.f, 0.f, 1.f);
-        float tmin = 0.f, tmax = 0.f, csx = 0.f, csy = 0.f;
-        if (live) {
-            const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
-            d = ld3(r1);
-            if (__float_as_uint(r0.w) == NO_PATH) { // partial-tile slot: no query
-                hits[idx] = make_uint4(0u, 0u, 0u, 0u);
-                live = false;
-            } else {
-                const float2 q = W.cxy[idx];
-                csx = q.x;
-                csy = q.y;
-                issued++;
-                Trav T;
-                if (trav_begin(S, eye, d, false, 0.f, T)) {
-                    tmin = T.tmin;
-                    tmax = T.tmax;
+        uint32_t idx[S];
+        bool live[S], active[S], found[S];
+        f3 d[S];
+        float tmin[S], tmax[S], csx[S], csy[S];
+#pragma unroll
+        for (int s = 0; s < S; s++) {
+            idx[s] = base + 64u * s + lane;
+            live[s] = idx[s] < hi;
+            d[s] = mk(0.f, 0.f, 1.f);
+            tmin[s] = tmax[s] = csx[s] = csy[s] = 0.f;
+            found[s] = false;
+            if (live[s]) {
+                const float4 r0 = rays[2 * (size_t)idx[s]], r1 = rays[2 * (size_t)idx[s] + 1];
+                d[s] = ld3(r1);
+                if (__float_as_uint(r0.w) == NO_PATH) { // partial-tile slot: no query
+                    hits[idx[s]] = make_uint4(0u, 0u, 0u, 0u);
+                    live[s] = false;
                 } else {
-                    hits[idx] = make_uint4(0u, 0u, 0u, 0u);
-                    live = false;
+                    const float2 q = W.cxy[idx[s]];
+                    csx[s] = q.x;
+                    csy[s] = q.y;
+                    issued++;
+                    Trav T;
+                    if (trav_begin(Sc, eye, d[s], false, 0.f, T)) {
+                        tmin[s] = T.tmin;
+                        tmax[s] = T.tmax;
+                    } else {
+                        hits[idx[s]] = make_uint4(0u, 0u, 0u, 0u);
+                        live[s] = false;
+                    }
                 }
             }
+            active[s] = live[s];
         }
-        bool active = live, found = false;
-        uint32_t tri = 0;
-        float bx = 0.f, by = 0.f;
         uint32_t cn = 0, sp = 0, nl = 0; // wave-uniform
+        auto any_active = [&]() {
+            bool a = false;
+#pragma unroll
+            for (int s = 0; s < S; s++) a = a | active[s];
+            return __ballot(a) != 0;
+        };
         // (bitwise &: four compares and three mask ands, no short-circuit branches)
-        auto inb = [&](float4 b) { return (csx >= b.x) & (csx <= b.y) & (csy >= b.z) & (csy <= b.w); };
-        auto push = [&](uint32_t node, bool act, float t0, float t1) {
+        auto inb = [&](int s, float4 b) {
+            return (csx[s] >= b.x) & (csx[s] <= b.y) & (csy[s] >= b.z) & (csy[s] <= b.w);
+        };
+        // push node with, per ray, its tmax (act) or INACTIVE
+        auto push = [&](uint32_t node, const bool (&act)[S]) {
             const uint32_t slot = (sp & (R - 1)) * bdim + tid;
-            if (nl == (uint32_t)R) gstk[(size_t)(sp - R) * gstride + gid] = ring[slot]; // spill the oldest
-            else nl++;
-            ring[slot] = act ? make_uint2(__float_as_uint(t0), __float_as_uint(t1)) : make_uint2(INACTIVE, INACTIVE);
+            if (nl == (uint32_t)R) { // spill the oldest
+                uint2 e = make_uint2(ring[slot * S], S == 2 ? ring[slot * S + (S - 1)] : 0u);
+                gstk[(size_t)(sp - R) * gstride + gid] = e;
+            } else {
+                nl++;
+            }
+#pragma unroll
+            for (int s = 0; s < S; s++) ring[slot * S + s] = act[s] ? __float_as_uint(tmax[s]) : INACTIVE;
             pnode[wv][sp] = node;
             sp++;
         };
-        // the next entry with an active lane; false: the packet's traversal is over
+        // the next entry with an active ray; false: the packet's traversal is over
         auto pop = [&]() -> bool {
             while (sp) {
                 sp--;
-                uint2 e;
+                uint32_t e[S];
                 if (nl) {
-                    e = ring[(sp & (R - 1)) * bdim + tid];
+                    const uint32_t slot = (sp & (R - 1)) * bdim + tid;
+#pragma unroll
+                    for (int s = 0; s < S; s++) e[s] = ring[slot * S + s];
                     nl--;
                 } else {
-                    e = gstk[(size_t)sp * gstride + gid];
+                    const uint2 ge = gstk[(size_t)sp * gstride + gid];
+                    e[0] = ge.x;
+                    if (S == 2) e[S - 1] = ge.y;
                 }
                 cn = __builtin_amdgcn_readfirstlane(pnode[wv][sp]);
-                active = live & !found & !((e.x == INACTIVE) & (e.y == INACTIVE));
-                tmin = __uint_as_float(e.x);
-                tmax = __uint_as_float(e.y);
-                if (__ballot(active)) return true;
+                bool a = false;
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    const bool act = live[s] & !found[s] & (e[s] != INACTIVE);
+                    tmin[s] = act ? tmax[s] : tmin[s]; // the stack invariant
+                    tmax[s] = act ? __uint_as_float(e[s]) : tmax[s];
+                    active[s] = act;
+                    a = a | act;
+                }
+                if (__ballot(a)) return true;
             }
             return false;
         };
         // a leaf reached with record nd; boxed: its box was read with its fat record
         auto leaf = [&](uint2 nd, bool boxed) {
             const uint32_t first = nd.x, count = nd.y >> 2;
-            if (!boxed) active = active & inb(sload_box(cnode + cn));
-            if (!__ballot(active) || !count) return;
-            const float4 *rb = S.recs + (size_t)REC_STRIDE * first;
+            if (!boxed) {
+                const float4 lb = sload_box(cnode + cn);
+#pragma unroll
+                for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, lb);
+            }
+            if (!any_active() || !count) return;
+            const float4 *rb = Sc.recs + (size_t)REC_STRIDE * first;
             for (uint32_t j = 0; j < count; j += 4) {
                 const cr_v16f bb = sload_box4(cref + first + j);
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) {
                     if (j + k >= count) break;
-                    const bool in = active & (csx >= bb[4 * k]) & (csx <= bb[4 * k + 1]) & (csy >= bb[4 * k + 2]) &
-                                    (csy <= bb[4 * k + 3]);
-                    if (!__ballot(in)) continue;
+                    const float4 b = make_float4(bb[4 * k], bb[4 * k + 1], bb[4 * k + 2], bb[4 * k + 3]);
+                    bool in[S], any = false;
+#pragma unroll
+                    for (int s = 0; s < S; s++) {
+                        in[s] = active[s] & inb(s, b);
+                        any = any | in[s];
+                    }
+                    if (!__ballot(any)) continue;
                     const TriRec r = sload_rec(rb + (size_t)REC_STRIDE * (j + k));
-                    float ux, uy, t;
-                    const bool acc = in & tri_test_wave(eye, d, r, tmax, ux, uy, t);
-                    bx = acc ? ux : bx;
-                    by = acc ? uy : by;
-                    tmax = acc ? t : tmax;
-                    tri = acc ? rec_id(r) : tri;
-                    found = found | acc;
+#pragma unroll
+                    for (int s = 0; s < S; s++) {
+                        if (!__ballot(in[s])) continue;
+                        float ux, uy, t;
+                        const bool acc = in[s] & tri_test_wave(eye, d[s], r, tmax[s], ux, uy, t);
+                        // the hit record straight to the queue (a later, nearer one in this leaf overwrites it)
+                        if (acc) hits[idx[s]] = make_uint4(rec_id(r), __float_as_uint(ux), __float_as_uint(uy), 1u);
+                        tmax[s] = acc ? t : tmax[s];
+                        found[s] = found[s] | acc;
+                    }
                 }
             }
         };
-        bool go = __ballot(active) != 0;
+        bool go = any_active();
         while (go) {
             // fetch node cn: its record, both children's records and its subtree box
             uint4 f0, f1;
             float4 b;
-            sload_fat_box_n(S.fat, cnode, cn, f0, f1, b);
-            active = active & inb(b);
+            sload_fat_box_n(Sc.fat, cnode, cn, f0, f1, b);
+#pragma unroll
+            for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, b);
             uint2 nd = make_uint2(f0.x, f0.y);
             bool popit = true;
             // one fat record serves two levels: the fetched node (lvl 0, its children's
             // records at hand) and the child stepped into (lvl 1, its children fetched next)
             for (uint32_t lvl = 0;; lvl++) {
-                if (!__ballot(active)) break;
+                if (!any_active()) break;
                 if ((nd.y & 3u) == 3u) {
                     leaf(nd, lvl == 0);
                     break;
                 }
                 const uint32_t a = nd.y & 3u, child = nd.y >> 2;
                 const float split = __uint_as_float(nd.x);
-                const float oa = comp(eye, a), da = comp(d, a);
-                const float tsplit = split_distance(split, oa, da);
+                const float oa = comp(eye, a);
                 const uint32_t below = oa < split ? 1u : 0u; // uniform: the eye is not on the plane
-                // (bitwise logic on the lane masks: no short-circuit branches)
-                const bool crosses = !(tsplit >= tmax) & !(tsplit < 0.f); // !near_only
-                const bool after = !(tsplit <= tmin);                     // far_only = crosses & !after
-                const bool both = crosses & after;
-                const bool to_near = active & (!crosses | after);
                 const uint32_t nearc = child + (1u - below), farc = child + below;
-                if (!__ballot(to_near)) { // every active lane goes to the far child only
+                // (bitwise logic on the lane masks: no short-circuit branches)
+                float tsp[S];
+                bool crosses[S], after[S], to_near[S], to_far[S], anyn = false, anyf = false;
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    tsp[s] = split_distance(split, oa, comp(d[s], a));
+                    crosses[s] = !(tsp[s] >= tmax[s]) & !(tsp[s] < 0.f); // !near_only
+                    after[s] = !(tsp[s] <= tmin[s]);                     // far_only = crosses & !after
+                    to_near[s] = active[s] & (!crosses[s] | after[s]);
+                    to_far[s] = active[s] & crosses[s];
+                    anyn = anyn | to_near[s];
+                    anyf = anyf | to_far[s];
+                }
+                if (!__ballot(anyn)) { // every active ray goes to the far child only
                     cn = farc;
                 } else {
-                    const bool to_far = active & crosses;
-                    if (__ballot(to_far)) push(farc, to_far, both ? tsplit : tmin, tmax);
-                    active = to_near;
-                    tmax = both ? tsplit : tmax;
+                    if (__ballot(anyf)) push(farc, to_far);
+#pragma unroll
+                    for (int s = 0; s < S; s++) {
+                        // both: near with tmax = tsplit; far only: parked with tmax = tmin
+                        const float nt = after[s] ? tsp[s] : tmin[s];
+                        tmax[s] = to_far[s] ? nt : tmax[s];
+                        active[s] = to_near[s];
+                    }
                     cn = nearc;
                 }
                 if (lvl == 1) { // cn's record is not in this fat record: fetch it
@@ -771,8 +837,9 @@ template <int R> __global__ void __launch_bounds__(256, 8) wf_trace_packet(Rende
             }
             go = popit ? pop() : true;
         }
-        if (live) hits[idx] = found ? make_uint4(tri, __float_as_uint(bx), __float_as_uint(by), 1u)
-                                    : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int s = 0; s < S; s++)
+            if (live[s] & !found[s]) hits[idx[s]] = make_uint4(0u, 0u, 0u, 0u);
     }
     c.closest = issued;
     flush_counters(A.counters, c, 0u);
@@ -785,11 +852,12 @@ struct WfVariant {
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
     int ring, waves_per_simd, tile;
     int cull; // the camera trace reads the cull boxes (1: references and leaves, 2: also subtrees)
+    int packet; // the camera trace is a packet trace (needs a near child common to all camera rays)
 };
 #define CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, PL)                                                     \
     {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
      wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>,                                  \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>, R, W, TL, CU}
+     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>, R, W, TL, CU, 0}
 #define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU) CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, 0)
 #define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, 0)
 #define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
@@ -815,18 +883,21 @@ static const WfVariant kWf[] = {
     // pass by the triangle's plane (planecull.hpp)
     CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1),
     // 17: 15 whose camera rays traverse as one packet per wave (wf_trace_packet)
-    {wf_trace_packet<8>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2}};
+    {wf_trace_packet<8, 1>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1},
+    // 18: 17 with two camera rays per lane (packets of 128 rays: the scalar control per node
+    // shared by twice the rays)
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1}};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
-                                   0};
+                                   0, 0};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
 // The camera-ray trace of a variant; the packet trace (build 17) needs a near child common
 // to all camera rays, which an eye lying exactly on a split plane breaks: build 15's then.
 static void (*camera_kernel(const WfVariant &v, const RenderArgs &A))(RenderArgs, WfArgs, uint32_t) {
-    return (v.camera == (void (*)(RenderArgs, WfArgs, uint32_t))wf_trace_packet<8> && A.eye_on_split) ? kWf[15].camera
-                                                                                                       : v.camera;
+    return (v.packet && A.eye_on_split) ? kWf[15].camera : v.camera;
 }
 bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].cull; }
 

@@ -56,7 +56,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
 
 
 @pytest.mark.parametrize("xcd,sort_min,variant", [(7, 0, 15), (7, 1 << 20, 15), (1, 0, 15), (2, 0, 15), (4, 0, 17),
-                                                   (7, 0, 17), (0, 0, 17)])
+                                                   (7, 0, 17), (0, 0, 17), (7, 0, 18), (0, 0, 18)])
 def test_wavefront_xcd_partition_bitexact(ca, sponza, nanobox, xcd, sort_min, variant):
     """XCD-partitioned queues (wf_xcd bits: shadow, secondary closest, camera) change which
     block traces which ray only: every ray is traced once, whatever the queue length
@@ -76,7 +76,7 @@ def test_wavefront_xcd_partition_bitexact(ca, sponza, nanobox, xcd, sort_min, va
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
     wave-uniform nodes / leaves) renders the same bits."""
@@ -100,7 +100,7 @@ CULL_CAMS = {
 }
 
 
-@pytest.mark.parametrize("variant", [14, 15, 16, 17])
+@pytest.mark.parametrize("variant", [14, 15, 16, 17, 18])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell", "cornell_box"])
 def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_mm, cfg, variant):
     """Trace builds 14 / 15 / 16: the camera-ray trace skips Moller-Trumbore tests, leaves
@@ -137,7 +137,7 @@ def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_
         pair.dev.set_option("variant", -1)
 
 
-@pytest.mark.parametrize("variant", [15, 17])
+@pytest.mark.parametrize("variant", [15, 17, 18])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell"])
 def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg, variant):
     """The default build (camera-ray cull boxes) at 12 random cameras per scene: eyes
@@ -172,7 +172,8 @@ def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg, variant):
         pair.dev.set_option("variant", -1)
 
 
-def test_packet_camera_eye_on_split_plane(ca, sponza, cornell):
+@pytest.mark.parametrize("variant", [17, 18])
+def test_packet_camera_eye_on_split_plane(ca, sponza, cornell, variant):
     """Build 17's packet camera trace needs every camera ray to agree on a node's near
     child; an eye exactly on a split plane breaks that (kdtree.cpp:262 then decides by
     the ray's direction), and the render falls back to build 15's camera trace.  Eyes
@@ -182,7 +183,7 @@ def test_packet_camera_eye_on_split_plane(ca, sponza, cornell):
         lo, hi = np.array(list(pair.desc.box_min)), np.array(list(pair.desc.box_max))
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("counters", 0)
-        pair.dev.set_option("variant", 17)
+        pair.dev.set_option("variant", variant)
         try:
             for axis in range(3):
                 inner = np.nonzero((e["is_leaf"] == 0) & (e["axis"] == axis))[0]
