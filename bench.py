@@ -134,7 +134,7 @@ def issue_roofline(dom, iss, views, issue, pass_view, kind):
     bytes_view = {"algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"], "achieved_gbs": dom["achieved"],
                   "frac_of_hbm": round(dom["achieved"] / HBM_PEAK_GBS, 4),
                   "frac_of_l2_aggregate": round(dom["achieved"] / L2_PEAK_GBS, 4),
-                  "fabric_bytes_per_launch": dom["traffic"],
+                  "fabric_bytes_per_launch": dom["traffic"], "work_per_launch": dom.get("work_per_launch"),
                   "note": "SURVEY 8d bytes of the reference algorithm's work (counting build); the cull boxes of the "
                           "camera trace skip most of that work exactly, so its rate is an effective one"}
     what = {"camera": "camera-ray", "closest": "secondary closest-hit", "shadow": "shadow-ray"}[kind]
