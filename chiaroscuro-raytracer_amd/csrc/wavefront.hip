@@ -28,6 +28,7 @@
 #include "camcull.hpp"
 #include "traverse.hpp"
 
+#include <atomic>
 #include <thread>
 
 namespace cr {
@@ -1021,6 +1022,19 @@ void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks) {
     blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * TAIL_MINW;
 }
 
+// Grid of the grid-stride wf_shade: every block resident at once.  wf_shade needs 71 VGPRs,
+// so a SIMD holds 7 of its waves, not 8: with 8 blocks per CU the eighth started only when
+// another had finished its whole share (the grid-stride loop gives every block the same).
+static uint32_t shade_grid(int num_cus) {
+    static std::atomic<int> per_cu{0};
+    int b = per_cu.load();
+    if (!b) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, wf_shade, 256, 0) != hipSuccess || b <= 0) b = 8;
+        per_cu.store(b);
+    }
+    return (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)std::min(b, 8);
+}
+
 int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st, const WfStreams &ss,
                            TraceEvents *te) {
     WfArgs W = W0;
@@ -1061,7 +1075,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     }
     closest(1, st, nullptr, W.gstack); // camera rays: path order is already coherent
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
-        hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        hipLaunchKernelGGL(wf_shade, dim3(shade_grid(num_cus)), dim3(256), 0, st, A, W, g);
         uint32_t cnt[2] = {0u, 0u}; // shadow queue g, closest queue g + 1
         if ((err = (int)hipMemcpyAsync(&cnt[0], W.cnt + WF_G + g, 4, hipMemcpyDeviceToHost, st)) ||
             (err = (int)hipMemcpyAsync(&cnt[1], W.cnt + g + 1, 4, hipMemcpyDeviceToHost, st)) ||
@@ -1129,7 +1143,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         err = trace_event(te, s, kind, false);
     };
     auto shade = [&](WfLane &ln, Run &r) { // wf_shade(g), then the queue lengths to the host, async
-        hipLaunchKernelGGL(wf_shade, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, r.g);
+        hipLaunchKernelGGL(wf_shade, dim3(shade_grid(num_cus)), dim3(256), 0, ln.st, A, r.W, r.g);
         if ((err = (int)hipMemcpyAsync(&ln.hcnt[0], r.W.cnt + WF_G + r.g, 4, hipMemcpyDeviceToHost, ln.st)) ||
             (err = (int)hipMemcpyAsync(&ln.hcnt[1], r.W.cnt + r.g + 1, 4, hipMemcpyDeviceToHost, ln.st)) ||
             (err = (int)hipEventRecord(ln.ready, ln.st)))
