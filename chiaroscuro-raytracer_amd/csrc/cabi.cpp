@@ -179,6 +179,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             const uint64_t nkeys = (uint64_t)(A.n_items / (T * T)) * sub * sub * c->wf_dir_res * c->wf_dir_res;
             int key_bits = 1;
             while (key_bits < 32 && (1ull << key_bits) < nkeys) key_bits++;
+            const int key_bits_pixel = key_bits;
             const uint64_t nworld = (1ull << (3 * c->wf_world_bits)) * c->wf_dir_res * c->wf_dir_res;
             while (c->wf_world_keys && key_bits < 32 && (1ull << key_bits) < nworld) key_bits++;
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
@@ -208,6 +209,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cxy = (float2 *)take(8 * (size_t)P);
                 W.sort = c->wf_sort && nkeys <= (1ull << 32);
                 W.key_bits = key_bits;
+                W.key_bits_pixel = key_bits_pixel;
                 W.sort_lib = c->wf_sort_lib;
                 W.sort_min = c->wf_sort_min;
                 W.sort_tile = c->wf_sort_tile;

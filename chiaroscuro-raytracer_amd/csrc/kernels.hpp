@@ -152,7 +152,8 @@ struct WfArgs {
     void *sort_tmp;
     size_t sort_tmp_bytes;
     int sort;         // 1: write keys and sort the queues of large generations
-    int key_bits;     // significant key bits
+    int key_bits;     // significant key bits (world keys included)
+    int key_bits_pixel; // significant bits of the pixel keys (generation-1 queues): fewer digit passes
     int sort_lib;     // 1: hipcub's radix sort instead of raysort.hip's (comparison)
     uint32_t sort_min;   // queues shorter than this are traced in append order
     uint32_t sort_tile;  // log2 of the pixel sub-tile edge of the key (3: 8x8 pixels)

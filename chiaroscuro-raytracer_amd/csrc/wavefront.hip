@@ -973,11 +973,14 @@ void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &bloc
 // Sorts the queue of n rays whose keys wf_shade wrote into key / perm set `set`
 // (0 shadow, 1 closest); returns the permutation for the trace kernel (nullptr:
 // trace in queue order).
-static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStream_t st, int &err) {
+// pixel: the queue's keys are pixel keys (wf_shade of a generation below world_keys), which
+// need fewer bits than world keys -- one digit pass fewer for a rank's share of a frame
+static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStream_t st, int &err, bool pixel) {
     if (!W.sort || err || n < W.sort_min) return nullptr;
     uint32_t *keys[2] = {W.key[set][0], W.key[set][1]}, *vals[2] = {W.perm[set][0], W.perm[set][1]};
     size_t tb = W.sort_tmp_bytes;
-    const int sel = sort_queue(keys, vals, n, W.key_bits, W.sort_tmp, tb, st, W.sort_lib != 0);
+    const int bits = pixel ? W.key_bits_pixel : W.key_bits;
+    const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, W.sort_lib != 0);
     if (sel < 0) {
         err = (int)hipErrorUnknown;
         return nullptr;
@@ -1083,8 +1086,9 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
             break;
         const uint32_t nc = g < (uint32_t)A.K ? cnt[1] : 0u;
         const bool next = nc >= W.tail_min && nc > 0; // closest g + 1 as its own launch, beside shadow g
-        const uint32_t *order_s = order_queue(W, 0, cnt[0], st, err);
-        const uint32_t *order_c = next ? order_queue(W, 1, nc, st, err) : nullptr;
+        const bool pixel = !(W.world_keys && g >= (uint32_t)W.world_keys); // wf_shade's key choice
+        const uint32_t *order_s = order_queue(W, 0, cnt[0], st, err, pixel);
+        const uint32_t *order_c = next ? order_queue(W, 1, nc, st, err, pixel) : nullptr;
         if (err) break;
         if (next) {
             if ((err = (int)hipEventRecord(ss.fork, st)) || (err = (int)hipStreamWaitEvent(ss.side, ss.fork, 0))) break;
@@ -1179,8 +1183,9 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         const uint32_t g = r.g, ns = ln.hcnt[0];
         const uint32_t nc = g < (uint32_t)A.K ? ln.hcnt[1] : 0u;
         const bool next = nc >= r.W.tail_min && nc > 0;
-        const uint32_t *order_s = order_queue(r.W, 0, ns, ln.st, err);
-        const uint32_t *order_c = next ? order_queue(r.W, 1, nc, ln.st, err) : nullptr;
+        const bool pixel = !(r.W.world_keys && g >= (uint32_t)r.W.world_keys); // wf_shade's key choice
+        const uint32_t *order_s = order_queue(r.W, 0, ns, ln.st, err, pixel);
+        const uint32_t *order_c = next ? order_queue(r.W, 1, nc, ln.st, err, pixel) : nullptr;
         if (err) return true;
         if (next) {
             if ((err = (int)hipEventRecord(ln.fork, ln.st)) || (err = (int)hipStreamWaitEvent(ln.side, ln.fork, 0)))
