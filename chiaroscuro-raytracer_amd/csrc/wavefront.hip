@@ -594,8 +594,9 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
 }
 
 // ------------------------------------------------- packet camera-ray trace --
-// Trace build 17's camera-ray trace.  A wave's 64 camera rays -- 64 samples of one
-// pixel, taken in lock-step -- traverse the kd tree as ONE packet: the node is
+// Trace builds 17 / 18's camera-ray trace.  A wave's 64 (S = 1) or 128 (S = 2, two per
+// lane) camera rays -- consecutive samples of one pixel, taken in lock-step -- traverse
+// the kd tree as ONE packet: the node is
 // wave-uniform (scalar loads, uniform control flow), and every lane keeps its own
 // interval and an active flag.  All camera rays start at the eye, so a node's near
 // child (kdtree.cpp:262, `belowFirst` from the origin's side of the split) is the same
@@ -608,8 +609,9 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
 // A lane that finds a hit in a leaf is done (the first leaf with a hit ends its query),
 // the others go on; cull boxes (camcull.hpp) deactivate a lane for a subtree / leaf /
 // triangle exactly as in build 15.  The stack: per entry the node (per wave, LDS) and
-// each lane's interval or an inactive mark (the ring [R][thread] in LDS, deeper entries
-// spilled to gstack as in trav_round).  If the eye lies exactly on a split plane of its
+// each ray's tmax at push or an inactive mark (the ring [R][thread][S] in LDS, deeper
+// entries spilled to gstack as in trav_round; tmin comes back by the stack invariant, see
+// below; tests/test_packet_model.py checks the scheme on the CPU).  If the eye lies exactly on a split plane of its
 // axis the near child could differ between lanes; the host then uses build 15's camera
 // trace for that render (RenderArgs::eye_on_split).
 enum : uint32_t { PACKET_DEPTH = 256 }; // >= the deepest tree cr_upload_scene accepts
