@@ -182,6 +182,13 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             const int key_bits_pixel = key_bits;
             const uint64_t nworld = (1ull << (3 * c->wf_world_bits)) * c->wf_dir_res * c->wf_dir_res;
             while (c->wf_world_keys && key_bits < 32 && (1ull << key_bits) < nworld) key_bits++;
+            // leaf keys: (leaf node, direction bin) when they fit 32 bits
+            int leaf_bits = 1;
+            while (leaf_bits < 40 &&
+                   (1ull << leaf_bits) < (((uint64_t)A.S.n_nodes >> c->wf_leaf_shift) + 1) * c->wf_dir_res * c->wf_dir_res)
+                leaf_bits++;
+            const bool leaf_keys = c->wf_leaf_keys && leaf_bits <= 32;
+            if (leaf_keys) key_bits = std::max(key_bits, leaf_bits);
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
             const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 16 * (size_t)P +
                                 (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
@@ -218,6 +225,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.world_bits = c->wf_world_bits;
                 W.tail_min = c->wf_tail_min;
                 W.xcd = c->wf_xcd;
+                W.leaf_keys = leaf_keys ? 1 : 0;
+                W.leaf_shift = c->wf_leaf_shift;
                 if (c->wf_sort) {
                     for (int q = 0; q < 2; q++)
                         for (int i = 0; i < 2; i++) {
@@ -830,6 +839,8 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_sort_lib") && (v == 0 || v == 1)) c->wf_sort_lib = (int)v;
     else if (!std::strcmp(key, "wf_lanes") && (v == 1 || v == 2)) c->wf_lanes = (int)v;
     else if (!std::strcmp(key, "wf_xcd") && v >= 0 && v <= 7) c->wf_xcd = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_leaf_keys") && (v == 0 || v == 1)) c->wf_leaf_keys = (int)v;
+    else if (!std::strcmp(key, "wf_leaf_shift") && v >= 0 && v <= 24) c->wf_leaf_shift = (uint32_t)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;
     else return fail(c, CR_E_INVALID, std::string("unknown option or value: ") + key);

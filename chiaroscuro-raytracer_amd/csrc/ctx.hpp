@@ -87,6 +87,11 @@ struct cr_ctx {
     // sponza 1080p x 128 spp, 2 interleaved rounds: 0 / 1 / 3 / 7 -> 435.1 / 432.4 / 431.4 / 423.1 ms
     // per pass (build 15); build 17: 429.3 -> 416.5 ms with 7
     uint32_t wf_xcd = 7;
+    // queue keys from the starting hit's kd leaf (WfArgs::leaf_keys), sponza 1080p x 128 spp,
+    // 2 interleaved rounds: pixel / world keys 409.5 -> leaf keys 396.4 ms per pass; coarser
+    // regions (node index >> 3 / 6 / 9) 405.2 / 418.7 / 440.2 vs 401.6 ms, 32 direction bins 409.3
+    int wf_leaf_keys = 1;
+    uint32_t wf_leaf_shift = 0; // ... its node index >> this
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

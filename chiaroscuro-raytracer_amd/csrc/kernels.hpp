@@ -168,6 +168,11 @@ struct WfArgs {
     // blockIdx % WF_XCDS (the dispatcher's round-robin) takes rays from its own range first,
     // then from the others' -- each XCD's L2 then holds the data of one region of key space
     uint32_t xcd;
+    // 1: queue keys are (leaf of the hit the ray starts from, direction bin) -- the hit
+    // record's w carries the leaf + 1 -- instead of pixel / world-position keys
+    int leaf_keys;
+    uint32_t leaf_shift; // leaf keys: the node index >> leaf_shift (depth-first numbering: a run of
+                         // consecutive nodes is one region of the tree)
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
-                                                           __float_as_uint(d.y), 1u)
+                                                           __float_as_uint(d.y), T.node + 1u) // w: the hit's leaf + 1
                                               : make_uint4(0u, 0u, 0u, 0u);
                 state = ST_NEED_WORK;
             }
@@ -448,8 +448,9 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
             W.sray[2 * (size_t)j + 1] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
             W.sexcl[j] = sh.light;
             if (W.sort) {
-                W.key[0][0][j] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
-                                                                               : sort_key(A, W, p, sh.d);
+                W.key[0][0][j] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res * W.dir_res) + dir_bin(sh.d, W.dir_res)
+                                 : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
+                                                                                 : sort_key(A, W, p, sh.d);
                 W.perm[0][0][j] = j;
             }
         }
@@ -458,8 +459,9 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
             next_rays[2 * (size_t)jc] = pk(org, p);
             next_rays[2 * (size_t)jc + 1] = pk(wi, 0u);
             if (W.sort) {
-                W.key[1][0][jc] = (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
-                                                                                : sort_key(A, W, p, wi);
+                W.key[1][0][jc] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res * W.dir_res) + dir_bin(wi, W.dir_res)
+                                  : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
+                                                                                  : sort_key(A, W, p, wi);
                 W.perm[1][0][jc] = jc;
             }
         }
@@ -750,12 +752,13 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
         auto leaf = [&](uint2 nd, bool boxed) {
             const uint32_t first = nd.x, count = nd.y >> 2;
             if (!boxed) {
-                const float4 lb = sload_box(cnode + cn);
+                const float4 lb = sload_box(cnode + __builtin_amdgcn_readfirstlane(cn));
 #pragma unroll
                 for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, lb);
             }
             if (!any_active() || !count) return;
             const float4 *rb = Sc.recs + (size_t)REC_STRIDE * first;
+            const uint32_t leafw = __builtin_amdgcn_readfirstlane(cn) + 1u; // hit record w: the leaf + 1
             for (uint32_t j = 0; j < count; j += 4) {
                 const cr_v16f bb = sload_box4(cref + first + j);
 #pragma unroll
@@ -776,7 +779,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                         float ux, uy, t;
                         const bool acc = in[s] & tri_test_wave(eye, d[s], r, tmax[s], ux, uy, t);
                         // the hit record straight to the queue (a later, nearer one in this leaf overwrites it)
-                        if (acc) hits[idx[s]] = make_uint4(rec_id(r), __float_as_uint(ux), __float_as_uint(uy), 1u);
+                        if (acc) hits[idx[s]] = make_uint4(rec_id(r), __float_as_uint(ux), __float_as_uint(uy), leafw);
                         tmax[s] = acc ? t : tmax[s];
                         found[s] = found[s] | acc;
                     }
@@ -788,6 +791,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             // fetch node cn: its record, both children's records and its subtree box
             uint4 f0, f1;
             float4 b;
+            cn = __builtin_amdgcn_readfirstlane(cn); // uniform by construction
             sload_fat_box_n(Sc.fat, cnode, cn, f0, f1, b);
 #pragma unroll
             for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, b);
@@ -1088,7 +1092,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
             break;
         const uint32_t nc = g < (uint32_t)A.K ? cnt[1] : 0u;
         const bool next = nc >= W.tail_min && nc > 0; // closest g + 1 as its own launch, beside shadow g
-        const bool pixel = !(W.world_keys && g >= (uint32_t)W.world_keys); // wf_shade's key choice
+        const bool pixel = !W.leaf_keys && !(W.world_keys && g >= (uint32_t)W.world_keys); // wf_shade's key choice
         const uint32_t *order_s = order_queue(W, 0, cnt[0], st, err, pixel);
         const uint32_t *order_c = next ? order_queue(W, 1, nc, st, err, pixel) : nullptr;
         if (err) break;
@@ -1185,7 +1189,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         const uint32_t g = r.g, ns = ln.hcnt[0];
         const uint32_t nc = g < (uint32_t)A.K ? ln.hcnt[1] : 0u;
         const bool next = nc >= r.W.tail_min && nc > 0;
-        const bool pixel = !(r.W.world_keys && g >= (uint32_t)r.W.world_keys); // wf_shade's key choice
+        const bool pixel = !r.W.leaf_keys && !(r.W.world_keys && g >= (uint32_t)r.W.world_keys); // wf_shade's key choice
         const uint32_t *order_s = order_queue(r.W, 0, ns, ln.st, err, pixel);
         const uint32_t *order_c = next ? order_queue(r.W, 1, nc, ln.st, err, pixel) : nullptr;
         if (err) return true;

@@ -36,21 +36,25 @@ def nanobox(ca, po, scenes):
     return Pair(ca, po, scenes.config_rtc("nanobox"))
 
 
+@pytest.mark.parametrize("leaf", [0, 1])
 @pytest.mark.parametrize("tile_dir", [(3, 8), (1, 2), (5, 32)])
-def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir):
+def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir, leaf):
     """Queue sorting reorders the trace work only: force it on every queue (the
-    default sorts queues of >= 1M rays) with several key layouts."""
+    default sorts queues of >= 1M rays) with several key layouts, pixel / world keys
+    (leaf 0) or keys from the kd leaf of the hit a ray starts from (leaf 1)."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_sort_min", 0)
         pair.dev.set_option("wf_sort_tile", tile_dir[0])
         pair.dev.set_option("wf_dir_res", tile_dir[1])
+        pair.dev.set_option("wf_leaf_keys", leaf)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
         finally:
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_sort_tile", 4)
             pair.dev.set_option("wf_dir_res", 64)
+            pair.dev.set_option("wf_leaf_keys", 0)
         assert_bitwise(g, o, "sorted wavefront %dx%dx%d" % (x, y, s))
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
