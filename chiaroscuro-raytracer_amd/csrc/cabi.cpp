@@ -99,9 +99,12 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.counters = c->d_counters;
     A.work = c->d_work;
     A.full_counters = c->full_counters;
-    // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783)
-    A.refill = c->refill ? c->refill : (c->kernel == 2 ? 56u : 16u);
-    A.refill_shadow = c->refill_shadow ? c->refill_shadow : (c->refill ? c->refill : 48u);
+    // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783);
+    // re-swept under leaf-keyed queues (scripts/gpu_leaf_sweep.sh, 1080p x 128 spp, closest /
+    // shadow): 56/48 397.4, 48/56 394.5, 48/48 395.9, 56/56 396.2 ms per pass; a rank of 8:
+    // 59.96 vs 59.64 ms -> closest 48 / shadow 56
+    A.refill = c->refill ? c->refill : (c->kernel == 2 ? 48u : 16u);
+    A.refill_shadow = c->refill_shadow ? c->refill_shadow : (c->refill ? c->refill : 56u);
     // camera rays (64 samples of one pixel per wave): lock-step is best, 64 -> 933 vs 56 -> 924 Mray/s
     A.refill_camera = c->refill_camera ? c->refill_camera : (c->refill ? c->refill : (c->kernel == 2 ? 64u : 16u));
     // wavefront trace builds (wavefront.hip kWf): 2 = LDS ring 8, 8 waves/SIMD, scalar loads for

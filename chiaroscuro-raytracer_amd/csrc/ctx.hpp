@@ -59,8 +59,8 @@ struct cr_ctx {
     int variant = -1;       // -1: the kernel's default build
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;
-    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 56 wavefront)
-    uint32_t refill_shadow = 0; // wavefront shadow trace; 0: refill if set, else 48
+    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 48 wavefront)
+    uint32_t refill_shadow = 0; // wavefront shadow trace; 0: refill if set, else 56
     uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: refill if set, else 64
     uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
     int wf_sort = 1;                // wavefront: sort large shadow / secondary queues for coherence
