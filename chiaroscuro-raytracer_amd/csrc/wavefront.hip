@@ -157,9 +157,11 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
             PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), 1u);
             PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key);
             PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
+            PS(W, 3, p) = make_float4(0.f, 0.f, 0.f, 0.f); // no resolve mark (wf_resolve)
             W.ray[1][2 * (size_t)p] = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(p));
             W.ray[1][2 * (size_t)p + 1] = pk(d, 0u);
         } else if (p < W.P) {
+            PS(W, 3, p) = make_float4(0.f, 0.f, 0.f, 0.f);
             W.ray[1][2 * (size_t)p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(NO_PATH));
             W.ray[1][2 * (size_t)p + 1] = make_float4(0.f, 0.f, 1.f, 0.f);
         }
@@ -367,7 +369,8 @@ __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W
 // need the shadow result (rayTracer.cpp:80-134): hit shading, emission, the NEE
 // light sample and -- for k < K -- the BRDF sample and Russian roulette, in the
 // reference's draw order.  The NEE term stays pending for wf_resolve:
-// dw[2(k-1)] = {direct, shadow slot (set by the caller)}, PS3 = {contrib, ended}.
+// dw[2(k-1)] = {direct, shadow slot (set by the caller)}, PS3 = {contrib, 2k | ended}:
+// the mark 2k tells wf_resolve's path-order sweep which paths hit at bounce k.
 // A continuing path gets W_k in dw[2(k-1)+1] and its next closest ray (org, wi).
 __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t k, f3 ro, uint4 h,
                                            bool &textured, ShadowRay &sh, bool &cont, f3 &org, f3 &wi) {
@@ -405,7 +408,7 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
         }
     }
     W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(hs.direct, NO_SLOT);
-    PS(W, 3, p) = pk(contrib, cont ? 0u : 1u);
+    PS(W, 3, p) = pk(contrib, (k << 1) | (cont ? 0u : 1u));
     return nee;
 }
 
@@ -475,20 +478,36 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
 // After the shadow trace of generation g: the bounce's direct term
 // D_k = direct + (visible ? contrib : 0) (rayTracer.cpp:96-99), and the
 // back-to-front fold of every path that ended at this bounce.
+__device__ __forceinline__ void resolve_path(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t g, float4 s3) {
+    float4 &dk = W.dw[(size_t)(2 * (g - 1)) * W.P + p];
+    const float4 d4 = dk;
+    const uint32_t slot = __float_as_uint(d4.w);
+    f3 direct = ld3(d4);
+    if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(s3));
+    if (__float_as_uint(s3.w) & 1u) finish_path(A, W, p, g, direct);
+    else dk = pk(direct, 0u);
+}
+
+// A long (sorted) queue is swept in PATH order: the hits of generation g are the
+// paths whose PS3 carries the mark 2g (wf_camera clears it, shade_next sets it), so
+// the path-state, dw and sample accesses are coalesced instead of scattered in the
+// queue's leaf order.  A short queue is swept in queue order (fewer bytes than a
+// pass over all P slots).  Each path's arithmetic is the same either way.
 __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32_t g) {
     const uint32_t n = *cnt_closest(W, g);
+    if (W.resolve_paths && (uint64_t)n * 4u >= (uint64_t)W.P) {
+        for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < W.P; p += gridDim.x * blockDim.x) {
+            const float4 s3 = PS(W, 3, p);
+            if ((__float_as_uint(s3.w) >> 1) == g) resolve_path(A, W, p, g, s3);
+        }
+        return;
+    }
     const float4 *rays = W.ray[g & 1];
     const uint4 *hits = W.hit[g & 1];
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         if (hits[i].w == 0u) continue;
         const uint32_t p = __float_as_uint(rays[2 * (size_t)i].w);
-        float4 &dk = W.dw[(size_t)(2 * (g - 1)) * W.P + p];
-        const float4 d4 = dk, s3 = PS(W, 3, p);
-        const uint32_t slot = __float_as_uint(d4.w);
-        f3 direct = ld3(d4);
-        if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(s3));
-        if (__float_as_uint(s3.w)) finish_path(A, W, p, g, direct);
-        else dk = pk(direct, 0u);
+        resolve_path(A, W, p, g, PS(W, 3, p));
     }
 }
 

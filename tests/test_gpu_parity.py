@@ -54,9 +54,37 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir, leaf):
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_sort_tile", 4)
             pair.dev.set_option("wf_dir_res", 64)
-            pair.dev.set_option("wf_leaf_keys", 0)
+            pair.dev.set_option("wf_leaf_keys", 1)
         assert_bitwise(g, o, "sorted wavefront %dx%dx%d" % (x, y, s))
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
+@pytest.mark.parametrize("resolve_paths", [0, 1])
+def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, resolve_paths):
+    """wf_resolve in queue order (0) or, for queues of at least P / 4 rays, in path order
+    by the PS3 bounce mark (1, default): the same bits and counters over progressive
+    layers 1..3 on the same buffers (a mark left by an earlier layer or chunk must not
+    resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_resolve_paths", resolve_paths)
+        pair.dev.set_option("wf_sort_min", 0)
+        cam = pair.camera(ca, x, y)
+        try:
+            for paths in (256 << 20, 4096):
+                pair.dev.set_option("wf_paths", paths)
+                o = None
+                for layer in (1, 2, 3):
+                    p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=layer)
+                    g = pair.dev.render(cam, p, None)
+                    gc = pair.dev.counters()
+                    o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
+                    assert_bitwise(g, o, "resolve_paths %d wf_paths %d layer %d" % (resolve_paths, paths, layer))
+                    assert {k: gc[k] for k in ORACLE_KEYS} == oc
+        finally:
+            pair.dev.set_option("wf_resolve_paths", 1)
+            pair.dev.set_option("wf_sort_min", 1 << 20)
+            pair.dev.set_option("wf_paths", 256 << 20)
 
 
 @pytest.mark.parametrize("xcd,sort_min,variant", [(7, 0, 15), (7, 1 << 20, 15), (1, 0, 15), (2, 0, 15), (4, 0, 17),
