@@ -171,7 +171,7 @@ struct WfArgs {
     // 1: queue keys are (leaf of the hit the ray starts from, direction bin) -- the hit
     // record's w carries the leaf + 1 -- instead of pixel / world-position keys
     int leaf_keys;
-    int resolve_paths; // wf_resolve sweeps long queues in path order (cr_set_option wf_resolve_paths)
+    uint32_t resolve_paths; // wf_resolve sweeps queues of >= P / this rays in path order (0: never)
     uint32_t leaf_shift; // leaf keys: the node index >> leaf_shift (depth-first numbering: a run of
                          // consecutive nodes is one region of the tree)
 };

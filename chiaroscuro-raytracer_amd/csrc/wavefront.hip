@@ -488,14 +488,14 @@ __device__ __forceinline__ void resolve_path(const RenderArgs &A, const WfArgs &
     else dk = pk(direct, 0u);
 }
 
-// A long (sorted) queue is swept in PATH order: the hits of generation g are the
+// A long queue (at least P / resolve_paths rays) is swept in PATH order: the hits of generation g are the
 // paths whose PS3 carries the mark 2g (wf_camera clears it, shade_next sets it), so
 // the path-state, dw and sample accesses are coalesced instead of scattered in the
 // queue's leaf order.  A short queue is swept in queue order (fewer bytes than a
 // pass over all P slots).  Each path's arithmetic is the same either way.
 __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32_t g) {
     const uint32_t n = *cnt_closest(W, g);
-    if (W.resolve_paths && (uint64_t)n * 4u >= (uint64_t)W.P) {
+    if (W.resolve_paths && (uint64_t)n * W.resolve_paths >= (uint64_t)W.P) {
         for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < W.P; p += gridDim.x * blockDim.x) {
             const float4 s3 = PS(W, 3, p);
             if ((__float_as_uint(s3.w) >> 1) == g) resolve_path(A, W, p, g, s3);
