@@ -92,7 +92,8 @@ struct cr_ctx {
     // regions (node index >> 3 / 6 / 9) 405.2 / 418.7 / 440.2 vs 401.6 ms, 32 direction bins 409.3
     int wf_leaf_keys = 1;
     uint32_t wf_leaf_shift = 0; // ... its node index >> this
-    uint32_t wf_resolve_paths = 4; // wf_resolve in path order for queues of at least P / this rays (0: never)
+    // sweep (1080p x 128 spp, 2 rounds): 0 / 1 / 2 / 4 / 8 / 16 / 64 -> 399.2 / 394.6 / 394.8 / 394.8 / 393.8 / 393.6 / 394.5 ms
+    uint32_t wf_resolve_paths = 16; // wf_resolve in path order for queues of at least P / this rays (0: never)
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

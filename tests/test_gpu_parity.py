@@ -62,7 +62,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir, leaf):
 @pytest.mark.parametrize("resolve_paths", [0, 1, 4, 64])
 def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, resolve_paths):
     """wf_resolve in queue order (0) or, for queues of at least P / resolve_paths rays, in
-    path order by the PS3 bounce mark (default 4; 64: nearly every generation): the same bits and counters over progressive
+    path order by the PS3 bounce mark (default 16; 64: nearly every generation): the same bits and counters over progressive
     layers 1..3 on the same buffers (a mark left by an earlier layer or chunk must not
     resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
@@ -82,7 +82,7 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, resolve_paths):
                     assert_bitwise(g, o, "resolve_paths %d wf_paths %d layer %d" % (resolve_paths, paths, layer))
                     assert {k: gc[k] for k in ORACLE_KEYS} == oc
         finally:
-            pair.dev.set_option("wf_resolve_paths", 4)
+            pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_paths", 256 << 20)
 
