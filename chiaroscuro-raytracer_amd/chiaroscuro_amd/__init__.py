@@ -85,6 +85,8 @@ class ChiaroSceneInfo(C.Structure):
 
 
 TRACE_KINDS = ("camera", "closest", "shadow", "tail")  # cr_trace_stats order
+DIAG_NAMES = ("rounds", "lanes", "distinct", "records", "maxcount", "lanetests", "fit64", "fit128",
+              "urounds", "tests", "geomiss", "rep1", "rep4", "rep8")  # cr_get_diag order (DIAG_* in kernels.hpp)
 
 
 class CrTraceStats(C.Structure):
@@ -110,10 +112,10 @@ _host = None
 # Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
                "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_tile_origin", "cr_intersect",
-               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize",
+               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize", "cr_get_diag",
                "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap",
                "cr_comm_unique_id", "cr_comm_init", "cr_comm_destroy", "cr_render_dist_device",
-               "cr_device_count", "cr_group_create", "cr_group_destroy", "cr_group_last_error", "cr_group_size",
+               "cr_device_count", "cr_group_create", "cr_group_destroy", "cr_group_last_error", "cr_group_size", "cr_group_ok",
                "cr_group_upload_scene", "cr_group_set_option", "cr_group_render", "cr_group_get_counters",
                "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
@@ -153,7 +155,10 @@ def libs():
     # libchiaro_hip.so needs (libamdhip64.so.7, librccl.so.1), so loaded in this
     # order the process holds one copy of each (the other order maps a second
     # runtime next to torch's, whose exit-time teardown collides with the first)
-    import torch  # noqa: F401
+    try:  # only the load order matters; host-only use (scene parsing, the preview camera) needs no torch
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     hip = C.CDLL(str(hip_path), mode=C.RTLD_GLOBAL)
     host = C.CDLL(str(host_path))
     _sig(hip, "cr_create", P, [C.c_int])
@@ -173,6 +178,7 @@ def libs():
     _sig(hip, "cr_last_kernel_ms", C.c_float, [P])
     _sig(hip, "cr_get_trace_stats", C.c_int, [P, C.POINTER(CrTraceStats)])
     _sig(hip, "cr_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
+    _sig(hip, "cr_get_diag", C.c_int, [P, C.POINTER(C.c_uint64), C.c_int])
     _sig(hip, "cr_synchronize", C.c_int, [P])
     _sig(hip, "cr_tonemap_setup", None, [C.c_float] * 5 + [C.POINTER(CrTonemapParams)])
     _sig(hip, "cr_tonemap_device", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32, P, P, P])
@@ -188,6 +194,7 @@ def libs():
     _sig(hip, "cr_group_destroy", None, [P])
     _sig(hip, "cr_group_last_error", C.c_char_p, [P])
     _sig(hip, "cr_group_size", C.c_int, [P])
+    _sig(hip, "cr_group_ok", C.c_int, [P])
     _sig(hip, "cr_group_upload_scene", C.c_int, [P, C.POINTER(CrSceneDesc)])
     _sig(hip, "cr_group_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
     _sig(hip, "cr_group_render", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), FP])
@@ -475,6 +482,13 @@ class Device:
                        "leaf": int(t.leaf[i]), "tritest": int(t.tritest[i])}
                 for i, name in enumerate(TRACE_KINDS)}
 
+    def diag(self) -> dict:
+        """cr_get_diag: leaf-round shapes and the repeated-miss census of the last
+        counting render, for the trace kinds of option "diag_kinds"."""
+        v = (C.c_uint64 * len(DIAG_NAMES))()
+        self._chk(libs()[0].cr_get_diag(self._c, v, len(DIAG_NAMES)), "cr_get_diag")
+        return {n: int(v[i]) for i, n in enumerate(DIAG_NAMES)}
+
     def set_option(self, key: str, value: int):
         self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")
 
@@ -522,6 +536,10 @@ class Group:
         devs = (C.c_int * len(devices))(*[int(d) for d in devices])
         self._g = hip.cr_group_create(len(devices), devs)
         self.devices = list(devices)
+        if not hip.cr_group_ok(self._g):  # a bad device, no GPU, or RCCL refused the communicator
+            err = hip.cr_group_last_error(self._g).decode()
+            self.close()
+            raise RuntimeError("cr_group_create(%s) failed: %s" % (self.devices, err))
 
     def _chk(self, rc, what):
         if rc != CR_OK:
@@ -631,7 +649,7 @@ class Preview:
     """The interactive preview's render path without a window (chiaro_preview_*,
     src/openglPreview.cpp:12-257): keys R / TAB / = / - / W S A D E Q, mouse, scroll,
     and the screen texture (getData after normalizeImage)."""
-    KEYS = {"R": 0, "TAB": 1, "=": 2, "-": 3, "W": 4, "S": 5, "A": 6, "D": 7, "E": 8, "Q": 9}
+    KEYS = {"R": 0, "TAB": 1, "=": 2, "-": 3, "W": 4, "S": 5, "A": 6, "D": 7, "E": 8, "Q": 9, "SHIFT": 10}
 
     def __init__(self, scene: Scene, rt: RayTracer):
         _, host = libs()

@@ -4,6 +4,7 @@
 // kernels.hip header), the progressive accumulator, the counters and the
 // per-launch HIP events.  No C++ exception or hipError_t crosses the ABI.
 #include "ctx.hpp"
+#include "leafcull.hpp"
 #include "planecull.hpp"
 
 #include <algorithm>
@@ -11,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace crx {
@@ -99,6 +101,8 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.counters = c->d_counters;
     A.work = c->d_work;
     A.full_counters = c->full_counters;
+    A.diag_kinds = c->diag_kinds;
+    A.lc_debug = c->lc_debug;
     // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783);
     // re-swept under leaf-keyed queues (scripts/gpu_leaf_sweep.sh, 1080p x 128 spp, closest /
     // shadow): 56/48 397.4, 48/56 394.5, 48/48 395.9, 56/56 396.2 ms per pass; a rank of 8:
@@ -255,7 +259,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         }
         // screen-space cull boxes of this camera for the camera-ray trace (camcull.hpp),
         // computed inside the timed region of every render
-        const bool cull = wf && !c->full_counters && cr::wf_variant_culls(A.variant) && c->n_refs > 0;
+        // (built for triangle-less scenes too: the culling kernels read them unconditionally, and
+        // with n_refs + 4 empty boxes every sample is outside)
+        const bool cull = wf && !c->full_counters && cr::wf_variant_culls(A.variant);
         if (cull) {
             if (int r = grow(c, &c->d_cull, c->cull_bytes, 16 * ((size_t)c->n_refs + 4))) return r;
             if (int r = grow(c, &c->d_cull_node, c->cull_node_bytes, 16 * (size_t)c->S.n_nodes)) return r;
@@ -308,6 +314,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     c->last = cr_counters{h[0], h[1],  h[2],  h[3],  h[4],  h[5],  h[6],  h[7], h[8],
                           h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16],
                           h[17], h[18], h[19], h[20], h[21]};
+    for (int i = 0; i < cr::DIAG_N; i++) c->last_diag[i] = h[cr::CTR_DIAG + i];
     c->last_trace = cr_trace_stats{};
     if (c->kernel == 2) {
         for (int i = 0; i < c->tev.n; i++) {
@@ -520,6 +527,29 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
             planes[r] = make_float4(o[0], o[1], o[2], o[3]);
         }
     }
+    // leaf cull records (leafcull.hpp), per node of the new numbering; host threads
+    std::vector<float4> lcull((size_t)cr::LC_REC * NN, make_float4(0.f, 0.f, 0.f, 0.f));
+    {
+        const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (unsigned w = 0; w < nth; w++)
+            th.emplace_back([&, w] {
+                float A[cr::LC_MAXREFS][3], e1[cr::LC_MAXREFS][3], e2[cr::LC_MAXREFS][3];
+                for (uint32_t i = w; i < NN; i += nth) {
+                    if ((nodes[i].y & 3u) != 3u) continue;
+                    const uint32_t first = nodes[i].x, cnt = nodes[i].y >> 2;
+                    const uint32_t m = std::min(cnt, (uint32_t)cr::LC_MAXREFS);
+                    for (uint32_t j = 0; j < m; j++) {
+                        const float4 *q = recs.data() + (size_t)cr::REC_STRIDE * (first + j);
+                        A[j][0] = q[0].x, A[j][1] = q[0].y, A[j][2] = q[0].z;
+                        e1[j][0] = q[1].x, e1[j][1] = q[1].y, e1[j][2] = q[1].z;
+                        e2[j][0] = q[2].x, e2[j][1] = q[2].y, e2[j][2] = q[2].z;
+                    }
+                    cr::leaf_cull_record(A, e1, e2, cnt, (cr::LcFloat4 *)(lcull.data() + (size_t)cr::LC_REC * i));
+                }
+            });
+        for (auto &t : th) t.join();
+    }
     std::vector<float4> tri((size_t)3 * nt), mn(nt), mkd(nt), mke(nt);
     std::vector<float2> muv((size_t)3 * nt);
     for (uint32_t t = 0; t < nt; t++) {
@@ -564,15 +594,20 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     // their parent in this numbering: one forward pass gives the depths)
     std::vector<uint32_t> depth(NN, 0), levels;
     std::vector<std::pair<uint32_t, uint32_t>> level_off;
+    uint32_t tree_depth = 0; // deepest node (root = 0): the most entries a traversal stack holds
     {
         uint32_t maxd = 0;
         for (uint32_t i = 0; i < NN; i++) {
+            tree_depth = std::max(tree_depth, depth[i]);
             if ((nodes[i].y & 3u) == 3u) continue;
             const uint32_t ch = nodes[i].y >> 2;
             if (ch <= i) return fail(c, CR_E_INVALID, "kd child numbered before its parent");
             depth[ch] = depth[ch + 1] = depth[i] + 1;
             maxd = std::max(maxd, depth[i]);
         }
+        // the stacks (LDS rings, gstack, the packet trace's PACKET_DEPTH node stack) are sized
+        // from the tree itself, never from the caller's declared max_depth
+        if (tree_depth > 256) return fail(c, CR_E_DEPTH, "kd tree deeper than 256");
         std::vector<uint32_t> cnt(maxd + 1, 0);
         for (uint32_t i = 0; i < NN; i++)
             if ((nodes[i].y & 3u) != 3u) cnt[depth[i]]++;
@@ -593,7 +628,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         free_scene(c);
         return rc;
     }
-    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, tri, &c->S.tri)) ||
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
         (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels))) {
@@ -604,7 +639,13 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     c->S.n_nodes = d->n_nodes;
     c->S.bmin = make_float3(d->box_min[0], d->box_min[1], d->box_min[2]);
     c->S.bmax = make_float3(d->box_max[0], d->box_max[1], d->box_max[2]);
-    c->stack_depth = d->max_depth > 0 ? d->max_depth : 1;
+    {
+        double db = 1.0; // every origin (a hit point + 0.001 n) and vertex lies in the padded box
+        for (int i = 0; i < 3; i++)
+            db = std::max(db, std::max(std::fabs((double)d->box_min[i]), std::fabs((double)d->box_max[i])) + 1.0);
+        c->S.db = (float)(db * 1.0001);
+    }
+    c->stack_depth = std::max(tree_depth, std::max(d->max_depth, 1u));
     c->n_refs = d->n_refs;
     for (int a = 0; a < 3; a++) c->splits[a].clear();
     for (uint32_t i = 0; i < NN; i++)
@@ -820,11 +861,19 @@ int cr_get_trace_stats(cr_ctx *c, cr_trace_stats *out) {
     return CR_OK;
 }
 
+int cr_get_diag(cr_ctx *c, uint64_t *out, int n) {
+    if (!c || !out || n < 0) return CR_E_INVALID;
+    for (int i = 0; i < n && i < cr::DIAG_N; i++) out[i] = c->last_diag[i];
+    return CR_OK;
+}
+
 int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!c || !key) return CR_E_INVALID;
     const int64_t nvar = std::max(cr::num_persistent_variants(), cr::num_wf_variants());
     if (!std::strcmp(key, "kernel") && (v == 0 || v == 1 || v == 2)) c->kernel = (int)v;
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
+    else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
+    else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
     else if (!std::strcmp(key, "variant") && v >= -1 && v < nvar) c->variant = (int)v; // -1 default; clamped per kernel
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;

@@ -56,6 +56,9 @@ struct cr_ctx {
     //   persistent megakernel (kernel 0), variant 0, refill 16:                615 Mray/s
     int kernel = 2;
     int full_counters = 1;
+    int lc_debug = 0;                      // measurement only (RenderArgs::lc_debug)
+    uint32_t diag_kinds = 0;               // counting renders: trace kinds of the DIAG_* census (1 << TK_*)
+    unsigned long long last_diag[cr::DIAG_N] = {};
     int variant = -1;       // -1: the kernel's default build
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;

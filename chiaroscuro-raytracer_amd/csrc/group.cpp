@@ -225,16 +225,19 @@ cr_group *cr_group_create(int ngpus, const int *devices) {
         return g;
     }
     for (int r = 0; r < ngpus; r++) g->devices.push_back(devices ? devices[r] : r);
-    for (int r = 0; r < ngpus; r++) {
-        g->ctx.push_back(cr_create(g->devices[r]));
-        if (g->ctx.back()->device < 0) {
-            g->err = "rank " + std::to_string(r) + ": " + cr_last_error(g->ctx.back());
-            return g;
-        }
-    }
+    // per-rank buffers sized before any ctx exists: cr_group_destroy walks them for every
+    // created ctx, also after a failed create
     g->tiles.assign(ngpus, nullptr);
     g->tiles_bytes.assign(ngpus, 0);
     g->rank_ms.assign(ngpus, 0.f);
+    for (int r = 0; r < ngpus; r++) {
+        g->ctx.push_back(cr_create(g->devices[r]));
+        if (!g->ctx.back() || g->ctx.back()->device < 0) {
+            g->err = "rank " + std::to_string(r) + " (device " + std::to_string(g->devices[r]) +
+                     "): " + cr_last_error(g->ctx.back());
+            return g;
+        }
+    }
     std::vector<int> sorted = g->devices;
     std::sort(sorted.begin(), sorted.end());
     if (std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end()) {
@@ -253,9 +256,10 @@ void cr_group_destroy(cr_group *g) {
     for (ncclComm_t c : g->comm)
         if (c) ncclCommDestroy(c);
     for (size_t r = 0; r < g->ctx.size(); r++) {
+        if (!g->ctx[r]) continue;
         if (g->ctx[r]->device >= 0) {
             hipSetDevice(g->devices[r]);
-            if (g->tiles[r]) hipFree(g->tiles[r]);
+            if (r < g->tiles.size() && g->tiles[r]) hipFree(g->tiles[r]);
             if (r == 0) {
                 if (g->gathered) hipFree(g->gathered);
                 if (g->frame) hipFree(g->frame);
@@ -267,14 +271,17 @@ void cr_group_destroy(cr_group *g) {
 }
 
 const char *cr_group_last_error(cr_group *g) { return g ? g->err.c_str() : "null group"; }
+static bool group_ok(cr_group *g);
 
 int cr_group_size(cr_group *g) { return g ? (int)g->ctx.size() : 0; }
 
+int cr_group_ok(cr_group *g) { return g && group_ok(g) ? 1 : 0; }
+
 // Usable: every ctx on a device, and a communicator unless a device repeats.
 static bool group_ok(cr_group *g) {
-    if (g->ctx.empty()) return false;
+    if (g->ctx.empty() || g->ctx.size() != g->devices.size()) return false;
     for (cr_ctx *c : g->ctx)
-        if (c->device < 0) return false;
+        if (!c || c->device < 0) return false;
     std::vector<int> sorted = g->devices;
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();

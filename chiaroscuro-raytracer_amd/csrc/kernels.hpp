@@ -9,13 +9,32 @@ enum { MODE_BLEND = 0, MODE_TILES = 1 };
 // float4 per triangle record.  3 (48 B, 1.5 lines per test on average) beat 4
 // (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
 enum { REC_STRIDE = 3 };
-enum { CTR_N = 22, CTR_SLOTS = 40 }; // Ctr fields (cr_counters order); device counter buffer entries
+enum { CTR_N = 22, CTR_SLOTS = 64 }; // Ctr fields (cr_counters order); device counter buffer entries
 // Wavefront trace launches by kind (cr_trace_stats order): camera rays (generation-1
 // closest trace), closest traces of later generations, shadow traces, the tail kernel.
 enum { TK_CAMERA = 0, TK_CLOSEST = 1, TK_SHADOW = 2, TK_TAIL = 3, TK_N = 4 };
 // Counting builds of the trace kernels also tally inner / leaf / tritest per kind
 // (not the tail): slots CTR_TRACE + 3 * kind + {0, 1, 2}.
 enum { CTR_TRACE = 24 };
+// Leaf-round and repeated-miss diagnostics of counting builds (cr_get_diag, DIAG_* order),
+// for the trace kinds in RenderArgs::diag_kinds (bit 1 << TK_*): slots CTR_DIAG + i.
+enum { CTR_DIAG = 40, DIAG_N = 16 };
+enum {
+    DIAG_ROUNDS = 0,    // divergent leaf rounds (the wave's busy lanes at more than one leaf)
+    DIAG_LANES = 1,     //   lanes at a leaf with triangles, summed over those rounds
+    DIAG_DISTINCT = 2,  //   distinct leaves with triangles, summed
+    DIAG_RECORDS = 3,   //   records of the distinct leaves, summed (what LDS staging would load)
+    DIAG_MAXCOUNT = 4,  //   the largest leaf of the round, summed (wave iterations of the leaf loop)
+    DIAG_LANETESTS = 5, //   records of every lane's leaf, summed (lane work of the leaf loop)
+    DIAG_FIT64 = 6,     //   rounds with at most 64 / 128 staged records
+    DIAG_FIT128 = 7,
+    DIAG_UROUNDS = 8,   // uniform leaf rounds
+    DIAG_TESTS = 9,     // triangle tests (lane)
+    DIAG_GEOMISS = 10,  //   rejected for any segment (det, u, v or t < 0): exact to skip later in the query
+    DIAG_REP1 = 11,     //   of those: the triangle was such a miss in the lane's last 1 / 4 / 8 such misses
+    DIAG_REP4 = 12,
+    DIAG_REP8 = 13,
+};
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one
 // texel past the row/image end for coords == 1.0 (src/mesh.cpp:23-30) and three
@@ -48,6 +67,10 @@ struct DevScene {
     // one per leaf reference (+ 3 padding): the triangle's plane scaled by its rounding
     // margin (planecull.hpp), the exact pre-test of the secondary / shadow traces
     const float4 *planes;
+    // LC_REC (leafcull.hpp) per kd node: a leaf's references in two normal groups, each with
+    // its box and normal cone -- the exact skip of the tests a unit-direction ray cannot pass
+    const float4 *lcull;
+    float db;             // bound on |coordinate| of any origin or vertex (padded box + 1)
     const float4 *tri;    // 3 per triangle: A, B, C
     const float4 *mat_n;  // normal, w = emissive flag bits
     const float4 *mat_kd; // Kd, w = texture index (int bits, -1 none)
@@ -101,6 +124,8 @@ struct RenderArgs {
     // 1: the eye lies exactly on a split plane of its axis, where camera rays may disagree on
     // a node's near child -- the packet camera trace (build 17) is not used for this render
     int eye_on_split;
+    uint32_t diag_kinds;          // counting builds: trace kinds (1 << TK_*) the DIAG_* slots describe
+    int lc_debug;                 // measurement only: leaf-cull masks 1 = every reference, 2 = none (wrong images)
 };
 int num_persistent_variants();
 

@@ -1,0 +1,268 @@
+// leafcull.hpp -- leaf cull records: an exact skip of the Moller-Trumbore tests
+// (kdtree.cpp:219-246 / 293-320) of secondary closest and shadow rays whose test
+// segment cannot reach the triangles.
+//
+// A kd leaf's reference list holds every triangle that has a vertex on the leaf's side
+// of each ancestor split, so most of its triangles lie far from the leaf's cell: on the
+// sponza stand-in 96% of the tests a shadow ray performs are of triangles whose tight box
+// the ray's test segment [0, tmax_leaf] does not even touch (scripts/leafcull_census.py).
+// A test accepts only for a segment that reaches the triangle up to rounding, so those
+// tests can be skipped -- exactly, if the rounding is bounded.
+//
+// The bound.  With sv = RN(o - A) and the record's e1, e2, Moller-Trumbore computes
+// AA = e1.(d x e2), U = sv.(d x e2), V = d.(sv x e1), T = e2.(sv x e1) with rounding
+// errors |dX| <= Ex (camcull.hpp's terms).  Let d be a unit vector (|d|_2 = 1 +- 8u,
+// checked per ray), S >= |sv_i| (the origin against the group box), E >= |e1|_1 + |e2|_1
+// and g >= E^2 / |e1 x e2| for every triangle of a group.  Then
+//     Ea <= 10.04u E^2,  Eu, Ev <= 10.04u S E,  Et <= 10.04u S E^2        (u = 2^-24)
+// and for any accepting evaluation with |AA| > Ea (so sign(AA) is the computed one) the
+// exact solution o' + t* d = A + u* e1 + v* e2 (o' = A + sv, |o' - o|_i <= u S) has
+// barycentric weights >= -m, m <= 10.05u (1 + 2S/E) g / cb + 3.1u, where cb <= |d^.n^|
+// bounds the cosine between the ray and the triangle's normal line: |AA| >= |n| cb.
+// So the point o + t* d lies within pad = 2 m E + u S of the triangle's box, at
+//     t* in [-dt, tmax (1 + 10.05u g / cb)(1 + 2.1u) + dt],  dt = 10.05u S g / cb.
+// cb comes from a cone of normal lines per group: every |a^.n^| >= ct (= cos theta), so
+// |d^.n^| >= cos(psi + theta) with cos psi = |d^.a^|.  A grazing ray (cb small) gets a
+// large pad or none (cb <= 20.2u g: never skipped) -- with |AA| near its rounding error
+// the test can accept anywhere along a line close to the triangle's PLANE, so no box
+// bound holds there, and a single cone per leaf would be too wide (columns, corners):
+// the leaf's triangles are split into two groups by normal direction (k-means on normal
+// lines), each with its own box and cone.  Degenerate triangles are always tested.
+//
+// Record per kd node (LC_REC float4, leaves with 1..32 references; others test all):
+//   {lo0, g0} {hi0, E0} {axis0, ct0} {lo1, g1} {hi1, E1} {axis1, ct1}
+//   {mask0, mask1, always, 0}   (bit j: reference first + j is in group 0 / 1 / tested always)
+// The kernel evaluates the skip in float with every rounding of its own accounted for
+// (leaf_cull_mask); tests/native/leafcull_check.cpp checks the whole argument against
+// the float test on random and adversarial rays and triangles.
+#pragma once
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define CR_LC_HD __host__ __device__
+#else
+#define CR_LC_HD
+#endif
+
+namespace cr {
+
+enum { LC_REC = 7, LC_MAXREFS = 32 };
+
+struct LcFloat4 {
+    float x, y, z, w;
+};
+
+// 1 when |d|^2 is within 12u of 1 (so |d| = 1 +- 8u): the bound assumes unit directions
+CR_LC_HD inline bool lc_unit(float dx, float dy, float dz) {
+    const float dd = (dx * dx + dy * dy) + dz * dz;
+    return fabsf(dd - 1.f) <= 12.f * 0x1p-24f;
+}
+
+// One group's skip for ray (o, d) (unit, inv = RN(1/d)), segment [0, tmax]; db bounds
+// |coordinate| of the scene (origins and vertices).  True: no triangle of the group can
+// accept.  Float arithmetic, every rounding covered by a margin.
+CR_LC_HD inline bool lc_group_skip(const float o[3], const float d[3], const float inv[3], float tmax, float db,
+                                   LcFloat4 lo, LcFloat4 hi, LcFloat4 ax) {
+    const float u = 0x1p-24f;
+    const float g = lo.w, E = hi.w, ct = ax.w;
+    // cos psi >= |d.a| - 16u (rounding of the dot, |d|, |a| = 1 +- 8u); sin psi and sin theta from above
+    const float dn = fabsf((d[0] * ax.x + d[1] * ax.y) + d[2] * ax.z);
+    const float cpl = fmaxf(dn - 16.f * u, 0.f);
+    const float sph = sqrtf(fmaxf(1.f - cpl * cpl, 0.f) + 3.f * u) * (1.f + u);
+    const float sth = sqrtf(fmaxf(1.f - ct * ct, 0.f) + 3.f * u) * (1.f + u);
+    const float cb = (cpl * ct - sph * sth) - 3.f * u;
+    if (!(cb > 20.2f * u * g)) return false; // grazing (or NaN): the test could accept anywhere near the plane
+    float S = 0.f;
+    for (int i = 0; i < 3; i++) S = fmaxf(S, fmaxf(fabsf(o[i] - (&lo.x)[i]), fabsf(o[i] - (&hi.x)[i])));
+    S *= 1.f + 3.f * u;
+    const float ic = (1.f / cb) * (1.f + 2.f * u);
+    // the slab arithmetic below rounds coordinates up to max(db, |o|): 4u of that on top
+    const float mb = fmaxf(db, fmaxf(fabsf(o[0]), fmaxf(fabsf(o[1]), fabsf(o[2]))));
+    const float pad = ((20.11f * u) * (E + 2.f * S) * g * ic + (6.21f * u) * E + u * S) * (1.f + 8.f * u) +
+                      4.f * u * mb + 1e-20f;
+    const float dt = ((10.06f * u) * S * g * ic) * (1.f + 4.f * u) + 1e-20f;
+    const float t_hi = (tmax * (1.f + (10.06f * u) * g * ic) * (1.f + 3.f * u)) * (1.f + 2.f * u) + dt;
+    const float t_lo = -dt;
+    float tn = -INFINITY, tf = INFINITY;
+    for (int i = 0; i < 3; i++) {
+        const float t0 = (((&lo.x)[i] - pad) - o[i]) * inv[i], t1 = (((&hi.x)[i] + pad) - o[i]) * inv[i];
+        const bool nan = !(t0 == t0) || !(t1 == t1); // o on a face with d_i = 0: the whole line
+        const float a = nan ? -INFINITY : (t0 < t1 ? t0 : t1), b = nan ? INFINITY : (t0 < t1 ? t1 : t0);
+        tn = a > tn ? a : tn;
+        tf = b < tf ? b : tf;
+    }
+    // the slab parameters carry 3u of relative rounding: widen before deciding
+    tn -= 4.f * u * fabsf(tn);
+    tf += 4.f * u * fabsf(tf);
+    return (tn > tf) | (tn > t_hi) | (tf < t_lo);
+}
+
+// The references of a leaf (count of them) its tests need for this ray: bit j for
+// reference first + j.  rec: the node's LC_REC float4.  Leaves beyond LC_MAXREFS and
+// non-unit rays: every reference (the caller tests count references then).
+CR_LC_HD inline uint32_t leaf_cull_mask(const float o[3], const float d[3], const float inv[3], bool unit,
+                                        float tmax, float db, const LcFloat4 *rec, uint32_t count) {
+    const uint32_t all = count >= 32 ? 0xffffffffu : ((1u << count) - 1u);
+    if (!unit || count > (uint32_t)LC_MAXREFS) return all;
+    const LcFloat4 m = rec[6];
+    uint32_t keep;
+    __builtin_memcpy(&keep, &m.z, 4);
+    uint32_t m0, m1;
+    __builtin_memcpy(&m0, &m.x, 4);
+    __builtin_memcpy(&m1, &m.y, 4);
+    if (m0 && !lc_group_skip(o, d, inv, tmax, db, rec[0], rec[1], rec[2])) keep |= m0;
+    if (m1 && !lc_group_skip(o, d, inv, tmax, db, rec[3], rec[4], rec[5])) keep |= m1;
+    return keep & all;
+}
+
+// Host: the record of a leaf from its references' floats as the test uses them
+// (A, e1, e2 per reference, in list order).  count 0 or > LC_MAXREFS: every bit "always".
+inline void leaf_cull_record(const float (*A)[3], const float (*e1)[3], const float (*e2)[3], uint32_t count,
+                             LcFloat4 out[LC_REC]) {
+    for (int i = 0; i < LC_REC; i++) out[i] = LcFloat4{0.f, 0.f, 0.f, 0.f};
+    auto put_u = [](float &f, uint32_t v) { __builtin_memcpy(&f, &v, 4); };
+    if (count == 0 || count > (uint32_t)LC_MAXREFS) {
+        put_u(out[6].z, 0xffffffffu);
+        return;
+    }
+    double N[LC_MAXREFS][3], Ev[LC_MAXREFS], Gv[LC_MAXREFS];
+    bool ok[LC_MAXREFS];
+    for (uint32_t j = 0; j < count; j++) {
+        const double a[3] = {e1[j][0], e1[j][1], e1[j][2]}, b[3] = {e2[j][0], e2[j][1], e2[j][2]};
+        const double n[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+        const double nl = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        double mag = 0;
+        for (int i = 0; i < 3; i++) mag = fmax(mag, fabs(A[j][i]));
+        Ev[j] = (fabs(a[0]) + fabs(a[1]) + fabs(a[2])) + (fabs(b[0]) + fabs(b[1]) + fabs(b[2]));
+        ok[j] = nl > 0 && nl < 1e30 && Ev[j] < 1e15 && mag < 1e15;
+        Gv[j] = ok[j] ? Ev[j] * Ev[j] / nl * (1 + 1e-12) : 0;
+        ok[j] = ok[j] && Gv[j] < 1e20;
+        for (int i = 0; i < 3; i++) N[j][i] = ok[j] ? n[i] / nl : 0;
+    }
+    // two groups of normal LINES (sign-free): farthest-point start, k-means on |cos|
+    double C[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    int nc = 0;
+    for (uint32_t j = 0; j < count && !nc; j++)
+        if (ok[j]) {
+            for (int i = 0; i < 3; i++) C[0][i] = N[j][i];
+            nc = 1;
+        }
+    if (nc) {
+        double worst = 2;
+        int wj = -1;
+        for (uint32_t j = 0; j < count; j++) {
+            if (!ok[j]) continue;
+            const double c = fabs(N[j][0] * C[0][0] + N[j][1] * C[0][1] + N[j][2] * C[0][2]);
+            if (c < worst) {
+                worst = c;
+                wj = (int)j;
+            }
+        }
+        if (wj >= 0 && worst < 0.999999) {
+            for (int i = 0; i < 3; i++) C[1][i] = N[wj][i];
+            nc = 2;
+        }
+    }
+    int lab[LC_MAXREFS];
+    for (int it = 0; it < 12 && nc; it++) {
+        double M[2][9] = {};
+        for (uint32_t j = 0; j < count; j++) {
+            if (!ok[j]) continue;
+            int q = 0;
+            double best = -1;
+            for (int k = 0; k < nc; k++) {
+                const double c = fabs(N[j][0] * C[k][0] + N[j][1] * C[k][1] + N[j][2] * C[k][2]);
+                if (c > best) {
+                    best = c;
+                    q = k;
+                }
+            }
+            lab[j] = q;
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) M[q][3 * a + b] += N[j][a] * N[j][b];
+        }
+        for (int k = 0; k < nc; k++) { // principal direction of the group's normal lines
+            double v[3] = {C[k][0], C[k][1], C[k][2]};
+            for (int r = 0; r < 40; r++) {
+                const double w[3] = {M[k][0] * v[0] + M[k][1] * v[1] + M[k][2] * v[2],
+                                     M[k][3] * v[0] + M[k][4] * v[1] + M[k][5] * v[2],
+                                     M[k][6] * v[0] + M[k][7] * v[1] + M[k][8] * v[2]};
+                const double l = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+                if (!(l > 0)) break;
+                for (int i = 0; i < 3; i++) v[i] = w[i] / l;
+            }
+            for (int i = 0; i < 3; i++) C[k][i] = v[i];
+        }
+    }
+    uint32_t mask[2] = {0u, 0u}, always = 0u;
+    double lo[2][3], hi[2][3], g[2] = {0, 0}, E[2] = {0, 0};
+    float axf[2][3];
+    double ct[2] = {1, 1};
+    for (int k = 0; k < 2; k++) {
+        // the axis as the kernel reads it (float), normalised; the cone is measured against it
+        double l = 0;
+        for (int i = 0; i < 3; i++) {
+            axf[k][i] = (float)C[k][i];
+            l += (double)axf[k][i] * axf[k][i];
+        }
+        l = sqrt(l);
+        for (int i = 0; i < 3; i++) {
+            lo[k][i] = INFINITY;
+            hi[k][i] = -INFINITY;
+        }
+        if (!(l > 0)) ct[k] = 0;
+        C[k][0] = l > 0 ? axf[k][0] / l : 0;
+        C[k][1] = l > 0 ? axf[k][1] / l : 0;
+        C[k][2] = l > 0 ? axf[k][2] / l : 0;
+    }
+    for (uint32_t j = 0; j < count; j++) {
+        if (!ok[j] || !nc) {
+            always |= 1u << j;
+            continue;
+        }
+        int q = 0;
+        double best = -1;
+        for (int k = 0; k < nc; k++) {
+            const double c = fabs(N[j][0] * C[k][0] + N[j][1] * C[k][1] + N[j][2] * C[k][2]);
+            if (c > best) {
+                best = c;
+                q = k;
+            }
+        }
+        mask[q] |= 1u << j;
+        ct[q] = fmin(ct[q], best);
+        g[q] = fmax(g[q], Gv[j]);
+        E[q] = fmax(E[q], Ev[j]);
+        // the triangle the test solves for: A, A + e1, A + e2 (exact, not the model's B, C)
+        for (int i = 0; i < 3; i++) {
+            const double a = A[j][i], b = a + (double)e1[j][i], c = a + (double)e2[j][i];
+            lo[q][i] = fmin(lo[q][i], fmin(a, fmin(b, c)));
+            hi[q][i] = fmax(hi[q][i], fmax(a, fmax(b, c)));
+        }
+    }
+    auto down = [](double x) {
+        float f = (float)x;
+        if ((double)f > x) f = nextafterf(f, -INFINITY);
+        return f;
+    };
+    auto up = [](double x) {
+        float f = (float)x;
+        if ((double)f < x) f = nextafterf(f, INFINITY);
+        return f;
+    };
+    for (int k = 0; k < 2; k++) {
+        if (!mask[k]) continue;
+        // 1e-9 below the measured cosine: the double evaluation of the normals and the axis
+        const double c = fmax(0.0, ct[k] - 1e-9);
+        out[3 * k + 0] = LcFloat4{down(lo[k][0]), down(lo[k][1]), down(lo[k][2]), up(g[k] * (1 + 1e-9))};
+        out[3 * k + 1] = LcFloat4{up(hi[k][0]), up(hi[k][1]), up(hi[k][2]), up(E[k] * (1 + 1e-9))};
+        out[3 * k + 2] = LcFloat4{axf[k][0], axf[k][1], axf[k][2], down(c)};
+    }
+    put_u(out[6].x, mask[0]);
+    put_u(out[6].y, mask[1]);
+    put_u(out[6].z, always);
+}
+
+} // namespace cr

@@ -1,6 +1,7 @@
 // traverse.hpp -- the resumable kd traversal shared by the persistent megakernel
 // (persistent.hip) and the wavefront trace kernels (wavefront.hip).
 #pragma once
+#include "leafcull.hpp"
 #include "render_common.hpp"
 
 namespace cr {
@@ -40,6 +41,35 @@ struct Trav {
     float tmin, tmax;
     f3 r;
 };
+
+// Counting-build diagnostics of one lane (DIAG_* in kernels.hpp): the lane's last 8
+// triangles that missed for any segment in its current query (a per-lane mailbox, as a
+// census: no test is skipped), and its tallies (wave-level ones kept by the leader).
+struct Diag {
+    bool on;        // the trace kind is in RenderArgs::diag_kinds
+    uint32_t n;     // misses recorded in this query (reset at each query start)
+    uint32_t mb[8]; // mb[i & 7]: the i-th
+    uint32_t v[DIAG_N];
+};
+__device__ __forceinline__ void diag_begin(Diag *dg) {
+    if (dg) dg->n = 0;
+}
+__device__ __forceinline__ void diag_flush(unsigned long long *ctrs, const Diag &dg) {
+#pragma unroll
+    for (int i = 0; i < DIAG_N; i++) {
+        unsigned long long s = dg.v[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+        if ((threadIdx.x & 63) == 0 && s) atomicAdd(&ctrs[CTR_DIAG + i], s);
+    }
+}
+
+// Phase clock of a wave (measurement builds, PROF): shader-clock cycles spent in
+// trav_round's descent, leaf cull, leaf tests and stack pop, and the calls' total.
+struct Prof {
+    uint64_t desc, cull, test, pop, calls;
+};
+__device__ __forceinline__ uint64_t prof_now() { return __builtin_amdgcn_s_memtime(); }
 
 // Root-box clip (kdtree.cpp:196-208, 276-283); false: the query ends without a hit.
 __device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool shadow, float limit, Trav &T) {
@@ -144,6 +174,42 @@ __device__ __forceinline__ void sload_fat_box_n(const uint4 *fat, const float4 *
     b = make_uint4(r[4], r[5], r[6], r[7]);
     box = make_float4(x[0], x[1], x[2], x[3]);
 }
+// A leaf cull record (LC_REC = 7 float4, 112 B) under one scalar-load wait.
+__device__ __forceinline__ void sload_lcull(const float4 *p, LcFloat4 (&r)[LC_REC]) {
+    cr_v16f a;
+    cr_v8f b;
+    cr_v4f c;
+    asm volatile("s_load_dwordx16 %0, %3, 0x0\n\ts_load_dwordx8 %1, %3, 0x40\n\ts_load_dwordx4 %2, %3, 0x60\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=s"(a), "=s"(b), "=s"(c)
+                 : "s"(p));
+#pragma unroll
+    for (int i = 0; i < 4; i++) r[i] = LcFloat4{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]};
+    r[4] = LcFloat4{b[0], b[1], b[2], b[3]};
+    r[5] = LcFloat4{b[4], b[5], b[6], b[7]};
+    r[6] = LcFloat4{c[0], c[1], c[2], c[3]};
+}
+// The references of the leaf at `node` that the lane's ray (o, d: unit, segment [0, tmax])
+// must test (leafcull.hpp); bits < count.
+template <bool SC>
+__device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
+    LcFloat4 rec[LC_REC];
+    if (SC && wave_uniform(node)) {
+        sload_lcull(S.lcull + (size_t)LC_REC * __builtin_amdgcn_readfirstlane(node), rec);
+    } else {
+        const float4 *p = (const float4 *)((const char *)S.lcull + node * (uint32_t)(16 * LC_REC));
+#pragma unroll
+        for (int i = 0; i < LC_REC; i++) {
+            const float4 v = p[i];
+            rec[i] = LcFloat4{v.x, v.y, v.z, v.w};
+        }
+    }
+    const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
+    // v_rcp_f32: within 1 ulp of 1/d (the check allows 2, tests/native/leafcull_check.cpp)
+    const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+    return leaf_cull_mask(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, S.db, rec, count);
+}
+
 template <bool SC> __device__ __forceinline__ float4 load_box(const float4 *b, uint32_t i) {
     if (SC && wave_uniform(i)) return sload_box(b + __builtin_amdgcn_readfirstlane(i));
     return b[i];
@@ -190,16 +256,22 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // test cannot accept, so skipping it changes nothing.  A uniform leaf reads four boxes
 // per scalar load and tests a triangle only if some lane is inside its box; a divergent
 // lane reads its box (16 B) and, inside, the record (48 B).
+// LC (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a leaf's tests run only
+// for the references its cull record (leafcull.hpp) cannot exclude for this ray and segment.
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false, int CULL = 0, int PLANE = 0>
-__device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
+          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0>
+__device__ __forceinline__ uint32_t trav_round(int lc_debug, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
-                                               const float4 *cull_node = nullptr) {
+                                               const float4 *cull_node = nullptr, Diag *dg = nullptr,
+                                               Prof *pf = nullptr) {
+    uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
+    if (pf) pt0 = prof_now();
     static_assert(!CULL || (BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "cull: lean BF + SC builds");
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
+    static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -256,6 +328,26 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
     // empty leaf -- none of its triangles can accept, so the traversal would leave it
     // without a hit and with tmax = its interval's end, which is exactly this state
     bool culled = false;
+    uint32_t first, count, lmask;
+    bool lin;
+    // the stack's top entry becomes the query's node and interval (stack invariant)
+    auto pop_entry = [&]() {
+        T.sp--;
+        uint2 e;
+        if (T.nl) {
+            e = ring[(T.sp & (R - 1)) * bdim + tid];
+            T.nl--;
+        } else {
+            e = gstk[(size_t)T.sp * gstride + gid];
+        }
+        T.node = e.x;
+        T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
+        T.tmax = __uint_as_float(e.y);
+    };
+    // LC 2: a leaf whose references are all excluded is passed like an empty leaf -- the lane
+    // pops and descends to its next leaf in the same round, so the round's tests run on every lane
+    for (;;) {
+    culled = false;
     if (FAT) { // two levels per dependent load: a node's record carries its children's
         uint4 f0, f1;
         auto fetch = [&](uint32_t node) {
@@ -310,21 +402,67 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
         c.leaf++;
         if (wave_leader()) c.wave_round++;
     }
-    const uint32_t first = nd.x;
-    uint32_t count = nd.y >> 2;
-    bool lin = !culled; // CULL: the sample lies in the leaf's box (the union of its references')
+    first = nd.x;
+    count = nd.y >> 2;
+    lin = !culled; // CULL: the sample lies in the leaf's box (the union of its references')
     if (CULL && !culled) {
         const float4 lb = load_box<SC>(cull_node, T.node);
         lin = csx >= lb.x && csx <= lb.y && csy >= lb.z && csy <= lb.w;
     }
+    if (pf) pt1 = prof_now();
+    // LC: the references to test (bit j: first + j); count > LC_MAXREFS: every one (lmask unused)
+    lmask = 0u;
+    if (LC && count && count <= (uint32_t)LC_MAXREFS) {
+        lmask = leaf_mask<SC>(S, T.node, count, o, d, T.tmax);
+        if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
+    }
+    if (LC == 2 && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp) {
+        pop_entry();
+        continue;
+    }
+    break;
+    }
+    if (pf) pt2 = prof_now();
     bool found = false, occluded = false;
     uint32_t tri = 0;
     float bx = 0.f, by = 0.f;
+    // the phase clock at a return
+    auto prof_out = [&]() {
+        if (pf) {
+            const uint64_t t4 = prof_now();
+            pf->desc += pt1 - pt0;
+            pf->cull += pt2 - pt1;
+            pf->test += pt3 - pt2;
+            pf->pop += t4 - pt3;
+            pf->calls++;
+        }
+    };
     // one triangle of the leaf (kdtree.cpp:235-246 / 309-320); false: stop the leaf
     auto test = [&](const TriRec &r) -> bool {
         const uint32_t id = rec_id(r);
         if (shadow && id == exclude) return true;
         if (FULL) c.tritest++;
+        if (FULL && dg && dg->on) { // repeated-miss census: a miss for any segment is one for every later one
+            dg->v[DIAG_TESTS]++;
+            float gx, gy, gt;
+            if (!tri_test(o, d, r, __builtin_inff(), gx, gy, gt)) {
+                dg->v[DIAG_GEOMISS]++;
+                const uint32_t n = dg->n;
+                bool r1 = false, r4 = false, r8 = false;
+#pragma unroll
+                for (uint32_t j = 0; j < 8; j++) {
+                    const bool m = j < n && dg->mb[(n - 1 - j) & 7u] == id;
+                    r1 = r1 | (m & (j < 1));
+                    r4 = r4 | (m & (j < 4));
+                    r8 = r8 | m;
+                }
+                dg->v[DIAG_REP1] += r1;
+                dg->v[DIAG_REP4] += r4;
+                dg->v[DIAG_REP8] += r8;
+                dg->mb[n & 7u] = id;
+                dg->n = n + 1;
+            }
+        }
         float ux, uy, t;
         // BF: the lanes that failed an early test compute on (wave-uniform exits, no exec bookkeeping)
         if (BF ? tri_test_wave(o, d, r, T.tmax, ux, uy, t) : tri_test(o, d, r, T.tmax, ux, uy, t)) {
@@ -351,15 +489,19 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             }
         }
     };
-    if (FULL && !wave_uniform(first)) { // what staging the wave's leaves in LDS would take
+    if (FULL && (!dg || dg->on) && !wave_uniform(first)) { // what staging the wave's leaves in LDS would take
         uint64_t m = __ballot(count > 0);
-        uint32_t nd = 0, nr = 0;
+        uint32_t nd = 0, nr = 0, mc = 0, lt = 0;
+        const uint32_t lanes = (uint32_t)__popcll(m);
         while (m) {
             const int l = __ffsll((long long)m) - 1;
             const uint32_t f = (uint32_t)__shfl((int)first, l, 64), n = (uint32_t)__shfl((int)count, l, 64);
-            m &= ~__ballot(first == f && count > 0);
+            const uint64_t same = __ballot(first == f && count > 0);
+            m &= ~same;
             nd++;
             nr += n;
+            mc = max(mc, n);
+            lt += n * (uint32_t)__popcll(same);
         }
         if (wave_leader()) {
             c.leaf_rounds++;
@@ -367,16 +509,29 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             c.leaf_records += nr;
             c.leaf_fit21 += nr <= 21;
             c.leaf_fit56 += nr <= 56;
+            if (dg) {
+                dg->v[DIAG_ROUNDS]++;
+                dg->v[DIAG_LANES] += lanes;
+                dg->v[DIAG_DISTINCT] += nd;
+                dg->v[DIAG_RECORDS] += nr;
+                dg->v[DIAG_MAXCOUNT] += mc;
+                dg->v[DIAG_LANETESTS] += lt;
+                dg->v[DIAG_FIT64] += nr <= 64;
+                dg->v[DIAG_FIT128] += nr <= 128;
+            }
         }
+    } else if (FULL && dg && dg->on && wave_leader()) {
+        dg->v[DIAG_UROUNDS]++;
     }
     if (BF && SC && wave_uniform(first)) { // uniform leaf, results by select
         const uint32_t uf = __builtin_amdgcn_readfirstlane(first), uc = __builtin_amdgcn_readfirstlane(count);
         const float4 *base = S.recs + (size_t)REC_STRIDE * uf;
         // one triangle of the uniform leaf; false: every active lane occluded (stop)
-        auto utest = [&](const TriRec &r, uint32_t j) -> bool {
+        // in: the lane tests this triangle (LC: the bit of its own mask)
+        auto utest = [&](const TriRec &r, uint32_t j, bool in = true) -> bool {
             tally_tri(uf + j);
             const uint32_t id = rec_id(r);
-            const bool live = !(shadow & (occluded | (id == exclude)));
+            const bool live = in & !(shadow & (occluded | (id == exclude)));
             if (FULL) c.tritest += live ? 1u : 0u;
             float ux, uy, t;
             const bool acc = live & tri_test_wave(o, d, r, T.tmax, ux, uy, t);
@@ -424,6 +579,15 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
                     if (__ballot(in)) utest(sload_rec(base + (size_t)REC_STRIDE * (j + k)), j + k);
                 }
             }
+        } else if (LC && uc <= (uint32_t)LC_MAXREFS) {
+            // a triangle runs when some lane's mask holds it (a lane tests only its own
+            // references: utest's `in`); per-bit ballots, since a butterfly over the wave
+            // would not see the bits of lanes whose partners are inactive
+            for (uint32_t j = 0; j < uc; j++) {
+                const bool in = (lmask >> j) & 1u;
+                if (!__ballot(in)) continue;
+                if (!utest(sload_rec(base + (size_t)REC_STRIDE * j), j, in)) break;
+            }
         } else if (UL2) {
             for (uint32_t j = 0; j < uc; j += 2) {
                 TriRec r0, r1;
@@ -463,6 +627,16 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             if (!((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f)))
                 if (!test(load_rec(S, first + j))) break;
         }
+    } else if (LC && count <= (uint32_t)LC_MAXREFS) { // the mask's references, pipelined one ahead
+        uint32_t m = lmask;
+        TriRec nx;
+        if (m) nx = load_rec(S, first + (uint32_t)__builtin_ctz(m));
+        while (m) {
+            m &= m - 1u;
+            const TriRec r = nx;
+            if (m) nx = load_rec(S, first + (uint32_t)__builtin_ctz(m));
+            if (!test(r)) break;
+        }
     } else if (CULL) { // boxes pipelined one ahead; a record only for a sample inside its box
         if (!lin) count = 0;
         float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -488,23 +662,22 @@ __device__ __forceinline__ uint32_t trav_round(const DevScene &S, uint2 *ring, u
             if (!test(r)) break;
         }
     }
-    if (occluded) return ST_OCCLUDED;
+    if (pf) pt3 = prof_now();
+    if (occluded) {
+        prof_out();
+        return ST_OCCLUDED;
+    }
     if (found) {
         d = mk(bx, by, __uint_as_float(tri));
+        prof_out();
         return ST_HIT;
     }
-    if (T.sp == 0) return shadow ? ST_VISIBLE : ST_MISS;
-    T.sp--;
-    uint2 e;
-    if (T.nl) {
-        e = ring[(T.sp & (R - 1)) * bdim + tid];
-        T.nl--;
-    } else {
-        e = gstk[(size_t)T.sp * gstride + gid];
+    if (T.sp == 0) {
+        prof_out();
+        return shadow ? ST_VISIBLE : ST_MISS;
     }
-    T.node = e.x;
-    T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
-    T.tmax = __uint_as_float(e.y);
+    pop_entry();
+    prof_out();
     return shadow ? ST_SHADOW : ST_CLOSEST;
 }
 

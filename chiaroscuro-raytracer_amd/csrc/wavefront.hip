@@ -180,7 +180,8 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // CULL (camera instantiation only): triangle tests skipped by the screen-space cull
 // boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0, int PLANE = 0>
+          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0,
+          bool PROF = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
@@ -197,6 +198,8 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     uint32_t *work = SHADOW ? work_shadow(W, g) : work_closest(W, g);
     const float4 *rays = SHADOW ? W.sray : W.ray[g & 1];
     Ctr c = {};
+    Diag dg = {};
+    dg.on = FULL && ((A.diag_kinds >> (SHADOW ? TK_SHADOW : (CAM ? TK_CAMERA : TK_CLOSEST))) & 1u);
     uint32_t state = ST_NEED_WORK, idx = 0, exclude = 0, issued = 0;
     f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
     float csx = 0.f, csy = 0.f;
@@ -206,6 +209,8 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     // XCD partition (WfArgs::xcd): wave-uniform range part = xs % 256, WF_XCDS ranges tried
     // in turn (xs / 256 of them drained); one register, the rest is derived at refill
     uint32_t xs = blockIdx.x % WF_XCDS;
+    Prof pf = {0, 0, 0, 0, 0};
+    const uint64_t pstart = PROF ? prof_now() : 0;
     for (;;) {
         const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
         if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= refill)) {
@@ -248,6 +253,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                             W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
                         } else if (issued++, trav_begin(S, o, d, SHADOW, r1.w, T)) {
                             state = busy_st;
+                            if (FULL) diag_begin(&dg);
                         } else if (SHADOW) {
                             W.occ[idx] = 0u; // culled: visible (kdtree.cpp:285-287)
                         } else {
@@ -262,9 +268,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE>(
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC>(A.lc_debug, 
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
-                A.cull_node);
+                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr);
             if (r != busy_st) {
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
@@ -273,6 +279,12 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                 state = ST_NEED_WORK;
             }
         }
+    }
+    if (PROF && (threadIdx.x & 63u) == 0 && ((A.diag_kinds >> (SHADOW ? TK_SHADOW : TK_CLOSEST)) & 1u)) {
+        // cycles per wave: trav_round phases, the loop's total (the kinds of "diag_kinds")
+        const uint64_t tot = prof_now() - pstart;
+        const uint64_t v[6] = {pf.desc, pf.cull, pf.test, pf.pop, pf.calls, tot};
+        for (int i = 0; i < 6; i++) atomicAdd(&A.counters[CTR_DIAG + i], (unsigned long long)v[i]);
     }
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
     else c.closest = issued;
@@ -287,6 +299,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
             if ((threadIdx.x & 63) == 0 && x) atomicAdd(&base[i], x);
         }
+        diag_flush(A.counters, dg);
     }
 }
 
@@ -603,7 +616,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
         }
         if (busy) {
             const bool shadow = state == ST_SHADOW;
-            const uint32_t r = trav_round<R, FULL, 1, false, true, true>(S, ring_lds, W.gstack, W.gstride, gid, o, d,
+            const uint32_t r = trav_round<R, FULL, 1, false, true, true>(A.lc_debug, S, ring_lds, W.gstack, W.gstride, gid, o, d,
                                                                         shadow, exclude, T, c);
             if (r != (shadow ? ST_SHADOW : ST_CLOSEST)) state = r;
         }
@@ -914,7 +927,25 @@ static const WfVariant kWf[] = {
     // 18: 17 with two camera rays per lane (packets of 128 rays: the scalar control per node
     // shared by twice the rays)
     {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1}};
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1},
+    // 19: 18 whose secondary closest and shadow traces skip the references a leaf's cull record
+    // (leafcull.hpp: two normal groups, each a box and a normal cone) excludes for the ray
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 8, 0, 2, 1},
+    // 20: 19 whose lanes pass a leaf with every reference excluded and descend to the next one
+    // in the same traversal round
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 8, 0, 2, 1},
+    // 21 / 22: 19 / 20 at 6 waves per SIMD (80 VGPRs: no spills)
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
+     wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 6, 0, 2, 1},
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
+     wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 6, 0, 2, 1},
+    // 23 / 24: 18 / 19 with the phase clock of the secondary and shadow traces (measurement only)
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>, 8, 8, 0, 2, 1},
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>, 8, 8, 0, 2, 1}};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
                                    0, 0};

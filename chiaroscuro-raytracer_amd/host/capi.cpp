@@ -330,6 +330,7 @@ int chiaro_preview_key(chiaro_preview *p, int key, float dt, int shift) {
             case CHIARO_KEY_D: P.move(RIGHT, dt, shift != 0); break;
             case CHIARO_KEY_E: P.move(UPWARD, dt, shift != 0); break;
             case CHIARO_KEY_Q: P.move(DOWNWARD, dt, shift != 0); break;
+            case CHIARO_KEY_SHIFT: P.shiftState(shift != 0); break;
             default: return CR_E_INVALID;
             }
             return CR_OK;

@@ -93,11 +93,17 @@ void PreviewSession::exposureDown() {
     updateScreen();
 }
 
-// src/openglPreview.cpp:178-195
+// src/openglPreview.cpp:178-197: the movement keys move at the speed the previous frame
+// left, and only then does the frame set the speed from the shift key for the next one
 void PreviewSession::move(CameraMovement d, float deltaTime, bool fast) {
     if (showRender) return;
-    camera.MovementSpeed = fast ? 30.f : 2.5f;
     camera.ProcessKeyboard(d, deltaTime);
+    camera.MovementSpeed = fast ? 30.f : 2.5f;
+}
+// a frame with no movement key (src/openglPreview.cpp:193-196 alone)
+void PreviewSession::shiftState(bool fast) {
+    if (showRender) return;
+    camera.MovementSpeed = fast ? 30.f : 2.5f;
 }
 void PreviewSession::look(float xoffset, float yoffset) {
     if (!showRender) camera.ProcessMouseMovement(xoffset, yoffset);

@@ -40,6 +40,7 @@ class PreviewSession {
     void toggleView() { showRender = !showRender; } // TAB
     // WASDQE / mouse / scroll: ignored while the render is shown, as processInputs does
     void move(CameraMovement d, float deltaTime, bool fast = false);
+    void shiftState(bool fast);
     void look(float xoffset, float yoffset);
     void scroll(float yoffset);
     // Screen::updateScreen: normalizeImage() with the scene's exposure, texture = getData()

@@ -241,6 +241,11 @@ int cr_get_trace_stats(cr_ctx *ctx, cr_trace_stats *out);
  * the wave_* diagnostics; 0 = only the per-query tallies, for timed launches),
  * "block", "waves_per_cu".  Returns CR_OK or CR_E_INVALID. */
 int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
+/* Diagnostics of the last counting render (wavefront trace kernels, option
+ * "diag_kinds" = mask of trace kinds 1 camera / 2 closest / 4 shadow): leaf-round
+ * shapes (what staging a wave's leaves in LDS would load) and a per-lane census of
+ * repeated any-segment triangle misses.  Up to n of the DIAG_* values (csrc/kernels.hpp). */
+int cr_get_diag(cr_ctx *ctx, uint64_t *out, int n);
 int cr_synchronize(cr_ctx *ctx);
 
 /* ---------------------------------------------------------- multi-GPU --
@@ -275,6 +280,10 @@ cr_group *cr_group_create(int ngpus, const int *devices);
 void cr_group_destroy(cr_group *g);
 const char *cr_group_last_error(cr_group *g);
 int cr_group_size(cr_group *g);
+/* 1 when every rank has a device and, for distinct devices, the RCCL communicator
+ * exists; 0 after a failed create (cr_group_last_error says why; cr_group_destroy
+ * is still required). */
+int cr_group_ok(cr_group *g);
 int cr_group_upload_scene(cr_group *g, const cr_scene_desc *desc);
 int cr_group_set_option(cr_group *g, const char *key, int64_t value); /* on every rank's ctx */
 /* cr_render across the group: layer p->layer of the whole frame (p->rank / p->nranks

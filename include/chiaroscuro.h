@@ -98,7 +98,9 @@ enum {
     CHIARO_KEY_TAB = 1,   /* toggle render / model view                        */
     CHIARO_KEY_EQUAL = 2, /* exposure + 0.2, re-normalise                      */
     CHIARO_KEY_MINUS = 3, /* exposure - 0.2, re-normalise                      */
-    CHIARO_KEY_W = 4, CHIARO_KEY_S = 5, CHIARO_KEY_A = 6, CHIARO_KEY_D = 7, CHIARO_KEY_E = 8, CHIARO_KEY_Q = 9
+    CHIARO_KEY_W = 4, CHIARO_KEY_S = 5, CHIARO_KEY_A = 6, CHIARO_KEY_D = 7, CHIARO_KEY_E = 8, CHIARO_KEY_Q = 9,
+    /* a frame without a movement key: only the shift state (the speed of the next move) */
+    CHIARO_KEY_SHIFT = 10
 };
 chiaro_preview *chiaro_preview_create(chiaro_scene *s, chiaro_raytracer *r);
 /* one key press; dt = frame time for the movement keys, shift = LEFT_SHIFT held */

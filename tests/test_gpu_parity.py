@@ -108,7 +108,7 @@ def test_wavefront_xcd_partition_bitexact(ca, sponza, nanobox, xcd, sort_min, va
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     """Every wavefront trace build (LDS ring depth, occupancy, scalar loads for
     wave-uniform nodes / leaves) renders the same bits."""
@@ -132,7 +132,7 @@ CULL_CAMS = {
 }
 
 
-@pytest.mark.parametrize("variant", [14, 15, 16, 17, 18])
+@pytest.mark.parametrize("variant", [14, 15, 16, 17, 18, 19, 20, 22])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell", "cornell_box"])
 def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_mm, cfg, variant):
     """Trace builds 14 / 15 / 16: the camera-ray trace skips Moller-Trumbore tests, leaves
@@ -169,7 +169,7 @@ def test_camera_cull_bitexact(ca, po, scenes, sponza, nanobox, cornell, cornell_
         pair.dev.set_option("variant", -1)
 
 
-@pytest.mark.parametrize("variant", [15, 17, 18])
+@pytest.mark.parametrize("variant", [15, 17, 18, 19])
 @pytest.mark.parametrize("cfg", ["sponza", "nanobox", "cornell"])
 def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg, variant):
     """The default build (camera-ray cull boxes) at 12 random cameras per scene: eyes
@@ -204,7 +204,7 @@ def test_camera_cull_fuzz_bitexact(ca, sponza, nanobox, cornell, cfg, variant):
         pair.dev.set_option("variant", -1)
 
 
-@pytest.mark.parametrize("variant", [17, 18])
+@pytest.mark.parametrize("variant", [17, 18, 19])
 def test_packet_camera_eye_on_split_plane(ca, sponza, cornell, variant):
     """Build 17's packet camera trace needs every camera ray to agree on a node's near
     child; an eye exactly on a split plane breaks that (kdtree.cpp:262 then decides by
@@ -588,3 +588,23 @@ def test_c5_eight_rank_tile32_split_sponza(ca, sponza):
             assert_bitwise(frame.cpu().numpy(), o, "sponza 8-rank tile-32 layer %d" % layer)
     finally:
         sponza.dev.set_option("sample_buf_bytes", 4 << 30)
+
+
+@pytest.mark.parametrize("variant", [15, 18, 19])
+def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
+    """A model without triangles still renders through the culling camera traces: the
+    cull boxes are built for an empty reference list too (every sample outside), so
+    the packet / subtree-cull kernels never read a null box buffer.  Every camera ray
+    misses; the frame is the background, as the oracle's."""
+    empty = tmp_path / "empty.obj"
+    empty.write_text("# no faces\nv 0 0 0\nv 1 0 0\nv 0 1 0\n")
+    pair = Pair(ca, po, scenes.config_rtc("cornell"), "input", str(empty))
+    assert pair.model.num_triangles == 0
+    pair.dev.set_option("kernel", 2)
+    pair.dev.set_option("variant", variant)
+    cam = pair.camera(ca, 24, 16)
+    p = ca.render_params(24, 16, 2, 3, 0xC41A05C0, background=(0.25, 0.5, 0.75))
+    g = pair.dev.render(cam, p)
+    o, oc = pair.oracle.render(cam.as_array(), 24, 16, 2, 3, 0xC41A05C0, bg=(0.25, 0.5, 0.75))
+    assert_bitwise(g, o, "triangle-less scene, variant %d" % variant)
+    assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2

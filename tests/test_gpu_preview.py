@@ -62,3 +62,25 @@ def test_preview_progressive_render(ca, po, scenes):
     pv.key("R")  # new camera: accumulation restarts
     assert rt.layers == 1
     assert_bitwise(rt.pixels, oracle_layers(pv.state(), 1), "preview after move")
+
+
+def test_preview_shift_applies_to_the_next_move(ca, scenes):
+    """src/openglPreview.cpp:181-196: a frame's movement keys move at the speed the
+    previous frame left (2.5, or 30 with LEFT_SHIFT held), and only then does the
+    frame set the speed from the shift key.  Toggling shift between moves must
+    therefore change the NEXT move's step, not this one's."""
+    sc = ca.Scene(scenes.config_rtc("cornell"), "xres", "16", "yres", "16", "samples", "1")
+    rt = ca.RayTracer(ca.Model(sc), sc)
+    pv = ca.Preview(sc, rt)
+    front = pv.state()["front"].astype(np.float32)
+    pos = pv.state()["position"].astype(np.float32)
+    # (key, dt, shift) -> the speed this move uses: the one the previous frame left
+    speed = np.float32(2.5)
+    for key, dt, shift in (("W", 0.5, False), ("W", 0.5, True), ("W", 0.25, False), ("SHIFT", 0.0, True),
+                           ("W", 0.125, True), ("S", 0.5, False)):
+        pv.key(key, dt=dt, shift=shift)
+        if key != "SHIFT":
+            v = np.float32(speed * np.float32(dt))  # ProcessKeyboard's velocity (src/camera.cpp:33)
+            pos = (pos + front * v) if key == "W" else (pos - front * v)
+        speed = np.float32(30.0 if shift else 2.5)
+        np.testing.assert_array_equal(pv.state()["position"], pos.astype(np.float32), err_msg=key)

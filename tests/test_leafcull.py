@@ -1,0 +1,59 @@
+"""CPU checks of the leaf cull records of trace build 19 (csrc/leafcull.hpp).
+
+The secondary closest and shadow traces of build 19 skip a leaf's Moller-Trumbore
+test when the leaf's cull record proves, for the ray's unit direction and its test
+segment [0, tmax], that the test cannot accept: the triangle's normal lies in a cone
+the ray is not grazing, and the segment misses the group's box padded by the rounding
+bound.  tests/native/leafcull_check.cpp evaluates the test as the kernels and the
+oracle do (IEEE single, no FMA contraction) on random and adversarial leaves (walls,
+boxes, column fans, slivers, degenerate triangles) and rays (aimed at edges and
+vertices a few ulps off, from the triangle planes, grazing, in-plane far to the side,
+tmax a few ulps around the hit), with inv perturbed by 2 ulp as v_rcp_f32 may, and
+counts accepted tests the mask dropped: there must be none.  Without the margins the
+same run finds such tests (test_margins_are_needed), so the check has teeth.
+"""
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+SRC = ROOT / "tests" / "native" / "leafcull_check.cpp"
+HDR = ROOT / "chiaroscuro-raytracer_amd" / "csrc" / "leafcull.hpp"
+
+
+def _build(tmp_path, header_dir):
+    exe = tmp_path / "leafcull_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", str(header_dir), "-o", str(exe), str(SRC)],
+                   check=True)
+    return exe
+
+
+def _run(exe, seed, leaves):
+    r = subprocess.run([str(exe), str(seed), str(leaves)], capture_output=True, text=True, timeout=600)
+    m = re.search(r"violations (\d+) tested (\d+) accepted (\d+) skipped (\d+)", r.stdout)
+    assert m, r.stdout + r.stderr
+    return [int(v) for v in m.groups()]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_leaf_cull_is_conservative(tmp_path, seed):
+    exe = _build(tmp_path, HDR.parent)
+    viol, tested, accepted, skipped = _run(exe, seed, 6000)
+    assert tested > 30_000_000 and accepted > 500_000 and skipped > 3_000_000
+    assert viol == 0
+
+
+def test_margins_are_needed(tmp_path):
+    """Without the rounding margins (u = 0, no slab / coordinate slack) the checker
+    finds accepted tests the mask would drop."""
+    src = HDR.read_text()
+    src = src.replace("const float u = 0x1p-24f;", "const float u = 0.0f;")
+    src = src.replace("4.f * u * mb + 1e-20f;", "0.f;").replace("(1.f + 4.f * u) + 1e-20f;", "(1.f + 4.f * u);")
+    assert "u = 0.0f" in src and "0.f;" in src
+    (tmp_path / "hdr").mkdir()
+    (tmp_path / "hdr" / "leafcull.hpp").write_text(src)
+    exe = _build(tmp_path, tmp_path / "hdr")
+    viol = _run(exe, 3, 6000)[0]
+    assert viol > 100
