@@ -178,6 +178,59 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+class GpuBackend:
+    """What a rank runs on: one MI355X per rank, RCCL (the nccl backend) between
+    ranks, the C-ABI device (chiaroscuro_amd.Device) with the scene in HBM.
+
+    The rank loop below (run_rank) only talks to this object and to the device it
+    makes, so the multi-rank protocol -- spawn, WORLD_SIZE check, per-rank timing,
+    slowest-rank step, gather, JSON line -- can be exercised on the CPU: a test
+    names a stand-in backend in CHIARO_BENCH_BACKEND ("path/to/file.py:factory";
+    tests/bench_cpu_backend.py, gloo + an oracle-backed device).  The product never
+    ships or imports a stand-in."""
+
+    name = "gpu"
+    device = "cuda"
+    dist_backend = "nccl"
+
+    def init_rank(self, world, local):
+        import torch
+        torch.cuda.set_device(local)
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            return dist
+        return None
+
+    def synchronize(self):
+        import torch
+        torch.cuda.synchronize()
+
+    def stream(self):
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+
+    def make_device(self, index, info, model, kd, opts):
+        import chiaroscuro_amd as ca
+        dev = ca.Device(index)
+        for key, val in opts:
+            dev.set_option(key, val)
+        dev.upload(kd.describe())
+        return dev
+
+
+def load_backend():
+    spec = os.environ.get("CHIARO_BENCH_BACKEND")
+    if not spec:
+        return GpuBackend()
+    import importlib.util
+    path, _, attr = spec.rpartition(":")
+    mod_spec = importlib.util.spec_from_file_location("chiaro_bench_backend", path)
+    mod = importlib.util.module_from_spec(mod_spec)
+    mod_spec.loader.exec_module(mod)
+    return getattr(mod, attr)()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (= rank processes) of one node, default 1")
@@ -195,13 +248,22 @@ def main():
                     help="cr_set_option before the scene upload (experiments; the default build is timed without)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
+    ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         sys.exit(spawn_ranks(args.gpus))
     if args.gpus is not None and args.gpus != world:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    out = run_rank(args, world, load_backend())
+    if out is not None:
+        print(json.dumps(out), flush=True)
 
+
+def run_rank(args, world, backend):
+    """One rank of the benchmark (the whole job when world == 1); returns the JSON
+    object on rank 0, None elsewhere."""
     import torch
 
     import chiaroscuro_amd as ca
@@ -210,29 +272,20 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist = backend.init_rank(world, local)
+    if dist is not None:
         assert dist.get_world_size() == world, (dist.get_world_size(), world)
         if rank == 0:
             log("bench: %d ranks, backend %s" % (dist.get_world_size(), dist.get_backend()))
-    dev_index = local
-    torch.cuda.set_device(dev_index)
 
     rtc = scenes.config_rtc(args.config)
     t0 = time.time()
-    scene = ca.Scene(rtc)
+    scene = ca.Scene(rtc, *(("xres", args.res.split("x")[0], "yres", args.res.split("x")[1]) if args.res else ()))
     info = scene.info
     model = ca.Model(scene)
     kd = ca.KDTree(model, scene)
-    dev = ca.Device(dev_index)
-    for kv in args.opt:
-        key, val = kv.split("=", 1)
-        dev.set_option(key, int(val, 0))
-    dev.upload(kd.describe())
+    opts = [(kv.split("=", 1)[0], int(kv.split("=", 1)[1], 0)) for kv in args.opt]
+    dev = backend.make_device(local, info, model, kd, opts)
     if args.kernel >= 0:
         dev.set_option("kernel", args.kernel)
     if args.variant >= 0:
@@ -243,8 +296,8 @@ def main():
     spp = args.spp or info["samples"]
     cam = ca.camera(info["VP"], info["LA"], info["UP"], info["yview"], xres, yres)
     tile = 32
-    stream = torch.cuda.current_stream().cuda_stream
-    fr = DistributedFrame(dev, xres, yres, rank, world, tile, dist, gather=args.gather)
+    stream = backend.stream()
+    fr = DistributedFrame(dev, xres, yres, rank, world, tile, dist, device=backend.device, gather=args.gather)
 
     totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0,
               "trace_ms": [0.0] * 4, "trace_launches": [0] * 4}
@@ -278,20 +331,23 @@ def main():
             log("warmup %d done" % w)
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    backend.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(layer, True)
         layer += 1
         if rank == 0:
             log("step %d: %.3fs elapsed" % (s, time.perf_counter() - t0))
-    torch.cuda.synchronize()
+    backend.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.save_frame and fr.frame is not None:
+        import numpy as np
+        np.save(args.save_frame, fr.frame.cpu().numpy())
     # per rank: wall time, device time of its render passes (HIP events), rays
     mine = torch.tensor([elapsed, totals["kernel_ms"] / max(totals["launches"], 1), totals["rays"]],
-                        dtype=torch.float64, device="cuda")
+                        dtype=torch.float64, device=backend.device)
     if dist:
         per_rank = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(per_rank, mine)
@@ -305,11 +361,11 @@ def main():
     # counting pass (untimed): algorithmic bytes of one launch of this rank
     dev.set_option("counters", 1)
     pc = ca.render_params(xres, yres, spp, k, seed, layer=first_timed, rank=rank, nranks=world, tile=tile)
-    scratch = torch.zeros((yres, xres, 3), dtype=torch.float32, device="cuda")
+    scratch = torch.zeros((yres, xres, 3), dtype=torch.float32, device=backend.device)
     if world == 1:
         dev.render_device(cam, pc, scratch.data_ptr(), stream)
     else:
-        scratch_tiles = torch.zeros((fr.layout.max_tiles, tile, tile, 3), dtype=torch.float32, device="cuda")
+        scratch_tiles = torch.zeros((fr.layout.max_tiles, tile, tile, 3), dtype=torch.float32, device=backend.device)
         dev.render_tiles_device(cam, pc, scratch_tiles.data_ptr(), stream)
     cc = dev.counters()
     cts = dev.trace_stats() if wavefront else None
@@ -317,6 +373,7 @@ def main():
     totals["tritest"] = cc["tritest"]
     totals["count_rays"] = cc["closest"] + cc["shadow"]
 
+    out = None
     if rank == 0:
         value = rays_all / elapsed / 1e6
         kms = totals["kernel_ms"] / max(totals["launches"], 1)
@@ -390,11 +447,12 @@ def main():
                 v = views.get(kind)
                 return ((v["avg_launch_ms"] * v["launches"] / max(totals["launches"], 1)) if v else 0.0), "live"
             ranked = {k: per_pass_ms(k) for k in ("camera", "closest", "shadow") if views.get(k)}
+        if wavefront and ranked:
             dom_kind = max(ranked, key=lambda k: ranked[k][0])
             dom = views[dom_kind]
             roofline = issue_roofline(dom, (issue or {}).get(dom_kind), views, issue, pass_view, dom_kind)
             roofline["dominant_by"] = {k: {"ms_per_pass": round(v[0], 3), "from": v[1]} for k, v in ranked.items()}
-        else:
+        else:  # (no per-kind trace launches: the other kernels, or a backend without them)
             roofline = {"bound": "hbm", "achieved": round(pass_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(pass_gbs / HBM_PEAK_GBS, 5), "traffic": pass_view["traffic"],
                         "kernel": pass_view["kernels"], "kernel_ms": round(kms, 3),
@@ -424,9 +482,11 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        if backend.name != "gpu":
+            out["backend"] = backend.name
     if dist:
         dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 if __name__ == "__main__":

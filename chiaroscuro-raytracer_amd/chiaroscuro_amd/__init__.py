@@ -56,6 +56,32 @@ class CrCounters(C.Structure):
         return {n: int(getattr(self, n)) for n in COUNTER_NAMES}
 
 
+class Checkpoint(C.Structure):
+    """chiaro_checkpoint (include/chiaroscuro.h): the progressive state of a frame."""
+    _fields_ = [("xres", C.c_uint32), ("yres", C.c_uint32), ("samples", C.c_uint32), ("k", C.c_uint32),
+                ("seed", C.c_uint32), ("layers", C.c_uint32), ("eye", f3), ("center", f3), ("up", f3),
+                ("yview", C.c_float), ("background", f3), ("scene", C.c_uint64)]
+
+
+def checkpoint_write(path, header: "Checkpoint", pixels: np.ndarray):
+    """chiaro_checkpoint_write: the frame [yres][xres][3] and its header, atomically."""
+    px = np.ascontiguousarray(pixels, np.float32)
+    assert px.shape == (header.yres, header.xres, 3), (px.shape, header.yres, header.xres)
+    if libs()[1].chiaro_checkpoint_write(str(path).encode(), C.byref(header), _ptr(px)):
+        raise RuntimeError("checkpoint_write: " + _host_err())
+
+
+def checkpoint_read(path):
+    """chiaro_checkpoint_read: (header, frame [yres][xres][3])."""
+    h = Checkpoint()
+    if libs()[1].chiaro_checkpoint_read(str(path).encode(), C.byref(h), None):
+        raise RuntimeError("checkpoint_read: " + _host_err())
+    px = np.zeros((h.yres, h.xres, 3), np.float32)
+    if libs()[1].chiaro_checkpoint_read(str(path).encode(), C.byref(h), _ptr(px)):
+        raise RuntimeError("checkpoint_read: " + _host_err())
+    return h, px
+
+
 class CrKdNode(C.Structure):
     _fields_ = [("split", C.c_float), ("axis", C.c_uint32), ("child_or_first", C.c_uint32), ("count", C.c_uint32)]
 
@@ -112,7 +138,7 @@ _host = None
 # Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
                "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_tile_origin", "cr_intersect",
-               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize", "cr_get_diag",
+               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize", "cr_get_diag", "cr_trace_build_available",
                "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap",
                "cr_comm_unique_id", "cr_comm_init", "cr_comm_destroy", "cr_render_dist_device",
                "cr_device_count", "cr_group_create", "cr_group_destroy", "cr_group_last_error", "cr_group_size", "cr_group_ok",
@@ -127,6 +153,8 @@ HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_g
                 "chiaro_raytracer_data", "chiaro_raytracer_maxval", "chiaro_raytracer_layers",
                 "chiaro_raytracer_counters", "chiaro_raytracer_normalize", "chiaro_raytracer_export",
                 "chiaro_raytracer_ctx", "chiaro_raytracer_destroy", "chiaro_camera",
+                "chiaro_raytracer_checkpoint", "chiaro_raytracer_resume", "chiaro_kdtree_fingerprint",
+                "chiaro_checkpoint_write", "chiaro_checkpoint_read",
                 "chiaro_preview_create", "chiaro_preview_key", "chiaro_preview_mouse", "chiaro_preview_scroll",
                 "chiaro_preview_texture", "chiaro_preview_state", "chiaro_preview_destroy",
                 "chiaro_preview_camera_replay")
@@ -179,6 +207,7 @@ def libs():
     _sig(hip, "cr_get_trace_stats", C.c_int, [P, C.POINTER(CrTraceStats)])
     _sig(hip, "cr_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
     _sig(hip, "cr_get_diag", C.c_int, [P, C.POINTER(C.c_uint64), C.c_int])
+    _sig(hip, "cr_trace_build_available", C.c_int, [C.c_int])
     _sig(hip, "cr_synchronize", C.c_int, [P])
     _sig(hip, "cr_tonemap_setup", None, [C.c_float] * 5 + [C.POINTER(CrTonemapParams)])
     _sig(hip, "cr_tonemap_device", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32, P, P, P])
@@ -233,6 +262,11 @@ def libs():
     _sig(host, "chiaro_raytracer_normalize", C.c_int, [P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float])
     _sig(host, "chiaro_raytracer_export", C.c_int, [P, C.c_char_p])
     _sig(host, "chiaro_raytracer_ctx", P, [P])
+    _sig(host, "chiaro_raytracer_checkpoint", C.c_int, [P, C.c_char_p])
+    _sig(host, "chiaro_raytracer_resume", C.c_int, [P, C.c_char_p])
+    _sig(host, "chiaro_kdtree_fingerprint", C.c_uint64, [P])
+    _sig(host, "chiaro_checkpoint_write", C.c_int, [C.c_char_p, C.POINTER(Checkpoint), FP])
+    _sig(host, "chiaro_checkpoint_read", C.c_int, [C.c_char_p, C.POINTER(Checkpoint), FP])
     _sig(host, "chiaro_raytracer_destroy", None, [P])
     _sig(host, "chiaro_camera", C.c_int, [FP, FP, FP, C.c_float, C.c_uint32, C.c_uint32, C.POINTER(CrCamera)])
     _sig(host, "chiaro_preview_create", P, [P, P])
@@ -363,6 +397,10 @@ class KDTree:
         if not self._h:
             raise ValueError("KDTree: " + _host_err())
 
+    def fingerprint(self) -> int:
+        """chiaro_kdtree_fingerprint: which triangles, in which tree (checkpoints record it)."""
+        return int(libs()[1].chiaro_kdtree_fingerprint(self._h))
+
     def export(self) -> dict:
         _, host = libs()
         n, r = host.chiaro_kdtree_num_nodes(self._h), host.chiaro_kdtree_num_refs(self._h)
@@ -491,6 +529,16 @@ class Device:
 
     def set_option(self, key: str, value: int):
         self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")
+
+    @staticmethod
+    def trace_builds(upto: int = 64) -> list:
+        """The wavefront trace builds compiled in (cr_trace_build_available)."""
+        return [b for b in range(upto) if libs()[0].cr_trace_build_available(b)]
+
+    @staticmethod
+    def device_count() -> int:
+        """cr_device_count: HIP devices this process sees (0 without a GPU)."""
+        return int(libs()[0].cr_device_count())
 
     # multi-process frame split (one process per GPU, RCCL inside the library)
     @staticmethod
@@ -625,6 +673,16 @@ class RayTracer:
         c = CrCounters()
         libs()[1].chiaro_raytracer_counters(self._h, C.byref(c))
         return c.as_dict()
+
+    def checkpoint(self, path):
+        """Save the progressive state (layers, camera, running average) -- chiaro_raytracer_checkpoint."""
+        if libs()[1].chiaro_raytracer_checkpoint(self._h, str(path).encode()):
+            raise RuntimeError("checkpoint: " + _host_err())
+
+    def resume(self, path):
+        """Continue a saved progressive render: the next rayTrace at its camera is layer layers + 1."""
+        if libs()[1].chiaro_raytracer_resume(self._h, str(path).encode()):
+            raise RuntimeError("resume: " + _host_err())
 
     def __del__(self):
         if getattr(self, "_h", None) and _host is not None:

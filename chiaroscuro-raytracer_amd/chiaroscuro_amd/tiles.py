@@ -89,6 +89,45 @@ class DistributedFrame:
             dist.broadcast_object_list(uid, src=0)
             dev.comm_init(nranks, rank, uid[0])
 
+    def save(self, path, header):
+        """Checkpoint the frame (rank 0; a no-op elsewhere): header is a
+        chiaroscuro_amd.Checkpoint describing the frame (layers = the last layer
+        rendered, camera, sampling, scene fingerprint).  The file is the one
+        RayTracer.checkpoint writes (include/chiaroscuro.h)."""
+        if self.frame is None:
+            return
+        from . import checkpoint_write
+        checkpoint_write(path, header, self.frame.cpu().numpy())
+
+    def resume(self, path, expect) -> int:
+        """Continue from a checkpoint: rank 0 loads the frame, every rank gets the
+        layer count (the next layer to render is that + 1).  `expect` is the
+        Checkpoint of this run (layers ignored): another frame, sampling or scene is
+        refused, as RayTracer.resume refuses it."""
+        import torch
+        layers = torch.zeros(1, dtype=torch.int64)
+        err = ""
+        if self.rank == 0:
+            from . import checkpoint_read
+            h, px = checkpoint_read(path)
+            keys = ("xres", "yres", "samples", "k", "seed", "scene")
+            if any(getattr(h, k) != getattr(expect, k) for k in keys) or list(h.background) != list(expect.background):
+                err = "resume: the checkpoint is of another frame / sampling / scene"
+            else:
+                self.frame.copy_(torch.from_numpy(px).to(self.frame.device))
+                layers[0] = h.layers
+        if self.layout.nranks > 1:
+            flag = torch.tensor([0 if not err else 1], dtype=torch.int64)
+            if self.dist.get_backend() == "nccl":
+                layers, flag = layers.cuda(), flag.cuda()
+            self.dist.broadcast(layers, src=0)
+            self.dist.broadcast(flag, src=0)
+            if int(flag.item()):
+                err = err or "resume: rank 0 refused the checkpoint"
+        if err:
+            raise ValueError(err)
+        return int(layers.item())
+
     def render_layer(self, cam, params, stream: int = 0):
         """params: chiaroscuro_amd.render_params(..., layer=L, rank, nranks, tile)."""
         L = self.layout

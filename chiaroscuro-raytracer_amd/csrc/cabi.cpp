@@ -103,6 +103,7 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.full_counters = c->full_counters;
     A.diag_kinds = c->diag_kinds;
     A.lc_debug = c->lc_debug;
+    A.lc_min = c->lc_min;
     // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783);
     // re-swept under leaf-keyed queues (scripts/gpu_leaf_sweep.sh, 1080p x 128 spp, closest /
     // shadow): 56/48 397.4, 48/56 394.5, 48/48 395.9, 56/56 396.2 ms per pass; a rank of 8:
@@ -124,8 +125,11 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 17 = 15 whose camera rays traverse one packet (one pixel's 64 samples) per wave:
     // 429.3 vs 435.1 ms per pass (2 interleaved rounds), 416.5 vs 423.1 ms with wf_xcd 7;
     // 18 = 17 with two camera rays per lane (128-ray packets): camera trace 44.1 -> 40.5 ms,
-    // 409.7 -> 406.9 ms per pass
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 18 : 0);
+    // 409.7 -> 406.9 ms per pass;
+    // 26 = 18 whose secondary closest and shadow traces (and the tail) skip the references a
+    // leaf's cull record excludes for the ray (leafcull.hpp, packed fixed-pad form): shadow trace
+    // 58.2 -> 53.3 ms per launch, closest 99.8 -> 91.5 ms beside it, 391.5 -> 367 ms per pass
+    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 26 : 0);
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
@@ -138,6 +142,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     HIPCHK(hipSetDevice(c->device));
     cr::RenderArgs A{};
     fill_args(c, A, cam, p, out, mode);
+    if (c->kernel == 2 && !c->full_counters && !cr::wf_variant_available(A.variant))
+        return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
+                                         " is not compiled in (make ALL_VARIANTS=1)");
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     if (c->kernel == 0 || c->kernel == 2) {
         const bool wf = c->kernel == 2;
@@ -550,6 +557,24 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
             });
         for (auto &t : th) t.join();
     }
+    // ... and in the fixed-pad form: origins and vertices inside the padded box (+1: the 0.001 n offsets)
+    std::vector<float4> lcullf((size_t)cr::LC_REC * NN, make_float4(0.f, 0.f, 0.f, 0.f));
+    {
+        double db = 1.0, smax = 0.0;
+        for (int i = 0; i < 3; i++) {
+            db = std::max(db, std::max(std::fabs((double)d->box_min[i]), std::fabs((double)d->box_max[i])) + 1.0);
+            smax = std::max(smax, (double)d->box_max[i] - (double)d->box_min[i] + 2.0);
+        }
+        db *= 1.0001;
+        for (uint32_t i = 0; i < NN; i++)
+            cr::leaf_cull_fixed((const cr::LcFloat4 *)(lcull.data() + (size_t)cr::LC_REC * i), db, smax,
+                                (cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i));
+    }
+    std::vector<float4> lcullp((size_t)cr::LC_RECP * NN, make_float4(0.f, 0.f, 0.f, 0.f));
+    for (uint32_t i = 0; i < NN; i++)
+        cr::leaf_cull_pack((const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
+                           (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u,
+                           (cr::LcFloat4 *)(lcullp.data() + (size_t)cr::LC_RECP * i));
     std::vector<float4> tri((size_t)3 * nt), mn(nt), mkd(nt), mke(nt);
     std::vector<float2> muv((size_t)3 * nt);
     for (uint32_t t = 0; t < nt; t++) {
@@ -628,7 +653,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         free_scene(c);
         return rc;
     }
-    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, tri, &c->S.tri)) ||
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, lcullf, &c->S.lcullf)) || (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
         (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels))) {
@@ -693,6 +718,23 @@ int cr_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float 
     rc = run_render(c, cam, &q, c->d_accum, cr::MODE_BLEND, c->stream);
     if (rc) return rc;
     HIPCHK(hipMemcpy(accum_rgb_out, c->d_accum, elems * sizeof(float), hipMemcpyDeviceToHost));
+    return CR_OK;
+}
+
+int cr_set_accumulator(cr_ctx *c, uint32_t xres, uint32_t yres, const float *rgb) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!rgb || !xres || !yres) return fail(c, CR_E_INVALID, "null / empty accumulator");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t elems = (size_t)xres * yres * 3;
+    if (elems != c->accum_elems) {
+        if (c->d_accum) hipFree(c->d_accum);
+        c->d_accum = nullptr;
+        c->accum_elems = 0;
+        if (hipMalloc(&c->d_accum, elems * sizeof(float)) != hipSuccess) return fail(c, CR_E_OOM, "accumulator");
+        c->accum_elems = elems;
+    }
+    HIPCHK(hipMemcpy(c->d_accum, rgb, elems * sizeof(float), hipMemcpyHostToDevice));
     return CR_OK;
 }
 
@@ -861,6 +903,8 @@ int cr_get_trace_stats(cr_ctx *c, cr_trace_stats *out) {
     return CR_OK;
 }
 
+int cr_trace_build_available(int build) { return cr::wf_variant_available(build) ? 1 : 0; }
+
 int cr_get_diag(cr_ctx *c, uint64_t *out, int n) {
     if (!c || !out || n < 0) return CR_E_INVALID;
     for (int i = 0; i < n && i < cr::DIAG_N; i++) out[i] = c->last_diag[i];
@@ -874,6 +918,8 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
     else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
     else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
+    else if (!std::strcmp(key, "lc_min") && v >= 0 && v <= 33) c->lc_min = (uint32_t)v;
+    else if (!std::strcmp(key, "comm_timeout_ms") && v >= 1 && v <= 3600000) c->comm_timeout_ms = (uint32_t)v;
     else if (!std::strcmp(key, "variant") && v >= -1 && v < nvar) c->variant = (int)v; // -1 default; clamped per kernel
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
     else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
@@ -889,7 +935,11 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_dir_res") && v >= 1 && v <= 256 && (v & (v - 1)) == 0)
         c->wf_dir_res = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
+#ifdef CR_SORT_LIB
     else if (!std::strcmp(key, "wf_sort_lib") && (v == 0 || v == 1)) c->wf_sort_lib = (int)v;
+#else
+    else if (!std::strcmp(key, "wf_sort_lib") && v == 0) c->wf_sort_lib = 0; // (1: make SORT_LIB=1)
+#endif
     else if (!std::strcmp(key, "wf_lanes") && (v == 1 || v == 2)) c->wf_lanes = (int)v;
     else if (!std::strcmp(key, "wf_xcd") && v >= 0 && v <= 7) c->wf_xcd = (uint32_t)v;
     else if (!std::strcmp(key, "wf_leaf_keys") && (v == 0 || v == 1)) c->wf_leaf_keys = (int)v;

@@ -57,6 +57,7 @@ struct cr_ctx {
     int kernel = 2;
     int full_counters = 1;
     int lc_debug = 0;                      // measurement only (RenderArgs::lc_debug)
+    uint32_t lc_min = 0;                   // RenderArgs::lc_min
     uint32_t diag_kinds = 0;               // counting renders: trace kinds of the DIAG_* census (1 << TK_*)
     unsigned long long last_diag[cr::DIAG_N] = {};
     int variant = -1;       // -1: the kernel's default build
@@ -102,6 +103,7 @@ struct cr_ctx {
     // communicator per process, this rank's compact tile buffer, the root's gather area
     ncclComm_t comm = nullptr;
     int comm_rank = 0, comm_nranks = 1;
+    uint32_t comm_timeout_ms = 120000; // cr_comm_init: peers must join within this (option "comm_timeout_ms")
     float *d_tiles = nullptr, *d_gathered = nullptr;
     size_t tiles_bytes = 0, gathered_bytes = 0;
 };

@@ -45,6 +45,14 @@ void release_dist(cr_ctx *c) {
     c->tiles_bytes = c->gathered_bytes = 0;
 }
 
+// A non-blocking communicator's state once its pending work is enqueued (or failed).
+static ncclResult_t nccl_settle(ncclComm_t comm) {
+    ncclResult_t st = ncclInProgress;
+    while (ncclCommGetAsyncError(comm, &st) == ncclSuccess && st == ncclInProgress)
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    return st;
+}
+
 // Wait for the stream's work while watching the communicator's asynchronous error.
 static int wait_comm(cr_ctx *c, ncclComm_t comm, hipStream_t st, const char *what) {
     for (;;) {
@@ -109,9 +117,32 @@ int cr_comm_init(cr_ctx *c, int nranks, int rank, const uint8_t *id) {
     release_dist(c);
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
+    // non-blocking init, polled against a deadline: a rank whose peers never join (a dead
+    // launcher, a wrong nranks, one GPU for two ranks) gets CR_E_COMM instead of a hang
     ncclComm_t comm = nullptr;
-    const ncclResult_t r = ncclCommInitRank(&comm, nranks, uid, rank);
-    if (r != ncclSuccess) return nccl_fail(c, r, "ncclCommInitRank");
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, uid, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        if (comm) ncclCommAbort(comm);
+        return nccl_fail(c, r, "ncclCommInitRankConfig");
+    }
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(c->comm_timeout_ms);
+    for (;;) {
+        ncclResult_t st = ncclInProgress;
+        if ((r = ncclCommGetAsyncError(comm, &st)) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress)) {
+            ncclCommAbort(comm);
+            return nccl_fail(c, r != ncclSuccess ? r : st, "ncclCommInitRankConfig");
+        }
+        if (st == ncclSuccess) break;
+        if (std::chrono::steady_clock::now() > deadline) {
+            ncclCommAbort(comm);
+            return fail(c, CR_E_COMM, "cr_comm_init: the " + std::to_string(nranks) +
+                                          "-rank communicator did not form within " +
+                                          std::to_string(c->comm_timeout_ms) + " ms (peers missing)");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
     c->comm = comm;
     c->comm_rank = rank;
     c->comm_nranks = nranks;
@@ -153,13 +184,16 @@ int cr_render_dist_device(cr_ctx *c, const cr_camera *cam, const cr_render_param
     if (int rc = run_render(c, cam, &q, mine, cr::MODE_TILES, st)) return rc;
     ncclResult_t r = ncclGroupStart();
     if (r == ncclSuccess) {
+        // (a non-blocking communicator may answer ncclInProgress: queued, not failed)
         if (root) {
-            for (uint32_t k = 1; k < q.nranks && r == ncclSuccess; k++)
+            for (uint32_t k = 1; k < q.nranks && (r == ncclSuccess || r == ncclInProgress); k++)
                 r = ncclRecv(c->d_gathered + k * slot, slot, ncclFloat32, (int)k, c->comm, st);
         } else {
             r = ncclSend(mine, slot, ncclFloat32, 0, c->comm, st);
         }
-        const ncclResult_t e = ncclGroupEnd();
+        if (r == ncclInProgress) r = ncclSuccess;
+        ncclResult_t e = ncclGroupEnd();
+        if (e == ncclInProgress) e = nccl_settle(c->comm); // non-blocking: enqueued before the blend
         if (r == ncclSuccess) r = e;
     }
     if (r != ncclSuccess) return nccl_fail(c, r, "tile gather");
@@ -378,6 +412,24 @@ int cr_group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p
         g->rank_ms[k] = g->ctx[k]->last_ms;
     }
     g->last = sum;
+    return CR_OK;
+}
+
+int cr_group_set_accumulator(cr_group *g, uint32_t xres, uint32_t yres, const float *rgb) {
+    if (!g) return CR_E_INVALID;
+    if (!group_ok(g)) return gfail(g, CR_E_HIP, g->err.empty() ? "group not initialised" : g->err);
+    if (!rgb || !xres || !yres) return gfail(g, CR_E_INVALID, "null / empty accumulator");
+    const size_t elems = (size_t)xres * yres * 3;
+    if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
+    if (elems != g->frame_elems) {
+        if (g->frame) hipFree(g->frame);
+        g->frame = nullptr;
+        g->frame_elems = 0;
+        if (hipMalloc(&g->frame, elems * sizeof(float)) != hipSuccess) return gfail(g, CR_E_OOM, "frame");
+        g->frame_elems = elems;
+    }
+    if (hipMemcpy(g->frame, rgb, elems * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+        return gfail(g, CR_E_HIP, "frame copy");
     return CR_OK;
 }
 

@@ -70,6 +70,8 @@ struct DevScene {
     // LC_REC (leafcull.hpp) per kd node: a leaf's references in two normal groups, each with
     // its box and normal cone -- the exact skip of the tests a unit-direction ray cannot pass
     const float4 *lcull;
+    const float4 *lcullf; // the same records in the fixed-pad form (leaf_cull_fixed, trace builds with LC 3)
+    const float4 *lcullp; // ... packed (LC_RECP float4 per node, leaf_cull_pack, LC 4)
     float db;             // bound on |coordinate| of any origin or vertex (padded box + 1)
     const float4 *tri;    // 3 per triangle: A, B, C
     const float4 *mat_n;  // normal, w = emissive flag bits
@@ -126,6 +128,7 @@ struct RenderArgs {
     int eye_on_split;
     uint32_t diag_kinds;          // counting builds: trace kinds (1 << TK_*) the DIAG_* slots describe
     int lc_debug;                 // measurement only: leaf-cull masks 1 = every reference, 2 = none (wrong images)
+    uint32_t lc_min;              // leaf-cull builds: leaves with fewer references are tested without the check
 };
 int num_persistent_variants();
 
@@ -211,6 +214,7 @@ struct WfStreams {
 int num_wf_variants();
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
+bool wf_variant_available(int variant); // compiled in (the default compile holds builds 0, 15, 18, 26)
 // cull boxes of this render's camera for the nrefs leaf references (+ 4 padding boxes)
 // and their unions per subtree (node_boxes[n_nodes]): leaves first, then the inner
 // nodes level by level from the deepest (levels: inner node ids grouped by depth,

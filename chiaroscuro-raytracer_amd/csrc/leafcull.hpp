@@ -99,6 +99,68 @@ CR_LC_HD inline bool lc_group_skip(const float o[3], const float d[3], const flo
     return (tn > tf) | (tn > t_hi) | (tf < t_lo);
 }
 
+// The same skip with the per-ray terms bounded once per scene (records of
+// leaf_cull_record_fixed): every ray whose |d.a| - 16u >= kappa has cb >= C0 on the group,
+// and with S <= the scene's extent the pad, dt and the tmax factor are constants of the
+// group -- the box comes pre-padded, so a ray does one dot product and a slab test.
+//   {lo - pad, kappa} {hi + pad, dt} {axis, tk}:  skip iff |d.a| >= kappa and
+//   o + t d misses the box for t in [-dt, tmax tk + dt]
+enum { LC_C0_INV = 16 }; // C0 = 1/16: rays within ~86 degrees of every normal of the group
+CR_LC_HD inline bool lc_group_skip_fixed(const float o[3], const float d[3], const float inv[3], float tmax, LcFloat4 lo,
+                                         LcFloat4 hi, LcFloat4 ax) {
+    const float u = 0x1p-24f;
+    const float dn = fabsf((d[0] * ax.x + d[1] * ax.y) + d[2] * ax.z);
+    if (!(dn >= lo.w)) return false; // possibly grazing (or NaN): never skipped
+    const float dt = hi.w, t_hi = (tmax * ax.w) * (1.f + 2.f * u) + dt, t_lo = -dt;
+    float tn = -INFINITY, tf = INFINITY;
+    for (int i = 0; i < 3; i++) {
+        const float t0 = ((&lo.x)[i] - o[i]) * inv[i], t1 = ((&hi.x)[i] - o[i]) * inv[i];
+        const bool nan = !(t0 == t0) || !(t1 == t1);
+        const float a = nan ? -INFINITY : (t0 < t1 ? t0 : t1), b = nan ? INFINITY : (t0 < t1 ? t1 : t0);
+        tn = a > tn ? a : tn;
+        tf = b < tf ? b : tf;
+    }
+    tn -= 4.f * u * fabsf(tn);
+    tf += 4.f * u * fabsf(tf);
+    return (tn > tf) | (tn > t_hi) | (tf < t_lo);
+}
+CR_LC_HD inline uint32_t leaf_cull_mask_fixed(const float o[3], const float d[3], const float inv[3], bool unit,
+                                              float tmax, const LcFloat4 *rec, uint32_t count) {
+    const uint32_t all = count >= 32 ? 0xffffffffu : ((1u << count) - 1u);
+    if (!unit || count > (uint32_t)LC_MAXREFS) return all;
+    const LcFloat4 m = rec[6];
+    uint32_t keep, m0, m1;
+    __builtin_memcpy(&keep, &m.z, 4);
+    __builtin_memcpy(&m0, &m.x, 4);
+    __builtin_memcpy(&m1, &m.y, 4);
+    if (m0 && !lc_group_skip_fixed(o, d, inv, tmax, rec[0], rec[1], rec[2])) keep |= m0;
+    if (m1 && !lc_group_skip_fixed(o, d, inv, tmax, rec[3], rec[4], rec[5])) keep |= m1;
+    return keep & all;
+}
+
+// Packed fixed-pad records (LC_RECP float4, leaves of up to 16 references): the three masks
+// ride in the low 8 mantissa bits of the six per-group constants kappa, dt, tk -- each
+// rounded UP to a multiple of 256 ulps first, so the bits only enlarge a bound that is
+// already an upper one.  {lo0, kappa0} {hi0, dt0} {axis0, tk0} {lo1, kappa1} {hi1, dt1} {axis1, tk1};
+// mask0 = kappa0 | dt0 << 8, mask1 = tk0 | kappa1 << 8, always = dt1 | tk1 << 8 (low bytes).
+enum { LC_RECP = 6, LC_MAXREFS_P = 16 };
+CR_LC_HD inline uint32_t lc_lowbyte(float f) {
+    uint32_t b;
+    __builtin_memcpy(&b, &f, 4);
+    return b & 0xffu;
+}
+CR_LC_HD inline uint32_t leaf_cull_mask_packed(const float o[3], const float d[3], const float inv[3], bool unit,
+                                               float tmax, const LcFloat4 *rec, uint32_t count) {
+    const uint32_t all = count >= 32 ? 0xffffffffu : ((1u << count) - 1u);
+    if (!unit || count > (uint32_t)LC_MAXREFS_P) return all;
+    const uint32_t m0 = lc_lowbyte(rec[0].w) | lc_lowbyte(rec[1].w) << 8;
+    const uint32_t m1 = lc_lowbyte(rec[2].w) | lc_lowbyte(rec[3].w) << 8;
+    uint32_t keep = lc_lowbyte(rec[4].w) | lc_lowbyte(rec[5].w) << 8;
+    if (m0 && !lc_group_skip_fixed(o, d, inv, tmax, rec[0], rec[1], rec[2])) keep |= m0;
+    if (m1 && !lc_group_skip_fixed(o, d, inv, tmax, rec[3], rec[4], rec[5])) keep |= m1;
+    return keep & all;
+}
+
 // The references of a leaf (count of them) its tests need for this ray: bit j for
 // reference first + j.  rec: the node's LC_REC float4.  Leaves beyond LC_MAXREFS and
 // non-unit rays: every reference (the caller tests count references then).
@@ -263,6 +325,66 @@ inline void leaf_cull_record(const float (*A)[3], const float (*e1)[3], const fl
     put_u(out[6].x, mask[0]);
     put_u(out[6].y, mask[1]);
     put_u(out[6].z, always);
+}
+
+// Host: leaf_cull_record turned into the fixed-pad form (lc_group_skip_fixed) for a scene
+// whose origins and vertices have |coordinate| <= db and differ by at most smax per axis.
+// The bound of lc_group_skip with cb >= C0 and S = smax, every factor rounded upward.
+inline void leaf_cull_fixed(const LcFloat4 in[LC_REC], double db, double smax, LcFloat4 out[LC_REC]) {
+    auto up = [](double x) {
+        float f = (float)x;
+        if ((double)f < x) f = nextafterf(f, INFINITY);
+        return f;
+    };
+    auto down = [](double x) {
+        float f = (float)x;
+        if ((double)f > x) f = nextafterf(f, -INFINITY);
+        return f;
+    };
+    const double u = 0x1p-24, c0 = 1.0 / LC_C0_INV, S = smax * (1 + 4 * u) + 1e-6;
+    for (int k = 0; k < 2; k++) {
+        const LcFloat4 lo = in[3 * k], hi = in[3 * k + 1], ax = in[3 * k + 2];
+        const double g = lo.w, E = hi.w, ct = ax.w;
+        // kappa: |d^.a^| >= kappa  =>  cos(psi + theta) >= c0 (the float dot's 16u margin added here)
+        const double th = acos(fmin(1.0, fmax(0.0, ct))), room = acos(c0) - th;
+        double kappa = room > 1e-6 ? cos(room) + 1e-12 : 2.0;
+        if (!(c0 > 20.2 * u * g) || !(g < 1e20)) kappa = 2.0; // no useful bound: never skip
+        kappa += 16 * u;
+        const double pad = (20.11 * u * (E + 2 * S) * g / c0 + 6.21 * u * E + u * S) * (1 + 1e-6) + 4 * u * db + 1e-20;
+        const double dt = 10.06 * u * S * g / c0 * (1 + 1e-6) + 1e-20;
+        const double tk = (1 + 10.06 * u * g / c0) * (1 + 3 * u) * (1 + 1e-6);
+        out[3 * k] = LcFloat4{down((double)lo.x - pad), down((double)lo.y - pad), down((double)lo.z - pad), up(kappa)};
+        out[3 * k + 1] = LcFloat4{up((double)hi.x + pad), up((double)hi.y + pad), up((double)hi.z + pad), up(dt)};
+        out[3 * k + 2] = LcFloat4{ax.x, ax.y, ax.z, up(tk)};
+    }
+    out[6] = in[6];
+}
+
+// Host: the fixed-pad record packed into LC_RECP float4 (leaf_cull_mask_packed); leaves of
+// more than 16 references keep every reference (the masks cannot hold them).
+inline void leaf_cull_pack(const LcFloat4 fx[LC_REC], uint32_t count, LcFloat4 out[LC_RECP]) {
+    uint32_t m[3];
+    __builtin_memcpy(&m[0], &fx[6].x, 4);
+    __builtin_memcpy(&m[1], &fx[6].y, 4);
+    __builtin_memcpy(&m[2], &fx[6].z, 4);
+    if (count > (uint32_t)LC_MAXREFS_P) {
+        m[0] = m[1] = 0u;
+        m[2] = 0xffffu;
+    }
+    for (int i = 0; i < LC_RECP; i++) out[i] = fx[i];
+    // the six constants (kappa, dt, tk per group), each carrying one byte of the masks
+    float *w[6] = {&out[0].w, &out[1].w, &out[2].w, &out[3].w, &out[4].w, &out[5].w};
+    const uint32_t bytes[6] = {m[0] & 0xffu, (m[0] >> 8) & 0xffu, m[1] & 0xffu, (m[1] >> 8) & 0xffu, m[2] & 0xffu,
+                               (m[2] >> 8) & 0xffu};
+    for (int i = 0; i < 6; i++) {
+        float f = *w[i];
+        uint32_t b;
+        __builtin_memcpy(&b, &f, 4);
+        // positive finite constants: round up to a multiple of 256 ulps, then the byte
+        if (!(f > 0.f) || !(f < 1e30f)) b = 0x7f000000u; // (2^127: a group that never passes)
+        b = ((b + 0xffu) & ~0xffu) | bytes[i];
+        __builtin_memcpy(w[i], &b, 4);
+    }
 }
 
 } // namespace cr

@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(256, MINW) render_dynamic(RenderArgs A) {
             continue;
         }
         if (go)
-            state = trav_round<R, FULL, PF, FD>(A.lc_debug, S, ring_lds, A.gstack, gstride, gid, o, d, state == ST_SHADOW,
+            state = trav_round<R, FULL, PF, FD>(A.lc_debug, A.lc_min, S, ring_lds, A.gstack, gstride, gid, o, d, state == ST_SHADOW,
                                                 exclude, T, c);
     }
     flush_counters(A.counters, c, 0u);

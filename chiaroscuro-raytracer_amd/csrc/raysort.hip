@@ -22,7 +22,9 @@
 // Traffic per pass: 4 B read (upsweep) + 8 B read + 8 B written (downsweep) per pair.
 // The hipcub DeviceRadixSort this replaced is kept as cr_set_option "wf_sort_lib" 1
 // for comparison.
+#ifdef CR_SORT_LIB // (make SORT_LIB=1: hipcub's sort as the comparison path, wf_sort_lib 1)
 #include <hipcub/hipcub.hpp>
+#endif
 
 #include "kernels.hpp"
 
@@ -223,10 +225,14 @@ static size_t rs_tmp_bytes(uint32_t n) {
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
                hipStream_t st, bool lib) {
     if (lib) {
+#ifdef CR_SORT_LIB
         hipcub::DoubleBuffer<uint32_t> k(keys[0], keys[1]), v(vals[0], vals[1]);
         if (hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, (int)n, 0, end_bit, st) != hipSuccess)
             return -1;
         return v.selector;
+#else
+        return -1; // not compiled in
+#endif
     }
     if (!tmp) {
         tmp_bytes = rs_tmp_bytes(n);

@@ -191,15 +191,30 @@ __device__ __forceinline__ void sload_lcull(const float4 *p, LcFloat4 (&r)[LC_RE
 }
 // The references of the leaf at `node` that the lane's ray (o, d: unit, segment [0, tmax])
 // must test (leafcull.hpp); bits < count.
-template <bool SC>
+// FORM 0: per-ray bound records (S.lcull), 1: fixed-pad (S.lcullf), 2: packed fixed-pad (S.lcullp)
+__device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_REC]) {
+    cr_v16f a;
+    cr_v8f b;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx8 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(a), "=s"(b)
+                 : "s"(p));
+#pragma unroll
+    for (int i = 0; i < 4; i++) r[i] = LcFloat4{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]};
+    r[4] = LcFloat4{b[0], b[1], b[2], b[3]};
+    r[5] = LcFloat4{b[4], b[5], b[6], b[7]};
+}
+template <bool SC, int FORM = 0>
 __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
     LcFloat4 rec[LC_REC];
+    constexpr int NR = FORM == 2 ? LC_RECP : LC_REC;
+    const float4 *recs = FORM == 2 ? S.lcullp : (FORM == 1 ? S.lcullf : S.lcull);
     if (SC && wave_uniform(node)) {
-        sload_lcull(S.lcull + (size_t)LC_REC * __builtin_amdgcn_readfirstlane(node), rec);
+        if (FORM == 2) sload_lcullp(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
+        else sload_lcull(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
     } else {
-        const float4 *p = (const float4 *)((const char *)S.lcull + node * (uint32_t)(16 * LC_REC));
+        const float4 *p = (const float4 *)((const char *)recs + node * (uint32_t)(16 * NR));
 #pragma unroll
-        for (int i = 0; i < LC_REC; i++) {
+        for (int i = 0; i < NR; i++) {
             const float4 v = p[i];
             rec[i] = LcFloat4{v.x, v.y, v.z, v.w};
         }
@@ -207,6 +222,8 @@ __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, 
     const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
     // v_rcp_f32: within 1 ulp of 1/d (the check allows 2, tests/native/leafcull_check.cpp)
     const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+    if (FORM == 2) return leaf_cull_mask_packed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
+    if (FORM == 1) return leaf_cull_mask_fixed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
     return leaf_cull_mask(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, S.db, rec, count);
 }
 
@@ -260,7 +277,7 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // for the references its cull record (leafcull.hpp) cannot exclude for this ray and segment.
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
           bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0>
-__device__ __forceinline__ uint32_t trav_round(int lc_debug, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
+__device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
@@ -413,10 +430,12 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, const DevScene &S, 
     // LC: the references to test (bit j: first + j); count > LC_MAXREFS: every one (lmask unused)
     lmask = 0u;
     if (LC && count && count <= (uint32_t)LC_MAXREFS) {
-        lmask = leaf_mask<SC>(S, T.node, count, o, d, T.tmax);
+        // LC 3: the fixed-pad records; leaves below lc_min: every reference, no check
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 4 ? 2 : (LC == 3 ? 1 : 0)>(S, T.node, count, o, d, T.tmax)
+                                : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }
-    if (LC == 2 && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp) {
+    if (LC == 2 && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp) { // (LC 2 only)
         pop_entry();
         continue;
     }

@@ -211,9 +211,11 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     uint32_t xs = blockIdx.x % WF_XCDS;
     Prof pf = {0, 0, 0, 0, 0};
     const uint64_t pstart = PROF ? prof_now() : 0;
+    uint64_t prefill = 0, nrefill = 0;
     for (;;) {
         const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
         if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= refill)) {
+            const uint64_t pr0 = PROF ? prof_now() : 0;
             const bool xp = (W.xcd >> (SHADOW ? 0 : (g == 1 ? 2 : 1))) & 1u;
             uint32_t *xwork = W.cnt + WF_XBASE + ((SHADOW ? WF_G : 0u) + g) * WF_XCDS * WF_XSTRIDE;
             for (;;) { // refill; a ray culled by the root box is answered at once and refetched
@@ -262,13 +264,17 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                     }
                 }
             }
+            if (PROF) {
+                prefill += prof_now() - pr0;
+                nrefill++;
+            }
         }
         if (!__any(state == busy_st)) {
             if (!__any(state != ST_DONE)) break;
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC>(A.lc_debug, 
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC>(A.lc_debug, A.lc_min, 
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
                 A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr);
             if (r != busy_st) {
@@ -283,8 +289,8 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     if (PROF && (threadIdx.x & 63u) == 0 && ((A.diag_kinds >> (SHADOW ? TK_SHADOW : TK_CLOSEST)) & 1u)) {
         // cycles per wave: trav_round phases, the loop's total (the kinds of "diag_kinds")
         const uint64_t tot = prof_now() - pstart;
-        const uint64_t v[6] = {pf.desc, pf.cull, pf.test, pf.pop, pf.calls, tot};
-        for (int i = 0; i < 6; i++) atomicAdd(&A.counters[CTR_DIAG + i], (unsigned long long)v[i]);
+        const uint64_t v[8] = {pf.desc, pf.cull, pf.test, pf.pop, pf.calls, tot, prefill, nrefill};
+        for (int i = 0; i < 8; i++) atomicAdd(&A.counters[CTR_DIAG + i], (unsigned long long)v[i]);
     }
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
     else c.closest = issued;
@@ -534,7 +540,7 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
 // and kind.  Lanes refill from the queue (one atomicAdd per wave) when `refill`
 // of them are idle or none is busy; a lane with a finished query advances its
 // path at once.
-template <bool FULL, int R, int MINW>
+template <bool FULL, int R, int MINW, int LC = 0>
 __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uint32_t g0) {
     extern __shared__ uint2 ring_lds[];
     __shared__ unsigned long long tl[T_N];
@@ -616,7 +622,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
         }
         if (busy) {
             const bool shadow = state == ST_SHADOW;
-            const uint32_t r = trav_round<R, FULL, 1, false, true, true>(A.lc_debug, S, ring_lds, W.gstack, W.gstride, gid, o, d,
+            const uint32_t r = trav_round<R, FULL, 1, false, true, true, LC != 0, 0, false, 0, 0, LC>(A.lc_debug, A.lc_min, S, ring_lds, W.gstack, W.gstride, gid, o, d,
                                                                         shadow, exclude, T, c);
             if (r != (shadow ? ST_SHADOW : ST_CLOSEST)) state = r;
         }
@@ -892,63 +898,84 @@ struct WfVariant {
     int ring, waves_per_simd, tile;
     int cull; // the camera trace reads the cull boxes (1: references and leaves, 2: also subtrees)
     int packet; // the camera trace is a packet trace (needs a near child common to all camera rays)
+    int lc;     // the tail kernel's leaf cull form (trav_round's LC; 0: none)
 };
 #define CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, PL)                                                     \
     {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
      wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>,                                  \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>, R, W, TL, CU, 0}
+     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>, R, W, TL, CU, 0, 0}
 #define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU) CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, 0)
 #define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, 0)
 #define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
 #define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
 #define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
 #define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
+// The trace builds, by index (cr_set_option "variant").  The default compile holds the
+// plain reference build 0, build 15 (the packet camera trace's fallback for an eye on a
+// split plane), build 18 (round 2's default) and build 26 (the default); every measured
+// and superseded build -- each is described below and in DESIGN.md §3 / §6 -- compiles
+// with `make ALL_VARIANTS=1` and is an empty entry (rejected at render) otherwise.
+#define CR_WF_NONE {nullptr, nullptr, nullptr, 8, 8, 0, 0, 0, 0}
+#ifdef CR_ALL_VARIANTS
+#define CR_WF_OPT(...) __VA_ARGS__
+#else
+#define CR_WF_OPT(...) CR_WF_NONE
+#endif
 static const WfVariant kWf[] = {
-    CR_WF(4, 8, false, false, false), CR_WF(8, 8, false, false, false), CR_WF(8, 8, true, false, false),
-    CR_WF(8, 6, false, false, false), CR_WF(8, 6, true, false, false),  CR_WF(8, 8, true, true, false),
-    CR_WF(8, 8, true, false, true),   CR_WF(8, 8, false, false, true),  CR_WF_PF(8, 8, true, false, false, 2),
-    CR_WF_BF(8, 8, true, false, true, 1, true),
+    CR_WF(4, 8, false, false, false), CR_WF_OPT(CR_WF(8, 8, false, false, false)),
+    CR_WF_OPT(CR_WF(8, 8, true, false, false)), CR_WF_OPT(CR_WF(8, 6, false, false, false)),
+    CR_WF_OPT(CR_WF(8, 6, true, false, false)), CR_WF_OPT(CR_WF(8, 8, true, true, false)),
+    CR_WF_OPT(CR_WF(8, 8, true, false, true)), CR_WF_OPT(CR_WF(8, 8, false, false, true)),
+    CR_WF_OPT(CR_WF_PF(8, 8, true, false, false, 2)),
+    CR_WF_OPT(CR_WF_BF(8, 8, true, false, true, 1, true)),
     // 10-12: build 9 with the top of the tree in LDS (TILE nodes, 32 B each, after the
     // stack ring: 8 blocks x (R x 2 KiB + TILE x 32 B) within the CU's 160 KiB)
-    CR_WF_T(8, 8, true, false, true, 1, true, 128), CR_WF_T(4, 8, true, false, true, 1, true, 384),
-    CR_WF_T(4, 8, true, false, true, 1, true, 0),
+    CR_WF_OPT(CR_WF_T(8, 8, true, false, true, 1, true, 128)), CR_WF_OPT(CR_WF_T(4, 8, true, false, true, 1, true, 384)),
+    CR_WF_OPT(CR_WF_T(4, 8, true, false, true, 1, true, 0)),
     // 13: build 9 with a uniform leaf's records two per scalar-load wait
-    CR_WF_U(8, 8, true, false, true, 1, true, 0, true),
+    CR_WF_OPT(CR_WF_U(8, 8, true, false, true, 1, true, 0, true)),
     // 14: build 9 whose camera trace skips triangle tests and leaves by the screen-space cull boxes
-    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 1),
+    CR_WF_OPT(CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 1)),
     // 15: 14 that also skips the subtrees whose box excludes the sample (checked at each fat-record fetch)
     CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 2),
     // 16: 15 whose secondary closest and shadow traces skip the tests their segment cannot
     // pass by the triangle's plane (planecull.hpp)
-    CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1),
+    CR_WF_OPT(CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1)),
     // 17: 15 whose camera rays traverse as one packet per wave (wf_trace_packet)
-    {wf_trace_packet<8, 1>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1},
+    CR_WF_OPT({wf_trace_packet<8, 1>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
+               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1, 0}),
     // 18: 17 with two camera rays per lane (packets of 128 rays: the scalar control per node
     // shared by twice the rays)
     {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1},
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1, 0},
     // 19: 18 whose secondary closest and shadow traces skip the references a leaf's cull record
     // (leafcull.hpp: two normal groups, each a box and a normal cone) excludes for the ray
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 8, 0, 2, 1},
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
+               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 8, 0, 2, 1, 0}),
     // 20: 19 whose lanes pass a leaf with every reference excluded and descend to the next one
     // in the same traversal round
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 8, 0, 2, 1},
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
+               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 8, 0, 2, 1, 0}),
     // 21 / 22: 19 / 20 at 6 waves per SIMD (80 VGPRs: no spills)
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
-     wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 6, 0, 2, 1},
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
-     wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 6, 0, 2, 1},
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
+               wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 6, 0, 2, 1, 0}),
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
+               wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 6, 0, 2, 1, 0}),
     // 23 / 24: 18 / 19 with the phase clock of the secondary and shadow traces (measurement only)
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>, 8, 8, 0, 2, 1},
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>, 8, 8, 0, 2, 1}};
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>,
+               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>, 8, 8, 0, 2, 1, 0}),
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>,
+               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>, 8, 8, 0, 2, 1, 0}),
+    // 25: 19 with the fixed-pad records (one dot product and a slab test per group)
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 3>,
+               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 3>, 8, 8, 0, 2, 1, 0}),
+    // 26 (default): 25 with the packed records (six float4 per leaf, leaves of up to 16 references);
+    // the tail kernel culls the same way
+    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
-                                   0, 0};
+                                   0, 0, 0};
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 int num_wf_variants() { return kNumWf; }
 // The camera-ray trace of a variant; the packet trace (build 17) needs a near child common
@@ -957,6 +984,7 @@ static void (*camera_kernel(const WfVariant &v, const RenderArgs &A))(RenderArgs
     return (v.packet && A.eye_on_split) ? kWf[15].camera : v.camera;
 }
 bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].cull; }
+bool wf_variant_available(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].closest; }
 
 // One thread per leaf reference: its cull box for this render's camera (camcull.hpp),
 // from the record's A, e1, e2 -- the floats the triangle test uses.  Boxes
@@ -1112,6 +1140,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+        else if (v.lc == 4)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
         else
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
         err = trace_event(te, st, TK_TAIL, false);
@@ -1189,6 +1219,8 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+        else if (v.lc == 4)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         err = trace_event(te, ln.st, TK_TAIL, false);

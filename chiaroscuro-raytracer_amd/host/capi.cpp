@@ -4,6 +4,7 @@
 #include "kdtree.hpp"
 #include "model.hpp"
 #include "preview.hpp"
+#include "checkpoint.hpp"
 #include "raytracer.hpp"
 #include "scene.hpp"
 
@@ -291,6 +292,48 @@ int chiaro_raytracer_export(chiaro_raytracer *r, const char *filename) {
         CR_E_INVALID);
 }
 cr_ctx *chiaro_raytracer_ctx(chiaro_raytracer *r) { return r ? r->r->context() : nullptr; }
+
+int chiaro_raytracer_checkpoint(chiaro_raytracer *r, const char *path) {
+    if (!r || !path) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            r->r->saveCheckpoint(path);
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+
+int chiaro_raytracer_resume(chiaro_raytracer *r, const char *path) {
+    if (!r || !path) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            r->r->resume(path);
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+
+uint64_t chiaro_kdtree_fingerprint(const chiaro_kdtree *k) { return k ? scene_fingerprint(*k->k) : 0; }
+
+int chiaro_checkpoint_write(const char *path, const chiaro_checkpoint *h, const float *pixels) {
+    if (!path || !h || !pixels) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            checkpoint_write(path, *h, pixels);
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+
+int chiaro_checkpoint_read(const char *path, chiaro_checkpoint *h, float *pixels) {
+    if (!path || !h) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            checkpoint_read(path, *h, pixels);
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
 void chiaro_raytracer_destroy(chiaro_raytracer *r) { delete r; }
 
 int chiaro_camera(const float eye[3], const float center[3], const float up[3], float yview, uint32_t xres,

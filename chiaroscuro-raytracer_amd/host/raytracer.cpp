@@ -1,6 +1,8 @@
 // raytracer.cpp -- host side of RayTracer (src/rayTracer.cpp), GPU render loop.
 #include "raytracer.hpp"
 
+#include "checkpoint.hpp"
+
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -148,6 +150,53 @@ void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) {
 }
 
 uint8_t *RayTracer::getData() { return data.data(); }
+
+void RayTracer::saveCheckpoint(const char *path) const {
+    if (!layers_) throw std::runtime_error("checkpoint: nothing rendered yet");
+    chiaro_checkpoint h{};
+    h.xres = scene.xres;
+    h.yres = scene.yres;
+    h.samples = scene.samples;
+    h.k = (uint32_t)scene.k;
+    h.seed = scene.seed;
+    h.layers = layers_;
+    const vec3 *v[3] = {&lastEye, &lastCenter, &lastUp};
+    float *dst[3] = {h.eye, h.center, h.up};
+    for (int i = 0; i < 3; i++) {
+        dst[i][0] = v[i]->x;
+        dst[i][1] = v[i]->y;
+        dst[i][2] = v[i]->z;
+    }
+    h.yview = lastYview;
+    h.background[0] = scene.background.x;
+    h.background[1] = scene.background.y;
+    h.background[2] = scene.background.z;
+    h.scene = scene_fingerprint(kdtree);
+    checkpoint_write(path, h, pixels.data());
+}
+
+void RayTracer::resume(const char *path) {
+    chiaro_checkpoint h{};
+    checkpoint_read(path, h, nullptr);
+    if (h.xres != scene.xres || h.yres != scene.yres || h.samples != scene.samples || h.k != (uint32_t)scene.k ||
+        h.seed != scene.seed || h.background[0] != scene.background.x || h.background[1] != scene.background.y ||
+        h.background[2] != scene.background.z)
+        throw std::runtime_error("resume: the checkpoint is of another frame size / spp / depth / seed / background");
+    if (h.scene != scene_fingerprint(kdtree)) throw std::runtime_error("resume: the checkpoint is of another scene");
+    if (!h.layers) throw std::runtime_error("resume: empty checkpoint");
+    checkpoint_read(path, h, pixels.data());
+    const int rc = group_ ? cr_group_set_accumulator(group_, scene.xres, scene.yres, pixels.data())
+                          : cr_set_accumulator(ctx_, scene.xres, scene.yres, pixels.data());
+    if (rc != CR_OK)
+        throw std::runtime_error(std::string("resume: ") + (group_ ? cr_group_last_error(group_) : cr_last_error(ctx_)));
+    layers_ = h.layers;
+    lastEye = vec3(h.eye[0], h.eye[1], h.eye[2]);
+    lastCenter = vec3(h.center[0], h.center[1], h.center[2]);
+    lastUp = vec3(h.up[0], h.up[1], h.up[2]);
+    lastYview = h.yview;
+    maxVal = 0.f;
+    for (float x : pixels) maxVal = maxVal > x ? maxVal : x;
+}
 
 // rayTracer.cpp:196-222 (exrdisplay-style): the scalar setup on the host, the
 // per-pixel transform on the GPU over the device accumulator of the last layer

@@ -49,6 +49,10 @@ class RayTracer {
     cr_group *group() { return group_; }        // gpus > 1, else null
     KDTree &tree() { return kdtree; }
     const cr_counters &lastCounters() const { return counters_; }
+    // checkpoint / resume of the progressive state (host/checkpoint.hpp); resume throws
+    // std::runtime_error for a checkpoint of another frame, sampling or scene
+    void saveCheckpoint(const char *path) const;
+    void resume(const char *path);
     double lastSeconds() const { return lastSeconds_; }
 
   private:

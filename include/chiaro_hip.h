@@ -172,6 +172,11 @@ int cr_upload_scene(cr_ctx *ctx, const cr_scene_desc *desc);
  * accum_rgb_out (host).  Layer 1 ignores the previous accumulator. */
 int cr_render(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out);
 
+/* Resume a progressive render (checkpoint / resume of the accumulator, the persisted
+ * counterpart of src/rayTracer.cpp:18-33,64): the ctx's accumulator becomes the host
+ * frame rgb [yres][xres][3]; the next cr_render of layer L > 1 blends into it. */
+int cr_set_accumulator(cr_ctx *ctx, uint32_t xres, uint32_t yres, const float *rgb);
+
 /* Same, blending into the caller-owned device buffer d_frame [yres][xres][3]
  * (only this rank's tiles are touched) on `stream` (hipStream_t, NULL = null stream). */
 int cr_render_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *d_frame, void *stream);
@@ -246,6 +251,10 @@ int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
  * shapes (what staging a wave's leaves in LDS would load) and a per-lane census of
  * repeated any-segment triangle misses.  Up to n of the DIAG_* values (csrc/kernels.hpp). */
 int cr_get_diag(cr_ctx *ctx, uint64_t *out, int n);
+/* 1 when wavefront trace build `build` (option "variant" with "kernel" 2) is compiled in:
+ * the default compile holds 0, 15, 18 and 26 (the default); `make ALL_VARIANTS=1` every
+ * measured build.  A render with a missing build returns CR_E_INVALID. */
+int cr_trace_build_available(int build);
 int cr_synchronize(cr_ctx *ctx);
 
 /* ---------------------------------------------------------- multi-GPU --
@@ -294,6 +303,8 @@ int cr_group_get_counters(cr_group *g, cr_counters *out); /* summed over the ran
 int cr_group_rank_ms(cr_group *g, float *ms_out);          /* [ngpus] each rank's last pass (HIP events) */
 /* rank's ctx (rank 0: the root, which also answers cr_intersect*), NULL if out of range */
 cr_ctx *cr_group_ctx(cr_group *g, int rank);
+/* cr_set_accumulator for the group's root accumulator */
+int cr_group_set_accumulator(cr_group *g, uint32_t xres, uint32_t yres, const float *rgb);
 /* cr_tonemap on the root's accumulator (the frame of the last cr_group_render) */
 int cr_group_tonemap(cr_group *g, const cr_tonemap_params *t, uint32_t xres, uint32_t yres, uint8_t *bytes_out);
 

@@ -86,6 +86,26 @@ int chiaro_raytracer_normalize(chiaro_raytracer *r, float exposure, float defog,
                                float gamma);
 int chiaro_raytracer_export(chiaro_raytracer *r, const char *filename);
 cr_ctx *chiaro_raytracer_ctx(chiaro_raytracer *r);
+
+/* Checkpoint / resume of a progressive render (the persisted counterpart of
+ * src/rayTracer.cpp:18-33,64 -- layer count, last camera, running average).
+ * A resumed RayTracer continues the layers where the checkpoint left them: the next
+ * rayTrace at the same camera renders layer `layers + 1` and blends it into the saved
+ * average, bit for bit as if the process had never stopped.  A checkpoint of another
+ * frame size / spp / depth / seed / background / scene is refused (CR_E_INVALID). */
+typedef struct {
+    uint32_t xres, yres, samples, k, seed, layers;
+    float eye[3], center[3], up[3], yview;
+    float background[3];
+    uint64_t scene; /* chiaro_kdtree_fingerprint of the scene the average belongs to */
+} chiaro_checkpoint;
+int chiaro_raytracer_checkpoint(chiaro_raytracer *r, const char *path);
+int chiaro_raytracer_resume(chiaro_raytracer *r, const char *path);
+uint64_t chiaro_kdtree_fingerprint(const chiaro_kdtree *k);
+/* the file format itself (for a caller keeping its own frame, e.g. the multi-GPU
+ * DistributedFrame): pixels [yres][xres][3]; read with pixels NULL = header only */
+int chiaro_checkpoint_write(const char *path, const chiaro_checkpoint *h, const float *pixels);
+int chiaro_checkpoint_read(const char *path, chiaro_checkpoint *h, float *pixels);
 void chiaro_raytracer_destroy(chiaro_raytracer *r);
 
 int chiaro_camera(const float eye[3], const float center[3], const float up[3], float yview, uint32_t xres,

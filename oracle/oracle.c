@@ -750,7 +750,7 @@ void or_render(or_scene *s, const float cam[12], uint32_t xres, uint32_t yres, u
 #pragma omp parallel num_threads(nth)
     {
         ctr_t ct; memset(&ct, 0, sizeof ct);
-#pragma omp for schedule(dynamic, 1)
+#pragma omp for schedule(static) /* src/rayTracer.cpp:55: the default (static) schedule over rows */
         for (int64_t ri = 0; ri < nrows; ri++) {
             const uint32_t y = y0 + (uint32_t)ri * ystep;
             for (uint32_t x = 0; x < xres; x++) {
@@ -767,6 +767,45 @@ void or_render(or_scene *s, const float cam[12], uint32_t xres, uint32_t yres, u
                 v3 nw = divs(add(muls(old, (float)(layer - 1)), muls(temp, inv)), (float)layer);
                 P[0] = nw.x; P[1] = nw.y; P[2] = nw.z;
             }
+        }
+#pragma omp critical
+        for (int i = 0; i < OR_C_COUNT; i++) tot[i] += ct.c[i];
+    }
+    if (counters)
+        for (int i = 0; i < OR_C_COUNT; i++) counters[i] = tot[i];
+}
+
+/* Batch means of a list of pixels (the tile split's per-rank work):
+ * mean[i] = (sum over samples in order of sendRay) * (1/spp), counters summed. */
+void or_render_pixels(or_scene *s, const float cam[12], uint32_t xres, uint32_t yres, uint32_t spp, int k,
+                      const float bg[3], uint32_t seed, uint32_t layer, uint32_t n, const uint32_t *px,
+                      const uint32_t *py, int threads, float *mean, uint64_t *counters) {
+    itg_t it = {s, k, V3(bg[0], bg[1], bg[2])};
+    const float inv = 1.f / (float)spp;
+    (void)yres;
+    uint64_t tot[OR_C_COUNT];
+    memset(tot, 0, sizeof tot);
+#ifdef _OPENMP
+    int nth = threads > 0 ? threads : omp_get_max_threads();
+#else
+    int nth = 1;
+    (void)threads;
+#endif
+#pragma omp parallel num_threads(nth)
+    {
+        ctr_t ct; memset(&ct, 0, sizeof ct);
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < (int64_t)n; i++) {
+            v3 temp = V3(0.f, 0.f, 0.f);
+            for (uint32_t smp = 0; smp < spp; smp++) {
+                rng_t rng = rng_make(seed, layer, py[i] * xres + px[i], smp);
+                v3 eye;
+                v3 dir = camera_sample(cam, px[i], py[i], &rng, &eye);
+                ct.c[OR_C_PATHS]++;
+                temp = add(temp, send_ray(&it, eye, dir, 1, &rng, &ct));
+            }
+            const v3 m = muls(temp, inv);
+            mean[3 * i] = m.x; mean[3 * i + 1] = m.y; mean[3 * i + 2] = m.z;
         }
 #pragma omp critical
         for (int i = 0; i < OR_C_COUNT; i++) tot[i] += ct.c[i];

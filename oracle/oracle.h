@@ -93,6 +93,12 @@ void or_render(or_scene *s, const float cam[12], uint32_t xres, uint32_t yres, u
                const float bg[3], uint32_t seed, uint32_t layer, uint32_t y0, uint32_t y1, uint32_t ystep,
                int threads, float *pix, uint64_t *counters);
 
+/* Batch means (no blend) of n listed pixels (px[i], py[i]) of layer `layer`:
+ * mean[3i..] = (sum over samples of sendRay) * (1/spp); counters summed (may be NULL). */
+void or_render_pixels(or_scene *s, const float cam[12], uint32_t xres, uint32_t yres, uint32_t spp, int k,
+                      const float bg[3], uint32_t seed, uint32_t layer, uint32_t n, const uint32_t *px,
+                      const uint32_t *py, int threads, float *mean, uint64_t *counters);
+
 /* glm / kd-tree primitives (pinned by tests/golden/ref_glm.json) */
 void or_glm_normalize(const float a[3], float out[3]);
 void or_glm_cross(const float a[3], const float b[3], float out[3]);

@@ -58,6 +58,8 @@ def lib():
                                C.c_uint32, C.c_uint32, FP]),
             "or_render": (None, [P, FP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, FP, C.c_uint32, C.c_uint32,
                                  C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, FP, C.POINTER(C.c_uint64)]),
+            "or_render_pixels": (None, [P, FP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, FP, C.c_uint32,
+                                        C.c_uint32, C.c_uint32, UP, UP, C.c_int, FP, C.POINTER(C.c_uint64)]),
             "or_set_trig_mode": (None, [C.c_int]),
             "or_sincos_check": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int]),
             "or_glm_normalize": (None, [FP, FP]),
@@ -164,6 +166,17 @@ class OracleScene:
         lib().or_render(self.h, _p(_f(cam)), xres, yres, spp, k, _p(_f(bg)), seed & 0xFFFFFFFF, layer, y0,
                         yres if y1 is None else y1, ystep, threads, _p(pix), ctr.ctypes.data_as(C.POINTER(C.c_uint64)))
         return pix, dict(zip(COUNTER_NAMES, (int(x) for x in ctr)))
+
+
+    def render_pixels(self, cam, xres, yres, spp, k, seed, px, py, layer=1, bg=(0, 0, 0), threads=0):
+        """Batch means [n][3] of the listed pixels (no blend) and the summed counters."""
+        px, py = np.ascontiguousarray(px, np.uint32), np.ascontiguousarray(py, np.uint32)
+        mean = np.zeros((len(px), 3), np.float32)
+        ctr = np.zeros(N_COUNTERS, np.uint64)
+        lib().or_render_pixels(self.h, _p(_f(cam)), xres, yres, spp, k, _p(_f(bg)), seed & 0xFFFFFFFF, layer,
+                               len(px), _p(px, C.c_uint32), _p(py, C.c_uint32), threads, _p(mean),
+                               ctr.ctypes.data_as(C.POINTER(C.c_uint64)))
+        return mean, dict(zip(COUNTER_NAMES, (int(x) for x in ctr)))
 
 
 def camera(eye, center, up, yview, xres, yres) -> np.ndarray:

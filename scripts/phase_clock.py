@@ -44,12 +44,13 @@ def main():
             dev.render_device(cam, p, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
             g = dev.diag()
-            tot = max(g["rounds"] if False else list(g.values())[5], 1)
-            vals = list(g.values())[:6]
-            names = ("descent", "cull", "tests", "pop", "calls", "loop_total")
+            vals = list(g.values())[:8]
+            names = ("descent", "cull", "tests", "pop", "calls", "loop_total", "refill", "refills")
             r = dict(zip(names, vals))
-            frac = {k: round(r[k] / max(r["loop_total"], 1), 3) for k in ("descent", "cull", "tests", "pop")}
-            frac["outside_trav_round"] = round(1 - sum(frac.values()), 3)
+            frac = {k: round(r[k] / max(r["loop_total"], 1), 3) for k in ("descent", "cull", "tests", "pop", "refill")}
+            frac["rest"] = round(1 - sum(frac.values()), 3)
+            frac["calls_per_refill"] = round(r["calls"] / max(r["refills"], 1), 2)
+            frac["cycles_per_refill"] = round(r["refill"] / max(r["refills"], 1), 1)
             ts = dev.trace_stats()[kind]
             out["%s/%s" % (v, kind)] = {"frac": frac, "cycles_per_call": {k: round(r[k] / max(r["calls"], 1), 1)
                                                                           for k in ("descent", "cull", "tests", "pop")},

@@ -10,7 +10,7 @@
 // points on their edges and vertices (a few ulps off), along grazing directions (d in
 // the plane up to 1e-9 ... 1e-1), with tmax random or a few ulps around the hit distance.
 // The kernels compute inv = v_rcp_f32(d) (1 ulp); the check perturbs inv by up to 2 ulp.
-//   leafcull_check <seed> <leaves>   prints "violations N tested M accepted A skipped K"
+//   leafcull_check <seed> <leaves> [form: 0 per-ray, 1 fixed-pad, 2 packed]   prints "violations N tested M accepted A skipped K"
 #include "leafcull.hpp"
 
 #include <cmath>
@@ -158,6 +158,7 @@ int main(int argc, char **argv) {
     rs ^= seed * 0x9E3779B97F4A7C15ull;
     for (int i = 0; i < 10; i++) rnd();
     uint64_t viol = 0, tested = 0, accepted = 0, skipped = 0;
+    const int form = argc > 3 ? atoi(argv[3]) : 0; // 1: fixed-pad records (leaf_cull_fixed), 2: packed
     for (int L = 0; L < leaves; L++) {
         const double scale = pow(10.0, rr(-2, 3.5));
         const std::vector<Tri> t = make_leaf(scale);
@@ -235,7 +236,26 @@ int main(int argc, char **argv) {
             const float db = std::fmax(db_leaf, 1.01f * std::fmax(std::fabs(o.x), std::fmax(std::fabs(o.y), std::fabs(o.z))));
             float inv[3];
             for (int i = 0; i < 3; i++) inv[i] = ulps(1.f / dv[i], (int)(rnd() * 5) - 2); // v_rcp_f32: within 1 ulp
-            const uint32_t keep = cr::leaf_cull_mask(ov, dv, inv, true, tmax, db, rec, n);
+            uint32_t keep;
+            if (form) { // the scene constants this ray satisfies: |o|, |vertex| <= db, |o_i - v_i| <= smax
+                double smax = 0;
+                for (uint32_t j = 0; j < n; j++)
+                    for (int i = 0; i < 3; i++) {
+                        const double v[3] = {A[j][i], (double)A[j][i] + e1[j][i], (double)A[j][i] + e2[j][i]};
+                        for (double x : v) smax = std::fmax(smax, std::fabs((double)ov[i] - x));
+                    }
+                cr::LcFloat4 fr[cr::LC_REC];
+                cr::leaf_cull_fixed(rec, db, smax, fr);
+                if (form == 2) {
+                    cr::LcFloat4 pr[cr::LC_RECP];
+                    cr::leaf_cull_pack(fr, n, pr);
+                    keep = cr::leaf_cull_mask_packed(ov, dv, inv, true, tmax, pr, n);
+                } else {
+                    keep = cr::leaf_cull_mask_fixed(ov, dv, inv, true, tmax, fr, n);
+                }
+            } else {
+                keep = cr::leaf_cull_mask(ov, dv, inv, true, tmax, db, rec, n);
+            }
             for (uint32_t j = 0; j < n; j++) {
                 tested++;
                 const bool acc = mt(o, d, t[j].A, t[j].e1, t[j].e2, tmax);

@@ -1,0 +1,58 @@
+"""bench.py's own multi-rank path on the CPU (the driver runs it on an
+8-GPU node as `bench.py --gpus N`).
+
+bench.py --gpus 2 without a torch.distributed environment spawns its two rank
+processes (torch.distributed.run, 127.0.0.1), each checks WORLD_SIZE, renders its
+tiles, rank 0 gathers them (gloo here, RCCL on the GPUs) and blends, every rank's
+wall and render times are all-gathered and the step is timed by the slowest rank;
+rank 0 prints the JSON line.  The device is the oracle-backed stand-in of
+tests/bench_cpu_backend.py, named through CHIARO_BENCH_BACKEND (the product never
+imports it).  The line must say n_gpus 2 with two per-rank render times, count
+the oracle's rays, and the frame rank 0 accumulated over the layers must equal the
+oracle's single-process progressive render bit for bit.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+RES, SPP, WARMUP, STEPS = (40, 24), 2, 1, 2
+
+
+def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
+    frame = tmp_path / "frame.npy"
+    env = dict(os.environ, CHIARO_BENCH_BACKEND="%s:make" % (ROOT / "tests" / "bench_cpu_backend.py"),
+               MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2", CHIARO_QUIET="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", str(STEPS), "--warmup", str(WARMUP),
+           "--config", "cornell", "--res", "%dx%d" % RES, "--spp", str(SPP), "--no-cpu-baseline",
+           "--save-frame", str(frame)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["steps"] == STEPS and line["backend"] == "cpu-oracle"
+    assert len(line["config"]["rank_render_ms"]) == 2 and all(v > 0 for v in line["config"]["rank_render_ms"])
+    assert line["config"]["parallelism"] == "tile-split x2"
+    # the oracle's frame and rays over the same layers (warmup layers included in the frame)
+    sc = scenes.config_rtc("cornell")
+    s = ca.Scene(sc, "xres", str(RES[0]), "yres", str(RES[1]))
+    i = s.info
+    m = ca.Model(s)
+    osc = po.OracleScene(m.triangles(), leaf_size=i["leaf_size"], textures=m.textures())
+    cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], RES[0], RES[1]).as_array()
+    ref, rays = None, 0
+    for L in range(1, WARMUP + STEPS + 1):
+        ref, c = osc.render(cam, RES[0], RES[1], SPP, i["k"], i["seed"], layer=L, bg=i["background"], pixels=ref)
+        if L > WARMUP:
+            rays += c["closest"] + c["shadow"]
+    assert line["config"]["rays"] == rays
+    got = np.load(frame)
+    assert got.shape == ref.shape and (got.view(np.uint32) == ref.view(np.uint32)).all() and got.mean() > 0
+    # value: the rays of all ranks over the slowest rank's wall time (ms_per_step is that / steps)
+    want = rays / (line["ms_per_step"] * STEPS / 1e3) / 1e6
+    assert abs(line["value"] - want) <= 1e-3 * want + 2e-3

@@ -109,3 +109,25 @@ def test_raytracer_gpus_key(ca, scenes):
         data.append(rt.getData())
     assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32)) and out[0].any()
     assert np.array_equal(data[0], data[1])
+
+
+def test_missing_peers_fail_cleanly(ca):
+    """The driver's N-GPU paths must fail, not hang, when their peers are missing: on a
+    one-GPU box a communicator of two ranks never forms -- cr_comm_init returns
+    CR_E_COMM once its deadline ("comm_timeout_ms") passes -- and a group over two
+    distinct devices fails its create (the second device does not exist) with the
+    reason, and is destroyed cleanly (the rank buffers are sized before the contexts)."""
+    import time
+    if ca.Device.device_count() >= 2:
+        pytest.skip("needs a box with exactly one GPU")
+    dev = ca.Device(0)
+    dev.set_option("comm_timeout_ms", 3000)
+    uid = ca.Device.comm_unique_id()
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="CR_E_COMM"):
+        dev.comm_init(2, 0, uid)
+    assert time.time() - t0 < 60
+    with pytest.raises(RuntimeError, match="device 1"):
+        ca.Group([0, 1])
+    with pytest.raises(RuntimeError, match="device 99"):
+        ca.Group([0, 99])
