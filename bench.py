@@ -75,8 +75,10 @@ def cpu_threads():
 
 
 def cpu_baseline(pair_tris, textures, info, leaf, cam, xres, yres, spp, k, seed, budget_s):
-    """Oracle restatement (OpenMP over rows, dynamic schedule) on a row sample of
-    the same frame, with all threads of the CPU share and with 1 thread."""
+    """Oracle restatement on a row sample of the same frame: OpenMP over the sampled
+    rows with the reference's static schedule (src/rayTracer.cpp:55), with all
+    threads of this process's CPU share and with 1 thread, on the SAME sample (every
+    ystep-th row x sample_spp), so the two legs and their ratio are comparable."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle as po
 
@@ -84,37 +86,38 @@ def cpu_baseline(pair_tris, textures, info, leaf, cam, xres, yres, spp, k, seed,
     t0 = time.time()
     osc = po.OracleScene(pair_tris, leaf_size=leaf, textures=textures, build_threads=threads)
     log("cpu_baseline: oracle kd build %.1fs" % (time.time() - t0))
+    # calibrate with 1 thread on every 16th row at 1 spp, then size the sample so the
+    # 1-thread leg takes ~0.7 of the budget (the all-thread leg then takes ~1/threads of it)
+    step = min(16, yres)
+    t0 = time.time()
+    osc.render(cam, xres, yres, 1, k, seed, y0=0, y1=yres, ystep=step, threads=1)
+    per_row_spp = max(time.time() - t0, 1e-3) / ((yres + step - 1) // step)
+    work = budget_s * 0.7 / per_row_spp                 # affordable (row x spp) units at 1 thread
+    s_spp = int(max(1, min(spp, work // yres)))         # the whole frame if it fits, more spp if time allows
+    nrows = int(max(threads, min(yres, work // s_spp)))
+    ystep = max(1, yres // nrows)
+    nr = (yres + ystep - 1) // ystep
 
-    def timed(nthreads, budget):
-        # calibrate on every 8th row at 1 spp, then size (rows, spp) to ~budget
-        step = 8
-        t0 = time.time()
-        osc.render(cam, xres, yres, 1, k, seed, y0=0, y1=yres, ystep=step, threads=nthreads)
-        dt = max(time.time() - t0, 1e-3)
-        rows = (yres + step - 1) // step
-        work = budget / (dt / rows)                   # affordable row-samples
-        s_spp = int(max(1, min(spp, work // yres)))   # whole frame if it fits, more spp if time allows
-        nrows = int(max(1, min(yres, work // s_spp)))
-        ystep = max(1, yres // nrows)
+    def leg(nthreads):
         t0 = time.time()
         _, c = osc.render(cam, xres, yres, s_spp, k, seed, y0=0, y1=yres, ystep=ystep, threads=nthreads)
-        dt = time.time() - t0
-        rays = c["closest"] + c["shadow"]
-        nr = (yres + ystep - 1) // ystep
-        return rays / dt / 1e6, "%d of %d rows (every %d-th) x %d px x %d spp, %d rays in %.1f s" % (
-            nr, yres, ystep, xres, s_spp, rays, dt)
+        return c["closest"] + c["shadow"], time.time() - t0
 
-    v_all, s_all = timed(threads, budget_s * 0.6)
-    v_1t, s_1t = timed(1, budget_s * 0.4)
+    rays, dt1 = leg(1)
+    runs = sorted(leg(threads)[1] for _ in range(3))
+    dtn = runs[1]  # the median of three
+    v_all, v_1t = rays / dtn / 1e6, rays / dt1 / 1e6
     phys = physical_cores()
+    sample = "%d of %d rows (every %d-th) x %d px x %d spp, %d rays" % (nr, yres, ystep, xres, s_spp, rays)
     return {"value": round(v_all, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
             "value_1t": round(v_1t, 4), "threads_all": threads, "physical_cores": phys,
             "parallel_efficiency": round(v_all / (v_1t * threads), 3) if v_1t > 0 else None,
             # linear in cores from the 1-thread rate: an upper bound for the whole host (the pool
             # gives one GPU's job a 16-thread CPU share, so the other cores are not timed)
             "projected_all_physical": round(v_1t * phys, 2) if phys else None,
-            "sample": "oracle/liboracle.so (OpenMP rows, dynamic) on the same frame/seed; %d threads: %s; "
-                      "1 thread: %s" % (threads, s_all, s_1t)}
+            "sample": "oracle/liboracle.so (OpenMP over rows, static schedule as src/rayTracer.cpp:55) on the "
+                      "same frame / seed, the same sample for both legs: %s; %d threads %.2f s (median of 3), "
+                      "1 thread %.1f s" % (sample, threads, dtn, dt1)}
 
 
 def issue_roofline(dom, iss, views, issue, pass_view, kind):
