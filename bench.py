@@ -134,12 +134,19 @@ def issue_roofline(dom, iss, views, issue, pass_view, kind):
     the one with the highest fraction; TA (vector address path) busy comes from
     the profile only (no live counterpart)."""
     t = dom["avg_launch_ms"] / 1e3
-    bytes_view = {"algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"], "achieved_gbs": dom["achieved"],
-                  "frac_of_hbm": round(dom["achieved"] / HBM_PEAK_GBS, 4),
-                  "frac_of_l2_aggregate": round(dom["achieved"] / L2_PEAK_GBS, 4),
-                  "fabric_bytes_per_launch": dom["traffic"], "work_per_launch": dom.get("work_per_launch"),
-                  "note": "SURVEY 8d bytes of the reference algorithm's work (counting build); the cull boxes of the "
-                          "camera trace skip most of that work exactly, so its rate is an effective one"}
+    perf_gbs = dom.get("achieved")
+    bytes_view = {"per_launch": dom.get("bytes_per_launch"),
+                  "performed_gbs": perf_gbs,
+                  "performed_frac_of_l2_aggregate": round(perf_gbs / L2_PEAK_GBS, 4) if perf_gbs else None,
+                  "reference_equivalent_gbs": dom["reference_equivalent_gbs"],
+                  "fabric_gbs": dom.get("fabric_gbs"),
+                  "fabric_frac_of_hbm": round(dom["fabric_gbs"] / HBM_PEAK_GBS, 4) if dom.get("fabric_gbs") else None,
+                  "work_per_launch": dom.get("work_per_launch"),
+                  "performed_work_per_launch": dom.get("performed_work_per_launch"),
+                  "note": "performed = the bytes the kernel's loads and stores move (cr_get_perf, vector per lane + "
+                          "scalar per wave), served mostly from L2 / Infinity Cache; fabric = measured HBM-side bytes "
+                          "(rocprofv3 PMC); reference_equivalent = SURVEY 8d bytes of the reference algorithm's "
+                          "work (counting build), which the culls skip in part"}
     what = {"camera": "camera-ray", "closest": "secondary closest-hit", "shadow": "shadow-ray"}[kind]
     base = {"kernel": dom["kernel"] + " (%s kd traversal, wavefront.hip)" % what,
             "avg_launch_ms": dom["avg_launch_ms"], "launches": dom["launches"],
@@ -147,9 +154,10 @@ def issue_roofline(dom, iss, views, issue, pass_view, kind):
             "other_traces": {k: v for k, v in views.items() if v is not None and v is not dom},
             "issue": issue, "pass": pass_view}
     if not iss or t <= 0 or "valu_insts_per_launch" not in iss:
-        return {"bound": "hbm", "achieved": dom["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(dom["achieved"] / HBM_PEAK_GBS, 5), "traffic": dom["traffic"],
-                "note": "no instruction-issue profile of this configuration: algorithmic bytes vs HBM", **base}
+        ach = dom["achieved"] if dom.get("achieved") is not None else dom["reference_equivalent_gbs"]
+        return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": dom["traffic"],
+                "note": "no instruction-issue profile of this configuration: performed bytes vs HBM", **base}
     valu = iss["valu_insts_per_launch"] / t / 1e9
     salu = iss["salu_insts_per_launch"] / t / 1e9
     ceil = {"valu": {"achieved": round(valu, 2), "peak": VALU_PEAK_GIPS, "frac": round(valu / VALU_PEAK_GIPS, 4),
@@ -159,7 +167,7 @@ def issue_roofline(dom, iss, views, issue, pass_view, kind):
             "ta_busy_profiled": iss.get("ta_busy"),
             "ta_note": "vector-memory address path busy fraction from the rocprofv3 PMC pass (no live "
                        "counterpart): the trace kernels are co-limited by issue and the address path",
-            "hbm_bytes": {"frac": bytes_view["frac_of_hbm"], "note": "algorithmic bytes, cache resident"}}
+            "hbm_bytes": {"frac": bytes_view["fabric_frac_of_hbm"], "note": "measured fabric bytes over the launch time"}}
     bound = max(("valu", "salu"), key=lambda k: ceil[k]["frac"])
     b = ceil[bound]
     return {"bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": "Gwave-inst/s", "frac": b["frac"],
@@ -251,6 +259,8 @@ def main():
                     help="cr_set_option before the scene upload (experiments; the default build is timed without)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-perf-pass", action="store_true",
+                    help="skip the untimed performed-work pass (profiling runs: its kernels are not the timed ones)")
     ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")
     args = ap.parse_args()
@@ -375,6 +385,18 @@ def run_rank(args, world, backend):
     totals["bytes"] = ca.algorithmic_bytes(cc, cc["pixels"])
     totals["tritest"] = cc["tritest"]
     totals["count_rays"] = cc["closest"] + cc["shadow"]
+    dev.set_option("counters", 0)
+    # performed-work pass (untimed): the default trace build's kernels with counters of what they
+    # actually execute and load (cr_get_perf), the same layer
+    perf = None
+    if wavefront and args.variant in (-1, 26) and hasattr(dev, "perf") and not args.no_perf_pass:
+        dev.set_option("perf_counters", 1)
+        if world == 1:
+            dev.render_device(cam, pc, scratch.data_ptr(), stream)
+        else:
+            dev.render_tiles_device(cam, pc, scratch_tiles.data_ptr(), stream)
+        perf = dev.perf()
+        dev.set_option("perf_counters", 0)
 
     out = None
     if rank == 0:
@@ -400,9 +422,23 @@ def run_rank(args, world, backend):
             cpu = cpu_baseline(model.triangles(), model.textures(), info, info["leaf_size"], cam.as_array(), xres,
                                yres, spp, k, seed,
                                args.cpu_budget)
+        # the pass: its measured fabric (HBM) bytes over its time is north_star's "rocprof HBM GB/s";
+        # the SURVEY §8d bytes of the reference algorithm's work over the same time are a
+        # reference-equivalent rate (the culls skip most of that work), not a performed one
+        fabric = pj.get("hbm_bytes_per_launch") if pj else None
+        perf_bytes = sum(v["vbytes"] + v["sbytes"] for v in perf.values()) if perf else None
         pass_view = {"kernels": "render pass (%s): all kernels of one layer" % kernel_name, "ms": round(kms, 3),
-                     "algorithmic_bytes": int(pass_bytes), "achieved": round(pass_gbs, 2),
-                     "traffic": pj.get("hbm_bytes_per_launch") if pj else None}
+                     "achieved": round(fabric / (kms / 1e3) / 1e9, 2) if fabric and kms > 0 else None,
+                     "achieved_is": "measured fabric (HBM) GB/s: rocprofv3 PMC bytes of one pass (profiles/pmc_%s.json) "
+                                    "over this run's pass time" % args.config,
+                     "peak": HBM_PEAK_GBS, "frac_of_hbm": round(fabric / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                     if fabric and kms > 0 else None,
+                     "traffic": fabric,
+                     "bytes": {"reference_equivalent": int(pass_bytes),
+                               "trace_performed": int(perf_bytes) if perf_bytes is not None else None,
+                               "fabric": fabric},
+                     "reference_equivalent_gbs": round(pass_gbs, 2),
+                     "trace_performed_gbs": round(perf_bytes / (kms / 1e3) / 1e9, 2) if perf_bytes and kms > 0 else None}
         if wavefront:
             # Per trace kind (camera = generation-1 closest queries, closest = later generations,
             # shadow): algorithmic bytes (8 per inner node, 8 per leaf, 40 per triangle test)
@@ -418,11 +454,27 @@ def run_rank(args, world, backend):
                 t = cts[kind]
                 kb = (8 * t["inner"] + 8 * t["leaf"] + 40 * t["tritest"]) / max(per_pass, 1e-9)
                 tr = (pj or {}).get("trace", {}).get(kind)
+                pf = (perf or {}).get(kind)
+                pb = (pf["vbytes"] + pf["sbytes"]) / max(per_pass, 1e-9) if pf else None
+                sec = avg_ms / 1e3
+                fab = tr["fabric_bytes_per_launch"] if tr else None
                 return {"kernel": "wf_trace<%s>" % kind, "avg_launch_ms": round(avg_ms, 3), "launches": launches,
                         "algorithmic_bytes_per_launch": int(kb),
                         "work_per_launch": {w: int(t[w] / max(per_pass, 1e-9)) for w in ("inner", "leaf", "tritest")},
-                        "achieved": round(kb / (avg_ms / 1e3) / 1e9, 2) if avg_ms > 0 else 0.0,
-                        "traffic": tr["fabric_bytes_per_launch"] if tr else None,
+                        # performed: the bytes the default build's loads and stores move (cr_get_perf);
+                        # reference_equivalent: SURVEY §8d bytes of the reference algorithm's work
+                        "bytes_per_launch": {"performed": int(pb) if pb is not None else None,
+                                             "performed_vector": int(pf["vbytes"] / max(per_pass, 1e-9)) if pf else None,
+                                             "performed_scalar": int(pf["sbytes"] / max(per_pass, 1e-9)) if pf else None,
+                                             "reference_equivalent": int(kb), "fabric": fab},
+                        "performed_work_per_launch": {w: int(pf[w] / max(per_pass, 1e-9))
+                                                      for w in ("queries", "steps", "leaves", "masks", "tests")}
+                        if pf else None,
+                        "achieved": round(pb / sec / 1e9, 2) if pb is not None and sec > 0 else None,
+                        "achieved_is": "performed bytes per launch / live launch time",
+                        "reference_equivalent_gbs": round(kb / sec / 1e9, 2) if sec > 0 else 0.0,
+                        "fabric_gbs": round(fab / sec / 1e9, 2) if fab and sec > 0 else None,
+                        "traffic": fab,
                         "rocprof_avg_launch_ms": round(tr["avg_ns"] / 1e6, 3) if tr else None}
             views = {k: kind_view(k) for k in ("camera", "closest", "shadow")}
             # what bounds the trace kernels instead of HBM: instruction issue (committed
@@ -456,8 +508,9 @@ def run_rank(args, world, backend):
             roofline = issue_roofline(dom, (issue or {}).get(dom_kind), views, issue, pass_view, dom_kind)
             roofline["dominant_by"] = {k: {"ms_per_pass": round(v[0], 3), "from": v[1]} for k, v in ranked.items()}
         else:  # (no per-kind trace launches: the other kernels, or a backend without them)
-            roofline = {"bound": "hbm", "achieved": round(pass_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(pass_gbs / HBM_PEAK_GBS, 5), "traffic": pass_view["traffic"],
+            ach = pass_view["achieved"] if pass_view["achieved"] is not None else round(pass_gbs, 2)
+            roofline = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": pass_view["traffic"],
                         "kernel": pass_view["kernels"], "kernel_ms": round(kms, 3),
                         "algorithmic_bytes_per_launch": int(pass_bytes)}
         label = {"sponza": "sponza_standin (Sponza-Crytek stand-in, ~261k tris) 1920x1080",

@@ -113,6 +113,7 @@ class ChiaroSceneInfo(C.Structure):
 TRACE_KINDS = ("camera", "closest", "shadow", "tail")  # cr_trace_stats order
 DIAG_NAMES = ("rounds", "lanes", "distinct", "records", "maxcount", "lanetests", "fit64", "fit128",
               "urounds", "tests", "geomiss", "rep1", "rep4", "rep8")  # cr_get_diag order (DIAG_* in kernels.hpp)
+PERF_NAMES = ("queries", "steps", "leaves", "masks", "tests", "vbytes", "sbytes", "waves")  # cr_get_perf (PERF_*)
 
 
 class CrTraceStats(C.Structure):
@@ -138,12 +139,13 @@ _host = None
 # Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
                "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_tile_origin", "cr_intersect",
-               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize", "cr_get_diag", "cr_trace_build_available",
+               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize", "cr_get_diag", "cr_get_perf", "cr_trace_build_available",
                "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap",
                "cr_comm_unique_id", "cr_comm_init", "cr_comm_destroy", "cr_render_dist_device",
                "cr_device_count", "cr_group_create", "cr_group_destroy", "cr_group_last_error", "cr_group_size", "cr_group_ok",
                "cr_group_upload_scene", "cr_group_set_option", "cr_group_render", "cr_group_get_counters",
-               "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap")
+               "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap", "cr_set_accumulator",
+               "cr_group_set_accumulator")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
                 "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
@@ -207,6 +209,7 @@ def libs():
     _sig(hip, "cr_get_trace_stats", C.c_int, [P, C.POINTER(CrTraceStats)])
     _sig(hip, "cr_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
     _sig(hip, "cr_get_diag", C.c_int, [P, C.POINTER(C.c_uint64), C.c_int])
+    _sig(hip, "cr_get_perf", C.c_int, [P, C.POINTER(C.c_uint64), C.c_int])
     _sig(hip, "cr_trace_build_available", C.c_int, [C.c_int])
     _sig(hip, "cr_synchronize", C.c_int, [P])
     _sig(hip, "cr_tonemap_setup", None, [C.c_float] * 5 + [C.POINTER(CrTonemapParams)])
@@ -230,6 +233,8 @@ def libs():
     _sig(hip, "cr_group_get_counters", C.c_int, [P, C.POINTER(CrCounters)])
     _sig(hip, "cr_group_rank_ms", C.c_int, [P, FP])
     _sig(hip, "cr_group_ctx", P, [P, C.c_int])
+    _sig(hip, "cr_set_accumulator", C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)])
+    _sig(hip, "cr_group_set_accumulator", C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)])
     _sig(hip, "cr_group_tonemap", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32,
                                             C.POINTER(C.c_uint8)])
 
@@ -526,6 +531,14 @@ class Device:
         v = (C.c_uint64 * len(DIAG_NAMES))()
         self._chk(libs()[0].cr_get_diag(self._c, v, len(DIAG_NAMES)), "cr_get_diag")
         return {n: int(v[i]) for i, n in enumerate(DIAG_NAMES)}
+
+    def perf(self) -> dict:
+        """cr_get_perf: performed work of the last render with option "perf_counters" 1, per
+        trace kind (TRACE_KINDS): queries, steps, leaves, masks, tests, vbytes, sbytes, waves."""
+        n = len(PERF_NAMES)
+        v = (C.c_uint64 * (n * len(TRACE_KINDS)))()
+        self._chk(libs()[0].cr_get_perf(self._c, v, len(v)), "cr_get_perf")
+        return {k: {nm: int(v[n * i + j]) for j, nm in enumerate(PERF_NAMES)} for i, k in enumerate(TRACE_KINDS)}
 
     def set_option(self, key: str, value: int):
         self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")

@@ -101,6 +101,7 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.counters = c->d_counters;
     A.work = c->d_work;
     A.full_counters = c->full_counters;
+    A.perf_counters = c->perf_counters;
     A.diag_kinds = c->diag_kinds;
     A.lc_debug = c->lc_debug;
     A.lc_min = c->lc_min;
@@ -145,6 +146,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     if (c->kernel == 2 && !c->full_counters && !cr::wf_variant_available(A.variant))
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
                                          " is not compiled in (make ALL_VARIANTS=1)");
+    if (c->perf_counters && (c->kernel != 2 || c->full_counters || A.variant != 26))
+        return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's default trace build 26 only, "
+                                     "without the counting build");
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     if (c->kernel == 0 || c->kernel == 2) {
         const bool wf = c->kernel == 2;
@@ -322,6 +326,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                           h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16],
                           h[17], h[18], h[19], h[20], h[21]};
     for (int i = 0; i < cr::DIAG_N; i++) c->last_diag[i] = h[cr::CTR_DIAG + i];
+    for (int i = 0; i < cr::TK_N * cr::PERF_N; i++) c->last_perf[i] = h[cr::CTR_PERF + i];
     c->last_trace = cr_trace_stats{};
     if (c->kernel == 2) {
         for (int i = 0; i < c->tev.n; i++) {
@@ -911,11 +916,18 @@ int cr_get_diag(cr_ctx *c, uint64_t *out, int n) {
     return CR_OK;
 }
 
+int cr_get_perf(cr_ctx *c, uint64_t *out, int n) {
+    if (!c || !out || n < 0) return CR_E_INVALID;
+    for (int i = 0; i < n && i < cr::TK_N * cr::PERF_N; i++) out[i] = c->last_perf[i];
+    return CR_OK;
+}
+
 int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!c || !key) return CR_E_INVALID;
     const int64_t nvar = std::max(cr::num_persistent_variants(), cr::num_wf_variants());
     if (!std::strcmp(key, "kernel") && (v == 0 || v == 1 || v == 2)) c->kernel = (int)v;
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
+    else if (!std::strcmp(key, "perf_counters") && (v == 0 || v == 1)) c->perf_counters = (int)v;
     else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
     else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
     else if (!std::strcmp(key, "lc_min") && v >= 0 && v <= 33) c->lc_min = (uint32_t)v;

@@ -60,6 +60,8 @@ struct cr_ctx {
     uint32_t lc_min = 0;                   // RenderArgs::lc_min
     uint32_t diag_kinds = 0;               // counting renders: trace kinds of the DIAG_* census (1 << TK_*)
     unsigned long long last_diag[cr::DIAG_N] = {};
+    int perf_counters = 0;                 // RenderArgs::perf_counters (option "perf_counters")
+    unsigned long long last_perf[cr::TK_N * cr::PERF_N] = {};
     int variant = -1;       // -1: the kernel's default build
     uint32_t block = 0;
     uint32_t waves_per_cu = 0;

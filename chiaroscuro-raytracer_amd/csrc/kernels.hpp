@@ -9,7 +9,7 @@ enum { MODE_BLEND = 0, MODE_TILES = 1 };
 // float4 per triangle record.  3 (48 B, 1.5 lines per test on average) beat 4
 // (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
 enum { REC_STRIDE = 3 };
-enum { CTR_N = 22, CTR_SLOTS = 64 }; // Ctr fields (cr_counters order); device counter buffer entries
+enum { CTR_N = 22, CTR_SLOTS = 96 }; // Ctr fields (cr_counters order); device counter buffer entries
 // Wavefront trace launches by kind (cr_trace_stats order): camera rays (generation-1
 // closest trace), closest traces of later generations, shadow traces, the tail kernel.
 enum { TK_CAMERA = 0, TK_CLOSEST = 1, TK_SHADOW = 2, TK_TAIL = 3, TK_N = 4 };
@@ -34,6 +34,21 @@ enum {
     DIAG_REP1 = 11,     //   of those: the triangle was such a miss in the lane's last 1 / 4 / 8 such misses
     DIAG_REP4 = 12,
     DIAG_REP8 = 13,
+};
+// Performed work of the default trace build's kernels (RenderArgs::perf_counters, cr_get_perf):
+// per trace kind, slots CTR_PERF + PERF_N * kind + PERF_*.  What the kernels actually execute
+// and load -- after the cull boxes, leaf cull records and packet traversal skipped work --
+// where the counting build (full_counters) counts the reference algorithm's work.
+enum { CTR_PERF = 64, PERF_N = 8 };
+enum {
+    PERF_QUERIES = 0, // queries started (ray fetched from the queue)
+    PERF_STEPS = 1,   // inner-node decisions, per ray
+    PERF_LEAVES = 2,  // leaves reached, per ray
+    PERF_MASKS = 3,   // leaf cull records evaluated, per ray
+    PERF_TESTS = 4,   // triangle tests executed, per ray
+    PERF_VBYTES = 5,  // bytes of vector-memory loads and stores (per lane) of the trace
+    PERF_SBYTES = 6,  // bytes of scalar-memory loads (per wave)
+    PERF_WAVES = 7,   // wave iterations: traversal rounds (wf_trace, tail) / node fetches (packet)
 };
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one
@@ -109,6 +124,7 @@ struct RenderArgs {
     float4 *pathbuf;              // per-bounce (direct, w) [2*K][gstride]
     uint32_t gstride;             // threads in the persistent grid
     int full_counters;            // 1: also count inner/leaf/tritest (SURVEY §8d bytes)
+    int perf_counters;            // 1: the default build's kernels with performed-work counts (CTR_PERF)
     int variant;                  // persistent-kernel variant index (kernels.hip kVariants)
     uint32_t refill;              // idle lanes of a wave that trigger a path-state step / ray fetch
     uint32_t refill_shadow;       // wavefront shadow-trace kernel's threshold

@@ -71,6 +71,30 @@ struct Prof {
 };
 __device__ __forceinline__ uint64_t prof_now() { return __builtin_amdgcn_s_memtime(); }
 
+// Performed work of one lane (perf builds, PERF_* in kernels.hpp): what the kernel executes and
+// the bytes its loads and stores move -- vector accesses per lane, scalar loads once per wave
+// (counted by the wave's leader).
+struct Pc {
+    uint32_t q, steps, leaves, masks, tests, waves;
+    uint64_t vb, sb;
+};
+__device__ __forceinline__ void pc_load(Pc *pc, bool scalar, uint32_t bytes) {
+    if (!pc) return;
+    if (!scalar) pc->vb += bytes;
+    else if (wave_leader()) pc->sb += bytes;
+}
+// Call with the whole wave converged: the lane sums go to ctrs[0 .. PERF_N).
+__device__ __forceinline__ void pc_flush(unsigned long long *ctrs, const Pc &pc) {
+    const unsigned long long v[PERF_N] = {pc.q, pc.steps, pc.leaves, pc.masks, pc.tests, pc.vb, pc.sb, pc.waves};
+#pragma unroll
+    for (int i = 0; i < PERF_N; i++) {
+        unsigned long long x = v[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&ctrs[i], x);
+    }
+}
+
 // Root-box clip (kdtree.cpp:196-208, 276-283); false: the query ends without a hit.
 __device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool shadow, float limit, Trav &T) {
     const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -282,9 +306,19 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
-                                               Prof *pf = nullptr) {
+                                               Prof *pf = nullptr, Pc *pc = nullptr) {
     uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
     if (pf) pt0 = prof_now();
+    if (pc && wave_leader()) pc->waves++;
+    // performed-work accounting of record loads (pc: perf builds)
+    auto lrec = [&](uint32_t i) -> TriRec {
+        if (pc) pc->vb += 16u * REC_STRIDE;
+        return load_rec(S, i);
+    };
+    auto srec = [&](const float4 *q) -> TriRec {
+        pc_load(pc, true, 16u * REC_STRIDE);
+        return sload_rec(q);
+    };
     static_assert(!CULL || (BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "cull: lean BF + SC builds");
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
@@ -293,6 +327,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
     auto step = [&](uint2 nd) -> uint32_t {
+        if (pc) pc->steps++;
         if (FULL) {
             c.inner++;
             const bool uni = wave_uniform(T.node);
@@ -317,6 +352,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             k = far_only ? below : 1u - below;
             if (push) {
                 const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
+                if (pc && T.nl == R) pc->vb += 8;
                 if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
                 ring[slot] = make_uint2(child + below, __float_as_uint(T.tmax));
             }
@@ -356,6 +392,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             T.nl--;
         } else {
             e = gstk[(size_t)T.sp * gstride + gid];
+            if (pc) pc->vb += 8;
         }
         T.node = e.x;
         T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
@@ -373,6 +410,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                 f1 = tile[2 * node + 1];
             } else if (CULL >= 2) { // the record and the subtree box, loads issued together
                 float4 b;
+                pc_load(pc, SC && wave_uniform(node), 48);
                 if (SC && wave_uniform(node)) {
                     const uint32_t un = __builtin_amdgcn_readfirstlane(node);
                     sload_fat_box(S.fat + 2u * un, cull_node + un, f0, f1, b);
@@ -389,6 +427,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                 }
                 return;
             } else {
+                pc_load(pc, SC && wave_uniform(node), 32);
                 load_fat<SC>(S, node, f0, f1);
             }
             nd = make_uint2(f0.x, f0.y);
@@ -409,9 +448,11 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             fetch(T.node);
         }
     } else {
+        pc_load(pc, SC && wave_uniform(T.node), 8);
         nd = load_node<SC>(S, T.node);
         while ((nd.y & 3u) != 3u) {
             step(nd);
+            pc_load(pc, SC && wave_uniform(T.node), 8);
             nd = load_node<SC>(S, T.node);
         }
     }
@@ -419,10 +460,12 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         c.leaf++;
         if (wave_leader()) c.wave_round++;
     }
+    if (pc) pc->leaves++;
     first = nd.x;
     count = nd.y >> 2;
     lin = !culled; // CULL: the sample lies in the leaf's box (the union of its references')
     if (CULL && !culled) {
+        pc_load(pc, SC && wave_uniform(T.node), 16);
         const float4 lb = load_box<SC>(cull_node, T.node);
         lin = csx >= lb.x && csx <= lb.y && csy >= lb.z && csy <= lb.w;
     }
@@ -431,6 +474,10 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     lmask = 0u;
     if (LC && count && count <= (uint32_t)LC_MAXREFS) {
         // LC 3: the fixed-pad records; leaves below lc_min: every reference, no check
+        if (pc && count >= lc_min) {
+            pc->masks++;
+            pc_load(pc, SC && wave_uniform(T.node), 16u * (LC == 4 ? LC_RECP : LC_REC));
+        }
         lmask = count >= lc_min ? leaf_mask<SC, LC == 4 ? 2 : (LC == 3 ? 1 : 0)>(S, T.node, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
@@ -461,6 +508,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         const uint32_t id = rec_id(r);
         if (shadow && id == exclude) return true;
         if (FULL) c.tritest++;
+        if (pc) pc->tests++;
         if (FULL && dg && dg->on) { // repeated-miss census: a miss for any segment is one for every later one
             dg->v[DIAG_TESTS]++;
             float gx, gy, gt;
@@ -552,6 +600,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             const uint32_t id = rec_id(r);
             const bool live = in & !(shadow & (occluded | (id == exclude)));
             if (FULL) c.tritest += live ? 1u : 0u;
+            if (pc) pc->tests += live ? 1u : 0u;
             float ux, uy, t;
             const bool acc = live & tri_test_wave(o, d, r, T.tmax, ux, uy, t);
             if (shadow) {
@@ -575,12 +624,13 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             const float4 *pb = S.planes + uf;
             bool go = true;
             for (uint32_t j = 0; j < uc && go; j += 4) {
+                pc_load(pc, true, 64);
                 const cr_v16f pl = sload_box4(pb + j);
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) {
                     if (j + k >= uc) break;
                     if (__ballot(needs(pl[4 * k], pl[4 * k + 1], pl[4 * k + 2], pl[4 * k + 3])) &&
-                        !utest(sload_rec(base + (size_t)REC_STRIDE * (j + k)), j + k)) {
+                        !utest(srec(base + (size_t)REC_STRIDE * (j + k)), j + k)) {
                         go = false;
                         break;
                     }
@@ -589,13 +639,14 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         } else if (CULL) {
             const float4 *cb = cull + uf;
             for (uint32_t j = 0; j < uc && __ballot(lin); j += 4) {
+                pc_load(pc, true, 64);
                 const cr_v16f bx = sload_box4(cb + j);
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) {
                     if (j + k >= uc) break;
                     const bool in = csx >= bx[4 * k] && csx <= bx[4 * k + 1] && csy >= bx[4 * k + 2] &&
                                     csy <= bx[4 * k + 3];
-                    if (__ballot(in)) utest(sload_rec(base + (size_t)REC_STRIDE * (j + k)), j + k);
+                    if (__ballot(in)) utest(srec(base + (size_t)REC_STRIDE * (j + k)), j + k);
                 }
             }
         } else if (LC && uc <= (uint32_t)LC_MAXREFS) {
@@ -605,78 +656,83 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             for (uint32_t j = 0; j < uc; j++) {
                 const bool in = (lmask >> j) & 1u;
                 if (!__ballot(in)) continue;
-                if (!utest(sload_rec(base + (size_t)REC_STRIDE * j), j, in)) break;
+                if (!utest(srec(base + (size_t)REC_STRIDE * j), j, in)) break;
             }
         } else if (UL2) {
             for (uint32_t j = 0; j < uc; j += 2) {
                 TriRec r0, r1;
+                pc_load(pc, true, 32u * REC_STRIDE);
                 sload_rec2(base + (size_t)REC_STRIDE * j, r0, r1);
                 if (!utest(r0, j) || j + 1 >= uc || !utest(r1, j + 1)) break;
             }
         } else {
             for (uint32_t j = 0; j < uc; j++)
-                if (!utest(sload_rec(base + (size_t)REC_STRIDE * j), j)) break;
+                if (!utest(srec(base + (size_t)REC_STRIDE * j), j)) break;
         }
     } else if (SC && wave_uniform(first)) { // every lane at the same leaf: scalar loads
         const float4 *base = S.recs + (size_t)REC_STRIDE * __builtin_amdgcn_readfirstlane(first);
         for (uint32_t j = 0; j < count; j++) {
             tally_tri(first + j);
-            if (!test(sload_rec(base + (size_t)REC_STRIDE * j))) break;
+            if (!test(srec(base + (size_t)REC_STRIDE * j))) break;
         }
     } else if (PF == 2) { // pipelined, unrolled by two: the record sets alternate roles, no copies
         TriRec ra, rb;
-        if (count) ra = load_rec(S, first);
+        if (count) ra = lrec(first);
         for (uint32_t j = 0; j < count; j += 2) {
-            if (j + 1 < count) rb = load_rec(S, first + j + 1);
+            if (j + 1 < count) rb = lrec(first + j + 1);
             tally_tri(first + j);
             if (!test(ra)) break;
             if (j + 1 >= count) break;
-            if (j + 2 < count) ra = load_rec(S, first + j + 2);
+            if (j + 2 < count) ra = lrec(first + j + 2);
             tally_tri(first + j + 1);
             if (!test(rb)) break;
         }
     } else if (PLANE) { // plane records pipelined one ahead; a record only when the plane is crossed
         float4 np = make_float4(0.f, 0.f, 0.f, 0.f);
         if (count) np = S.planes[first];
+        if (pc && count) pc->vb += 16;
         for (uint32_t j = 0; j < count; j++) {
             const float4 pl = np;
             if (j + 1 < count) np = S.planes[first + j + 1];
+            if (pc && j + 1 < count) pc->vb += 16;
             const float s0 = dot(mk(pl.x, pl.y, pl.z), o) - pl.w;
             const float s1 = s0 + T.tmax * dot(mk(pl.x, pl.y, pl.z), d);
             if (!((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f)))
-                if (!test(load_rec(S, first + j))) break;
+                if (!test(lrec(first + j))) break;
         }
     } else if (LC && count <= (uint32_t)LC_MAXREFS) { // the mask's references, pipelined one ahead
         uint32_t m = lmask;
         TriRec nx;
-        if (m) nx = load_rec(S, first + (uint32_t)__builtin_ctz(m));
+        if (m) nx = lrec(first + (uint32_t)__builtin_ctz(m));
         while (m) {
             m &= m - 1u;
             const TriRec r = nx;
-            if (m) nx = load_rec(S, first + (uint32_t)__builtin_ctz(m));
+            if (m) nx = lrec(first + (uint32_t)__builtin_ctz(m));
             if (!test(r)) break;
         }
     } else if (CULL) { // boxes pipelined one ahead; a record only for a sample inside its box
         if (!lin) count = 0;
         float4 nb = make_float4(0.f, 0.f, 0.f, 0.f);
         if (count) nb = cull[first];
+        if (pc && count) pc->vb += 16;
         for (uint32_t j = 0; j < count; j++) {
             const float4 b = nb;
             if (j + 1 < count) nb = cull[first + j + 1];
+            if (pc && j + 1 < count) pc->vb += 16;
             if (csx >= b.x && csx <= b.y && csy >= b.z && csy <= b.w)
-                if (!test(load_rec(S, first + j))) break;
+                if (!test(lrec(first + j))) break;
         }
     } else {
         TriRec nx;
-        if (PF && count) nx = load_rec(S, first);
+        if (PF && count) nx = lrec(first);
         for (uint32_t j = 0; j < count; j++) {
             tally_tri(first + j);
             TriRec r;
             if (PF) { // software pipeline: issue triangle j+1's loads before testing j
                 r = nx;
-                if (j + 1 < count) nx = load_rec(S, first + j + 1);
+                if (j + 1 < count) nx = lrec(first + j + 1);
             } else {
-                r = load_rec(S, first + j);
+                r = lrec(first + j);
             }
             if (!test(r)) break;
         }

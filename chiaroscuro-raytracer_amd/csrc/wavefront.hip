@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
           bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0,
-          bool PROF = false>
+          bool PROF = false, bool PC = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
@@ -210,6 +210,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     // in turn (xs / 256 of them drained); one register, the rest is derived at refill
     uint32_t xs = blockIdx.x % WF_XCDS;
     Prof pf = {0, 0, 0, 0, 0};
+    Pc pc = {};
     const uint64_t pstart = PROF ? prof_now() : 0;
     uint64_t prefill = 0, nrefill = 0;
     for (;;) {
@@ -242,6 +243,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         if (!xp) state = ST_DONE; // else: stays idle and takes a ray of the next range
                     } else {
                         if (W.order) idx = W.order[idx]; // sorted queue: results still go to slot idx
+                        if (PC) pc.vb += (W.order ? 4u : 0u) + 32u + (SHADOW ? 4u : 0u) + (CULL ? 8u : 0u);
                         const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
                         o = ld3(r0);
                         d = ld3(r1);
@@ -257,8 +259,10 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                             state = busy_st;
                             if (FULL) diag_begin(&dg);
                         } else if (SHADOW) {
+                            if (PC) pc.vb += 4;
                             W.occ[idx] = 0u; // culled: visible (kdtree.cpp:285-287)
                         } else {
+                            if (PC) pc.vb += 16;
                             W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u);
                         }
                     }
@@ -276,8 +280,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
         if (state == busy_st) {
             const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC>(A.lc_debug, A.lc_min, 
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
-                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr);
+                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr);
             if (r != busy_st) {
+                if (PC) pc.vb += SHADOW ? 4u : 16u;
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
                                                            __float_as_uint(d.y), T.node + 1u) // w: the hit's leaf + 1
@@ -295,6 +300,10 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
     else c.closest = issued;
     flush_counters(A.counters, c, 0u);
+    if (PC) {
+        pc.q = issued;
+        pc_flush(A.counters + CTR_PERF + PERF_N * (SHADOW ? TK_SHADOW : (CAM ? TK_CAMERA : TK_CLOSEST)), pc);
+    }
     if (FULL) { // per-instantiation split of the §8d work counters (bench roofline)
         unsigned long long *base = A.counters + CTR_TRACE + 3 * (SHADOW ? TK_SHADOW : (CAM ? TK_CAMERA : TK_CLOSEST));
         const uint32_t v[3] = {c.inner, c.leaf, c.tritest};
@@ -540,7 +549,7 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
 // and kind.  Lanes refill from the queue (one atomicAdd per wave) when `refill`
 // of them are idle or none is busy; a lane with a finished query advances its
 // path at once.
-template <bool FULL, int R, int MINW, int LC = 0>
+template <bool FULL, int R, int MINW, int LC = 0, bool PC = false>
 __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uint32_t g0) {
     extern __shared__ uint2 ring_lds[];
     __shared__ unsigned long long tl[T_N];
@@ -552,6 +561,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
     uint32_t *work = work_closest(W, g0);
     const float4 *rays = W.ray[g0 & 1];
     Ctr c = {};
+    Pc pc = {};
     uint32_t state = ST_NEED_WORK, p = 0, exclude = 0, nclosest = 0, nshadow = 0;
     f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
@@ -574,6 +584,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                 if (idx >= n) {
                     state = ST_DONE;
                 } else {
+                    if (PC) pc.vb += 32;
                     const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
                     o = ld3(r0);
                     d = ld3(r1);
@@ -623,13 +634,19 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
         if (busy) {
             const bool shadow = state == ST_SHADOW;
             const uint32_t r = trav_round<R, FULL, 1, false, true, true, LC != 0, 0, false, 0, 0, LC>(A.lc_debug, A.lc_min, S, ring_lds, W.gstack, W.gstride, gid, o, d,
-                                                                        shadow, exclude, T, c);
+                                                                        shadow, exclude, T, c, nullptr, 0.f, 0.f,
+                                                                        nullptr, nullptr, nullptr, nullptr,
+                                                                        PC ? &pc : nullptr);
             if (r != (shadow ? ST_SHADOW : ST_CLOSEST)) state = r;
         }
     }
     c.closest = nclosest;
     c.shadow = nshadow;
     flush_counters(A.counters, c, 0u);
+    if (PC) { // the tail's traversal work (its shading is not counted)
+        pc.q = nclosest + nshadow;
+        pc_flush(A.counters + CTR_PERF + PERF_N * TK_TAIL, pc);
+    }
     flush_tallies(A, tl);
 }
 
@@ -664,7 +681,7 @@ enum : uint32_t { PACKET_DEPTH = 256 }; // >= the deepest tree cr_upload_scene a
 // end; a ray going to the far child only is parked with tmax = its tmin.  Only active
 // rays' intervals change, so an inactive ray's tmax still holds its value for the next
 // entry it owns.
-template <int R, int S>
+template <int R, int S, bool PC = false>
 __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint32_t pring_lds[]; // [R][blockDim][S] per-ray tmax bits at push
     __shared__ uint32_t pnode[4][PACKET_DEPTH];
@@ -682,6 +699,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
     const float4 *cnode = A.cull_node, *cref = A.cull;
     const uint32_t INACTIVE = 0xffffffffu;
     Ctr c = {};
+    Pc pc = {};
     uint32_t issued = 0;
     // XCD partition (WfArgs::xcd bit 2), as in wf_trace: own range first, then the others
     const bool xp = (W.xcd >> 2) & 1u;
@@ -710,12 +728,14 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             tmin[s] = tmax[s] = csx[s] = csy[s] = 0.f;
             found[s] = false;
             if (live[s]) {
+                if (PC) pc.vb += 32;
                 const float4 r0 = rays[2 * (size_t)idx[s]], r1 = rays[2 * (size_t)idx[s] + 1];
                 d[s] = ld3(r1);
                 if (__float_as_uint(r0.w) == NO_PATH) { // partial-tile slot: no query
                     hits[idx[s]] = make_uint4(0u, 0u, 0u, 0u);
                     live[s] = false;
                 } else {
+                    if (PC) pc.vb += 8;
                     const float2 q = W.cxy[idx[s]];
                     csx[s] = q.x;
                     csy[s] = q.y;
@@ -747,6 +767,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
         auto push = [&](uint32_t node, const bool (&act)[S]) {
             const uint32_t slot = (sp & (R - 1)) * bdim + tid;
             if (nl == (uint32_t)R) { // spill the oldest
+                if (PC) pc.vb += 8;
                 uint2 e = make_uint2(ring[slot * S], S == 2 ? ring[slot * S + (S - 1)] : 0u);
                 gstk[(size_t)(sp - R) * gstride + gid] = e;
             } else {
@@ -768,6 +789,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                     for (int s = 0; s < S; s++) e[s] = ring[slot * S + s];
                     nl--;
                 } else {
+                    if (PC) pc.vb += 8;
                     const uint2 ge = gstk[(size_t)sp * gstride + gid];
                     e[0] = ge.x;
                     if (S == 2) e[S - 1] = ge.y;
@@ -789,7 +811,12 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
         // a leaf reached with record nd; boxed: its box was read with its fat record
         auto leaf = [&](uint2 nd, bool boxed) {
             const uint32_t first = nd.x, count = nd.y >> 2;
+            if (PC) {
+#pragma unroll
+                for (int s = 0; s < S; s++) pc.leaves += active[s] ? 1u : 0u;
+            }
             if (!boxed) {
+                if (PC && wave_leader()) pc.sb += 16;
                 const float4 lb = sload_box(cnode + __builtin_amdgcn_readfirstlane(cn));
 #pragma unroll
                 for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, lb);
@@ -798,6 +825,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             const float4 *rb = Sc.recs + (size_t)REC_STRIDE * first;
             const uint32_t leafw = __builtin_amdgcn_readfirstlane(cn) + 1u; // hit record w: the leaf + 1
             for (uint32_t j = 0; j < count; j += 4) {
+                if (PC && wave_leader()) pc.sb += 64;
                 const cr_v16f bb = sload_box4(cref + first + j);
 #pragma unroll
                 for (uint32_t k = 0; k < 4; k++) {
@@ -810,12 +838,15 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                         any = any | in[s];
                     }
                     if (!__ballot(any)) continue;
+                    if (PC && wave_leader()) pc.sb += 16u * REC_STRIDE;
                     const TriRec r = sload_rec(rb + (size_t)REC_STRIDE * (j + k));
 #pragma unroll
                     for (int s = 0; s < S; s++) {
                         if (!__ballot(in[s])) continue;
                         float ux, uy, t;
                         const bool acc = in[s] & tri_test_wave(eye, d[s], r, tmax[s], ux, uy, t);
+                        if (PC) pc.tests += in[s] ? 1u : 0u;
+                        if (PC && acc) pc.vb += 16;
                         // the hit record straight to the queue (a later, nearer one in this leaf overwrites it)
                         if (acc) hits[idx[s]] = make_uint4(rec_id(r), __float_as_uint(ux), __float_as_uint(uy), leafw);
                         tmax[s] = acc ? t : tmax[s];
@@ -830,6 +861,10 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             uint4 f0, f1;
             float4 b;
             cn = __builtin_amdgcn_readfirstlane(cn); // uniform by construction
+            if (PC && wave_leader()) {
+                pc.sb += 48;
+                pc.waves++;
+            }
             sload_fat_box_n(Sc.fat, cnode, cn, f0, f1, b);
 #pragma unroll
             for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, b);
@@ -853,6 +888,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                 bool crosses[S], after[S], to_near[S], to_far[S], anyn = false, anyf = false;
 #pragma unroll
                 for (int s = 0; s < S; s++) {
+                    if (PC) pc.steps += active[s] ? 1u : 0u;
                     tsp[s] = split_distance(split, oa, comp(d[s], a));
                     crosses[s] = !(tsp[s] >= tmax[s]) & !(tsp[s] < 0.f); // !near_only
                     after[s] = !(tsp[s] <= tmin[s]);                     // far_only = crosses & !after
@@ -883,11 +919,17 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             go = popit ? pop() : true;
         }
 #pragma unroll
-        for (int s = 0; s < S; s++)
+        for (int s = 0; s < S; s++) {
+            if (PC && (live[s] & !found[s])) pc.vb += 16;
             if (live[s] & !found[s]) hits[idx[s]] = make_uint4(0u, 0u, 0u, 0u);
+        }
     }
     c.closest = issued;
     flush_counters(A.counters, c, 0u);
+    if (PC) {
+        pc.q = issued;
+        pc_flush(A.counters + CTR_PERF + PERF_N * TK_CAMERA, pc);
+    }
 }
 
 // --------------------------------------------------------------- launch --
@@ -973,6 +1015,10 @@ static const WfVariant kWf[] = {
     // the tail kernel culls the same way
     {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}};
+// Build 26 with the performed-work counts (RenderArgs::perf_counters; measurement only)
+static const WfVariant kWfPerf = {
+    wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
+    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>, 8, 8, 0, 2, 1, 4};
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
                                    0, 0, 0};
@@ -1125,7 +1171,9 @@ static uint32_t shade_grid(int num_cus) {
 int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st, const WfStreams &ss,
                            TraceEvents *te) {
     WfArgs W = W0;
-    const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
+    const WfVariant &v = A.full_counters ? kWfCount
+                         : A.perf_counters ? kWfPerf
+                                           : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     wf_tail_geometry(num_cus, tblk, tblocks);
@@ -1140,6 +1188,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+        else if (A.perf_counters)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
         else if (v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
         else
@@ -1198,7 +1248,9 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
 }
 
 int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hipStream_t st, TraceEvents *te) {
-    const WfVariant &v = A.full_counters ? kWfCount : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
+    const WfVariant &v = A.full_counters ? kWfCount
+                         : A.perf_counters ? kWfPerf
+                                           : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     wf_tail_geometry(num_cus, tblk, tblocks);
@@ -1219,6 +1271,8 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+        else if (A.perf_counters)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else

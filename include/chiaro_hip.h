@@ -251,6 +251,14 @@ int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
  * shapes (what staging a wave's leaves in LDS would load) and a per-lane census of
  * repeated any-segment triangle misses.  Up to n of the DIAG_* values (csrc/kernels.hpp). */
 int cr_get_diag(cr_ctx *ctx, uint64_t *out, int n);
+/* Performed work of the last render with option "perf_counters" 1 (the default trace build 26
+ * instantiated with counters; measurement only): per trace kind k (0 camera, 1 closest, 2 shadow,
+ * 3 tail) the PERF_N = 8 values out[8k + i] -- queries, inner-node steps, leaves reached, leaf
+ * cull records evaluated, triangle tests executed (all per ray), bytes of vector-memory loads and
+ * stores (per lane), bytes of scalar-memory loads (per wave), wave iterations (PERF_* in
+ * csrc/kernels.hpp).  Where the counting build ("counters" 1) counts the reference algorithm's
+ * work, these count what the culling kernels actually do.  Up to n values. */
+int cr_get_perf(cr_ctx *ctx, uint64_t *out, int n);
 /* 1 when wavefront trace build `build` (option "variant" with "kernel" 2) is compiled in:
  * the default compile holds 0, 15, 18 and 26 (the default); `make ALL_VARIANTS=1` every
  * measured build.  A render with a missing build returns CR_E_INVALID. */

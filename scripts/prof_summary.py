@@ -29,7 +29,10 @@ ROOT = Path(__file__).resolve().parents[1]
 
 def is_counting(name: str) -> bool:
     # FULL is the second template argument of both trace kernels
-    return re.search(r"(wf_trace|render_dynamic)<\w+, true,", name) is not None
+    # (and the performed-work counting instances of bench.py's perf pass: last template argument
+    # PC; profile runs pass --no-perf-pass, so these are not expected)
+    return (re.search(r"(wf_trace|render_dynamic)<\w+, true,", name) is not None or "wf_tail<true" in name or
+            re.search(r"(wf_trace|wf_trace_packet|wf_tail)<[^()]*, true>\(", name) is not None)
 
 
 def main():

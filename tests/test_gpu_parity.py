@@ -612,3 +612,62 @@ def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
     o, oc = pair.oracle.render(cam.as_array(), 24, 16, 2, 3, 0xC41A05C0, bg=(0.25, 0.5, 0.75))
     assert_bitwise(g, o, "triangle-less scene, variant %d" % variant)
     assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2
+
+
+@pytest.mark.parametrize("tail_min", [0, 3000])
+def test_perf_counters_build(ca, sponza, nanobox, tail_min):
+    """The performed-work build (option perf_counters: build 26's kernels with counters,
+    cr_get_perf) renders the same bits, and its counts agree with the counting build's:
+    the secondary and shadow traces take the reference traversal (steps and leaves equal),
+    the leaf cull and the camera culls only remove triangle tests (and, for the packet
+    camera trace, steps of rays a subtree box excludes)."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_tail_min", tail_min)
+        cam = pair.camera(ca, x, y)
+        p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=1)
+        try:
+            pair.dev.render(cam, p, None)
+            gc, ts = pair.dev.counters(), pair.dev.trace_stats()
+            pair.dev.set_option("counters", 0)
+            pair.dev.set_option("perf_counters", 1)
+            g = pair.dev.render(cam, p, None)
+            lc, perf = pair.dev.counters(), pair.dev.perf()
+        finally:
+            pair.dev.set_option("perf_counters", 0)
+            pair.dev.set_option("counters", 1)
+            pair.dev.set_option("wf_tail_min", 0)
+        o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=1)
+        assert_bitwise(g, o, "perf-counting build %dx%dx%d" % (x, y, s))
+        assert {k: lc[k] for k in LEAN_KEYS} == {k: gc[k] for k in LEAN_KEYS}
+        assert sum(v["queries"] for v in perf.values()) == gc["closest"] + gc["shadow"]
+        for kind in ("camera", "closest", "shadow"):
+            pk, rk = perf[kind], ts[kind]
+            if tail_min == 0:
+                assert pk["queries"] > 0 and pk["vbytes"] + pk["sbytes"] > 0, (kind, pk)
+            assert pk["tests"] <= rk["tritest"], (kind, pk, rk)
+            assert pk["leaves"] <= rk["leaf"] and pk["steps"] <= rk["inner"], (kind, pk, rk)
+            if kind != "camera" and tail_min == 0:
+                assert (pk["steps"], pk["leaves"]) == (rk["inner"], rk["leaf"]), (kind, pk, rk)
+                assert pk["masks"] <= pk["leaves"]
+        if tail_min == 0:
+            assert perf["tail"]["queries"] == 0
+            assert perf["camera"]["tests"] < ts["camera"]["tritest"]
+        else:
+            assert perf["tail"]["queries"] > 0 and perf["tail"]["steps"] > 0
+
+
+def test_perf_counters_default_build_only(ca, cornell):
+    """perf_counters instruments build 26 only: another build is refused loudly."""
+    cornell.dev.set_option("kernel", 2)
+    cornell.dev.set_option("counters", 0)
+    cornell.dev.set_option("perf_counters", 1)
+    cornell.dev.set_option("variant", 18)
+    cam = cornell.camera(ca, 16, 16)
+    try:
+        with pytest.raises(RuntimeError):
+            cornell.dev.render(cam, ca.render_params(16, 16, 1, 6, 0xC41A05C0, layer=1), None)
+    finally:
+        cornell.dev.set_option("variant", -1)
+        cornell.dev.set_option("perf_counters", 0)
+        cornell.dev.set_option("counters", 1)
