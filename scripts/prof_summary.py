@@ -43,7 +43,13 @@ def main():
     stats = next(src.glob("trace/*kernel_stats.csv"))
     shutil.copy(stats, prof / ("%s_kernel_stats.csv" % tag))
     rows = {r["Name"]: r for r in csv.DictReader(open(stats))}
-    passes = int(rows[next(n for n in rows if "sum_samples" in n)]["Calls"])  # timed + counting passes
+    # passes: the timed (lean) renders and ONE counting render.  A render of a large frame runs in
+    # several sample chunks (one sum_samples each), so the lean renders are counted by the cull-box
+    # kernel, which runs once per lean render of a culling build
+    calls = {n: int(r["Calls"]) for n, r in rows.items()}
+    cull = [c for n, c in calls.items() if "cam_cull_kernel" in n]
+    lean = cull[0] if cull else calls[next(n for n in rows if "sum_samples" in n)] - 1
+    passes = lean + 1
     # PMC: sum per kernel over its dispatches (one pass per counter group)
     sums = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in src.glob("*/pmc_counter_collection.csv"):
@@ -51,10 +57,13 @@ def main():
             sums[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
     summary, per_pass = {}, collections.defaultdict(float)
     for name, r in rows.items():
-        if not any(k in name for k in ("render_", "wf_", "sum_samples", "rocprim")):  # rocprim: queue sorts
+        if not any(k in name for k in ("render_", "wf_", "sum_samples", "rocprim", "cam_cull")):  # rocprim: queue sorts
             continue
         counting = is_counting(name)
-        frames = 1 if counting else (passes - 1 if "wf_trace" in name or "render_dynamic" in name else passes)
+        # counting-build kernels run in the counting render only, the lean trace / tail / cull kernels in
+        # the timed renders only, the rest (camera, shade, resolve, sorts, sum_samples) in both
+        lean_only = any(k in name for k in ("wf_trace", "wf_tail", "render_dynamic", "cam_cull"))
+        frames = 1 if counting else (lean if lean_only else passes)
         e = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "total_ns": float(r["TotalDurationNs"]),
              "counting_build": counting, "passes": frames}
         c = sums.get(name, {})
@@ -76,7 +85,7 @@ def main():
                 if k in c:
                     per_pass[k] += c[k] / frames
     per_pass["fabric_GBps"] = per_pass["fabric_bytes"] / max(per_pass["duration_ns"], 1.0)
-    out = {"render_pass": dict(per_pass), "kernels": summary, "passes_profiled": passes}
+    out = {"render_pass": dict(per_pass), "kernels": summary, "passes_profiled": passes, "timed_passes": lean}
     (prof / ("%s_pmc.json" % tag)).write_text(json.dumps(out, indent=1, sort_keys=True))
     spp = int(sys.argv[sys.argv.index("--spp") + 1]) if "--spp" in sys.argv else 128
     # the trace kernel's lean instantiations (bench.py roofline): fabric bytes per launch
