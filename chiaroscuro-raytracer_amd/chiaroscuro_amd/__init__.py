@@ -82,6 +82,42 @@ def checkpoint_read(path):
     return h, px
 
 
+def exr_write(path, rgb: np.ndarray):
+    """chiaro_exr_write: [H][W][3] float (R, G, B, row 0 = top) as the reference's exportImage
+    writes EXR -- HALF B, G, R, PIZ (src/rayTracer.cpp:229-272)."""
+    px = np.ascontiguousarray(rgb, np.float32)
+    if libs()[1].chiaro_exr_write(str(path).encode(), _ptr(px), px.shape[1], px.shape[0]):
+        raise RuntimeError("exr_write: " + _host_err())
+
+
+def exr_write_half(path, rgb: np.ndarray):
+    """chiaro_exr_write_half: the same from half bits [H][W][3] uint16."""
+    px = np.ascontiguousarray(rgb, np.uint16)
+    if libs()[1].chiaro_exr_write_half(str(path).encode(), px.ctypes.data_as(C.POINTER(C.c_uint16)), px.shape[1],
+                                       px.shape[0]):
+        raise RuntimeError("exr_write_half: " + _host_err())
+
+
+def exr_read_half(path) -> np.ndarray:
+    """chiaro_exr_read_half: half bits [H][W][3] (R, G, B) of a scanline HALF EXR (NO / PIZ)."""
+    w, h = C.c_uint32(), C.c_uint32()
+    if libs()[1].chiaro_exr_read_half(str(path).encode(), C.byref(w), C.byref(h), None, 0):
+        raise RuntimeError("exr_read_half: " + _host_err())
+    px = np.zeros((h.value, w.value, 3), np.uint16)
+    if libs()[1].chiaro_exr_read_half(str(path).encode(), C.byref(w), C.byref(h),
+                                      px.ctypes.data_as(C.POINTER(C.c_uint16)), px.size):
+        raise RuntimeError("exr_read_half: " + _host_err())
+    return px
+
+
+def float_to_half(x: np.ndarray) -> np.ndarray:
+    """chiaro_float_to_half: OpenEXR's half(float) -- nearest even, overflow to infinity."""
+    a = np.ascontiguousarray(x, np.float32)
+    out = np.zeros(a.shape, np.uint16)
+    libs()[1].chiaro_float_to_half(_ptr(a), out.ctypes.data_as(C.POINTER(C.c_uint16)), a.size)
+    return out
+
+
 class CrKdNode(C.Structure):
     _fields_ = [("split", C.c_float), ("axis", C.c_uint32), ("child_or_first", C.c_uint32), ("count", C.c_uint32)]
 
@@ -157,6 +193,7 @@ HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_g
                 "chiaro_raytracer_ctx", "chiaro_raytracer_destroy", "chiaro_camera",
                 "chiaro_raytracer_checkpoint", "chiaro_raytracer_resume", "chiaro_kdtree_fingerprint",
                 "chiaro_checkpoint_write", "chiaro_checkpoint_read",
+                "chiaro_exr_write", "chiaro_exr_write_half", "chiaro_exr_read_half", "chiaro_float_to_half",
                 "chiaro_preview_create", "chiaro_preview_key", "chiaro_preview_mouse", "chiaro_preview_scroll",
                 "chiaro_preview_texture", "chiaro_preview_state", "chiaro_preview_destroy",
                 "chiaro_preview_camera_replay")
@@ -273,6 +310,12 @@ def libs():
     _sig(host, "chiaro_checkpoint_write", C.c_int, [C.c_char_p, C.POINTER(Checkpoint), FP])
     _sig(host, "chiaro_checkpoint_read", C.c_int, [C.c_char_p, C.POINTER(Checkpoint), FP])
     _sig(host, "chiaro_raytracer_destroy", None, [P])
+    U16P = C.POINTER(C.c_uint16)
+    _sig(host, "chiaro_exr_write", C.c_int, [C.c_char_p, FP, C.c_uint32, C.c_uint32])
+    _sig(host, "chiaro_exr_write_half", C.c_int, [C.c_char_p, U16P, C.c_uint32, C.c_uint32])
+    _sig(host, "chiaro_exr_read_half", C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), U16P,
+                                                 C.c_size_t])
+    _sig(host, "chiaro_float_to_half", C.c_int, [FP, U16P, C.c_size_t])
     _sig(host, "chiaro_camera", C.c_int, [FP, FP, FP, C.c_float, C.c_uint32, C.c_uint32, C.POINTER(CrCamera)])
     _sig(host, "chiaro_preview_create", P, [P, P])
     _sig(host, "chiaro_preview_key", C.c_int, [P, C.c_int, C.c_float, C.c_int])

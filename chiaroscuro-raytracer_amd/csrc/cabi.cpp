@@ -206,7 +206,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                    (1ull << leaf_bits) < (((uint64_t)A.S.n_nodes >> c->wf_leaf_shift) + 1) * c->wf_dir_res * c->wf_dir_res)
                 leaf_bits++;
             const bool leaf_keys = c->wf_leaf_keys && leaf_bits <= 32;
-            if (leaf_keys) key_bits = std::max(key_bits, leaf_bits);
+            // (leaf keys replace the pixel and world keys in every queue: their width alone sets the
+            // digit passes)
+            if (leaf_keys) key_bits = leaf_bits;
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
             const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 16 * (size_t)P +
                                 (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +

@@ -300,13 +300,13 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // LC (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a leaf's tests run only
 // for the references its cull record (leafcull.hpp) cannot exclude for this ray and segment.
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0>
+          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0, bool REV = false>
 __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
-                                               Prof *pf = nullptr, Pc *pc = nullptr) {
+                                               Prof *pf = nullptr, Pc *pc = nullptr, const float *rcp_lds = nullptr) {
     uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
     if (pf) pt0 = prof_now();
     if (pc && wave_leader()) pc->waves++;
@@ -323,6 +323,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
     static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
+    static_assert(!REV || (BF && !FULL), "far-first order: lean BF builds (shadow queries only)");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -341,7 +342,11 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         const uint32_t a = nd.y & 3u;
         const float split = __uint_as_float(nd.x);
         const float oa = comp(o, a), da = comp(d, a);
-        const float tsplit = FD ? div_by_rcp(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
+        // rcp_lds (RL builds): the ray's RN(1/d) per axis in LDS [axis][thread], set at query start --
+        // the exact short division without three more VGPRs
+        const float tsplit = rcp_lds ? div_by_rcp(split - oa, da, rcp_lds[a * bdim + tid])
+                             : FD    ? div_by_rcp(split - oa, da, comp(T.r, a))
+                                     : split_distance(split, oa, da);
         const uint32_t below = (oa < split) || (oa == split && da <= 0);
         const uint32_t child = nd.y >> 2;
         uint32_t k;
@@ -349,16 +354,21 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             const bool near_only = (tsplit >= T.tmax) | (tsplit < 0);
             const bool far_only = !near_only & (tsplit <= T.tmin);
             const bool push = !near_only & !far_only;
-            k = far_only ? below : 1u - below;
+            // REV (shadow queries): a node crossed in both children is entered far side first, the
+            // near child pushed with its interval start (the query's answer does not depend on
+            // the order of the leaves, each tested over its own interval)
+            k = (far_only | (REV & push)) ? below : 1u - below;
             if (push) {
                 const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
                 if (pc && T.nl == R) pc->vb += 8;
                 if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
-                ring[slot] = make_uint2(child + below, __float_as_uint(T.tmax));
+                ring[slot] = REV ? make_uint2(child + 1u - below, __float_as_uint(T.tmin))
+                                 : make_uint2(child + below, __float_as_uint(T.tmax));
             }
             T.nl = push && T.nl < R ? T.nl + 1 : T.nl;
             T.sp += push ? 1u : 0u;
-            T.tmax = push ? tsplit : T.tmax;
+            if (REV) T.tmin = push ? tsplit : T.tmin;
+            else T.tmax = push ? tsplit : T.tmax;
         } else if (tsplit >= T.tmax || tsplit < 0) {
             k = 1u - below;
         } else if (tsplit <= T.tmin) {
@@ -395,8 +405,13 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             if (pc) pc->vb += 8;
         }
         T.node = e.x;
-        T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
-        T.tmax = __uint_as_float(e.y);
+        if (REV) { // the far subtree ended with its nearest leaf, whose interval starts at the split
+            T.tmax = T.tmin;
+            T.tmin = __uint_as_float(e.y);
+        } else {
+            T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
+            T.tmax = __uint_as_float(e.y);
+        }
     };
     // LC 2: a leaf whose references are all excluded is passed like an empty leaf -- the lane
     // pops and descends to its next leaf in the same round, so the round's tests run on every lane

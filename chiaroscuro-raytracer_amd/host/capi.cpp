@@ -5,10 +5,13 @@
 #include "model.hpp"
 #include "preview.hpp"
 #include "checkpoint.hpp"
+#include "exr.hpp"
 #include "raytracer.hpp"
 #include "scene.hpp"
 
+#include <cstdio>
 #include <cstring>
+#include <stdexcept>
 #include <memory>
 #include <string>
 #include <vector>
@@ -314,6 +317,66 @@ int chiaro_raytracer_resume(chiaro_raytracer *r, const char *path) {
 }
 
 uint64_t chiaro_kdtree_fingerprint(const chiaro_kdtree *k) { return k ? scene_fingerprint(*k->k) : 0; }
+
+static void write_file(const char *path, const std::vector<unsigned char> &bytes) {
+    FILE *f = std::fopen(path, "wb");
+    if (!f) throw std::runtime_error("cannot open " + std::string(path));
+    const bool ok = std::fwrite(bytes.data(), 1, bytes.size(), f) == bytes.size();
+    if (std::fclose(f) != 0 || !ok) throw std::runtime_error("cannot write " + std::string(path));
+}
+
+int chiaro_exr_write(const char *path, const float *rgb, uint32_t w, uint32_t h) {
+    if (!path || !rgb || !w || !h) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            write_file(path, chiaro::exr_encode(rgb, (int)w, (int)h));
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+
+int chiaro_exr_write_half(const char *path, const uint16_t *rgb, uint32_t w, uint32_t h) {
+    if (!path || !rgb || !w || !h) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            write_file(path, chiaro::exr_encode_half(rgb, (int)w, (int)h));
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+
+int chiaro_exr_read_half(const char *path, uint32_t *w, uint32_t *h, uint16_t *rgb, size_t cap) {
+    if (!path || !w || !h) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            FILE *f = std::fopen(path, "rb");
+            if (!f) throw std::runtime_error("cannot open " + std::string(path));
+            std::vector<unsigned char> bytes;
+            unsigned char buf[1 << 16];
+            size_t n;
+            while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) bytes.insert(bytes.end(), buf, buf + n);
+            std::fclose(f);
+            int W = 0, H = 0;
+            std::vector<uint16_t> px;
+            std::string err;
+            if (!chiaro::exr_decode_half(bytes.data(), bytes.size(), W, H, px, err))
+                throw std::runtime_error(std::string(path) + ": " + err);
+            *w = (uint32_t)W;
+            *h = (uint32_t)H;
+            if (rgb) {
+                if (cap < px.size()) throw std::runtime_error("rgb buffer too small");
+                std::memcpy(rgb, px.data(), px.size() * sizeof(uint16_t));
+            }
+            return CR_OK;
+        },
+        CR_E_INVALID);
+}
+
+int chiaro_float_to_half(const float *in, uint16_t *out, size_t n) {
+    if ((!in || !out) && n) return CR_E_INVALID;
+    for (size_t i = 0; i < n; i++) out[i] = chiaro::float_to_half(in[i]);
+    return CR_OK;
+}
 
 int chiaro_checkpoint_write(const char *path, const chiaro_checkpoint *h, const float *pixels) {
     if (!path || !h || !pixels) return CR_E_INVALID;

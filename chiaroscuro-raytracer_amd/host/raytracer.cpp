@@ -2,6 +2,7 @@
 #include "raytracer.hpp"
 
 #include "checkpoint.hpp"
+#include "exr.hpp"
 
 #include <chrono>
 #include <cmath>
@@ -269,39 +270,9 @@ void RayTracer::exportImage(const char *filename) {
             }
             o.write((const char *)row.data(), (std::streamsize)row.size());
         }
-    } else if (ends_with(fn, ".exr")) { // scanline, uncompressed, FLOAT B,G,R
-        std::vector<unsigned char> h;
-        auto u32 = [&](uint32_t v) { for (int i = 0; i < 4; i++) h.push_back((unsigned char)(v >> (8 * i))); };
-        auto str = [&](const char *s) { h.insert(h.end(), s, s + std::strlen(s) + 1); };
-        u32(20000630u); u32(2u);
-        str("channels"); str("chlist"); u32(3 * 18 + 1);
-        for (const char *ch : {"B", "G", "R"}) { str(ch); u32(2u); u32(0u); u32(1u); u32(1u); }
-        h.push_back(0);
-        str("compression"); str("compression"); u32(1); h.push_back(0);
-        str("dataWindow"); str("box2i"); u32(16); u32(0); u32(0); u32(W - 1); u32(H - 1);
-        str("displayWindow"); str("box2i"); u32(16); u32(0); u32(0); u32(W - 1); u32(H - 1);
-        str("lineOrder"); str("lineOrder"); u32(1); h.push_back(0);
-        str("pixelAspectRatio"); str("float"); u32(4); { float one = 1.f; uint32_t b; std::memcpy(&b, &one, 4); u32(b); }
-        str("screenWindowCenter"); str("v2f"); u32(8); u32(0); u32(0);
-        str("screenWindowWidth"); str("float"); u32(4); { float one = 1.f; uint32_t b; std::memcpy(&b, &one, 4); u32(b); }
-        h.push_back(0);
-        const uint64_t line_bytes = 8 + 12ull * W;
-        const uint64_t table_end = h.size() + 8ull * H;
-        for (unsigned y = 0; y < H; y++) {
-            const uint64_t off = table_end + line_bytes * y;
-            for (int i = 0; i < 8; i++) h.push_back((unsigned char)(off >> (8 * i)));
-        }
-        o.write((const char *)h.data(), (std::streamsize)h.size());
-        std::vector<float> line(3 * (size_t)W);
-        for (unsigned y = 0; y < H; y++) {
-            const int32_t yy = (int32_t)y;
-            const uint32_t sz = 12 * W;
-            o.write((const char *)&yy, 4);
-            o.write((const char *)&sz, 4);
-            for (int c = 2, k = 0; c >= 0; c--, k++)
-                for (unsigned x = 0; x < W; x++) line[(size_t)k * W + x] = pixels[3 * ((size_t)y * W + x) + c];
-            o.write((const char *)line.data(), (std::streamsize)(line.size() * 4));
-        }
+    } else if (ends_with(fn, ".exr")) { // HALF B, G, R, PIZ: what FreeImage_Save(FIF_EXR, ..., 0) writes
+        const std::vector<unsigned char> f = chiaro::exr_encode(pixels.data(), (int)W, (int)H);
+        o.write((const char *)f.data(), (std::streamsize)f.size());
     } else { // 8-bit: rows of `data` are bottom-up (rayTracer.cpp:217), write top-down
         normalizeImage();
         if (ends_with(fn, ".png")) {

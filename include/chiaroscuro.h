@@ -108,6 +108,16 @@ int chiaro_checkpoint_write(const char *path, const chiaro_checkpoint *h, const 
 int chiaro_checkpoint_read(const char *path, chiaro_checkpoint *h, float *pixels);
 void chiaro_raytracer_destroy(chiaro_raytracer *r);
 
+/* OpenEXR as the reference's exportImage writes it (FreeImage_Save(FIF_EXR, FIT_RGBF, 0),
+ * src/rayTracer.cpp:229-272): channels B, G, R of HALF, PIZ compression, increasing-Y lines.
+ * rgb [H][W][3] (R, G, B; row 0 = top); floats are rounded to half (nearest even, overflow to
+ * infinity).  chiaro_exr_read_half reads scanline HALF R/G/B files with NO or PIZ compression;
+ * with rgb NULL it returns the size only; cap = halves available at rgb. */
+int chiaro_exr_write(const char *path, const float *rgb, uint32_t w, uint32_t h);
+int chiaro_exr_write_half(const char *path, const uint16_t *rgb, uint32_t w, uint32_t h);
+int chiaro_exr_read_half(const char *path, uint32_t *w, uint32_t *h, uint16_t *rgb, size_t cap);
+int chiaro_float_to_half(const float *in, uint16_t *out, size_t n);
+
 int chiaro_camera(const float eye[3], const float center[3], const float up[3], float yview, uint32_t xres,
                   uint32_t yres, cr_camera *out);
 

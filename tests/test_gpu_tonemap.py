@@ -64,32 +64,6 @@ def test_raytracer_normalize_image_on_rendered_frame(ca, po, scenes):
     _compare(rt.getData(), po.tonemap(rt.pixels, i["exposure"]), "nanobox scene exposure")
 
 
-def _read_exr(path):
-    """Minimal reader of the scanline, uncompressed, FLOAT B,G,R file exportImage writes."""
-    b = open(path, "rb").read()
-    assert b[:4] == (20000630).to_bytes(4, "little")
-    pos, attrs = 8, {}
-    while b[pos] != 0:
-        name_end = b.index(b"\0", pos)
-        name = b[pos:name_end].decode()
-        type_end = b.index(b"\0", name_end + 1)
-        size = int.from_bytes(b[type_end + 1:type_end + 5], "little")
-        attrs[name] = b[type_end + 5:type_end + 5 + size]
-        pos = type_end + 5 + size
-    pos += 1
-    x0, y0, x1, y1 = np.frombuffer(attrs["dataWindow"], "<i4")
-    w, h = x1 - x0 + 1, y1 - y0 + 1
-    assert attrs["compression"] == b"\0"
-    offsets = np.frombuffer(b[pos:pos + 8 * h], "<u8")
-    img = np.zeros((h, w, 3), np.float32)
-    for y, off in enumerate(int(o) for o in offsets):
-        yy, sz = (int(v) for v in np.frombuffer(b[off:off + 8], "<i4"))
-        assert yy == y and sz == 12 * w
-        line = np.frombuffer(b[off + 8:off + 8 + sz], "<f4").reshape(3, w)  # B, G, R planes
-        img[y] = line[::-1].T
-    return img
-
-
 def _read_hdr(path):
     """Radiance RGBE, flat scanlines, -Y H +X W -> [H][W][3] float32 (row 0 = top)."""
     b = open(path, "rb").read()
@@ -105,8 +79,10 @@ def _read_hdr(path):
 
 def test_export_formats_round_trip(ca, scenes, tmp_path):
     """RayTracer.exportImage (rayTracer.cpp:225-279 with this build's writers, FreeImage
-    being absent): PFM and EXR hold the float pixels exactly, HDR within RGBE's 8-bit
-    mantissa, PNG and PPM the normalizeImage bytes (top row first)."""
+    being absent): PFM holds the float pixels exactly, EXR their halves (HALF PIZ, as
+    FreeImage's EXR save; tests/test_exr.py pins the codec against the reference's own
+    renders), HDR within RGBE's 8-bit mantissa, PNG and PPM the normalizeImage bytes (top
+    row first)."""
     from PIL import Image
 
     sc = ca.Scene(scenes.config_rtc("nanobox"), "xres", "64", "yres", "36", "samples", "2")
@@ -124,7 +100,7 @@ def test_export_formats_round_trip(ca, scenes, tmp_path):
     raw = open(tmp_path / "a.pfm", "rb").read().split(b"\n", 3)[3]
     pfm = np.frombuffer(raw, "<f4").reshape(36, 64, 3)[::-1]
     assert np.array_equal(pfm.view(np.uint32), px.view(np.uint32))
-    assert np.array_equal(_read_exr(tmp_path / "a.exr").view(np.uint32), px.view(np.uint32))
+    assert np.array_equal(ca.exr_read_half(tmp_path / "a.exr"), ca.float_to_half(px))
     hdr = _read_hdr(tmp_path / "a.hdr")
     peak = np.maximum(px.max(axis=2, keepdims=True), 1e-30)
     assert np.all(np.abs(hdr - px) <= peak / 128.0 + 1e-30)
