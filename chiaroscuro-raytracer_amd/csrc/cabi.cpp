@@ -75,6 +75,9 @@ int grow(cr_ctx *c, void **buf, size_t &cap, size_t need) {
     return CR_OK;
 }
 
+// scenes with fewer triangles default to trace build 18 instead of 26 (fill_args)
+const uint32_t LEAF_CULL_MIN_TRIS = 65536;
+
 void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_render_params *p, float *out, int mode) {
     A.S = c->S;
     std::memcpy(A.cam, cam->eye, 3 * sizeof(float));
@@ -130,7 +133,13 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 26 = 18 whose secondary closest and shadow traces (and the tail) skip the references a
     // leaf's cull record excludes for the ray (leafcull.hpp, packed fixed-pad form): shadow trace
     // 58.2 -> 53.3 ms per launch, closest 99.8 -> 91.5 ms beside it, 391.5 -> 367 ms per pass
-    A.variant = c->variant >= 0 ? c->variant : (c->kernel == 2 ? 26 : 0);
+    // the leaf cull (26) pays on large scenes only (round 3, 1080p): sponza stand-in (261k triangles)
+    // 391.5 -> 366 ms per pass, nanobox stand-in (20k) 167.6 -> 171.0, cornell_box (36) 147.9 -> 149.3
+    // -- on small trees a leaf's references lie close to its cell and the record costs more than
+    // the tests it removes -- so scenes below LEAF_CULL_MIN_TRIS triangles default to 18
+    A.variant = c->variant >= 0 ? c->variant
+                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 26 : 18)
+                                 : 0;
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
@@ -146,8 +155,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     if (c->kernel == 2 && !c->full_counters && !cr::wf_variant_available(A.variant))
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
                                          " is not compiled in (make ALL_VARIANTS=1)");
-    if (c->perf_counters && (c->kernel != 2 || c->full_counters || A.variant != 26))
-        return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's default trace build 26 only, "
+    if (c->perf_counters && (c->kernel != 2 || c->full_counters || !cr::wf_perf_available(A.variant)))
+        return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18 and 26 only, "
                                      "without the counting build");
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     if (c->kernel == 0 || c->kernel == 2) {
@@ -679,6 +688,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     }
     c->stack_depth = std::max(tree_depth, std::max(d->max_depth, 1u));
     c->n_refs = d->n_refs;
+    c->n_tris = d->n_tris;
     for (int a = 0; a < 3; a++) c->splits[a].clear();
     for (uint32_t i = 0; i < NN; i++)
         if (d->nodes[i].axis < 3) c->splits[d->nodes[i].axis].push_back(d->nodes[i].split);

@@ -30,6 +30,7 @@ struct cr_ctx {
     cr::DevScene S{};
     uint32_t stack_depth = 1;
     uint32_t n_refs = 0;     // leaf references (triangle records) of the scene
+    uint32_t n_tris = 0;     // triangles of the scene (the default trace build depends on it)
     std::vector<float> splits[3]; // split positions of the inner nodes per axis, sorted (eye_on_split)
     // inner kd nodes grouped by depth (device ids, deepest level first) and the
     // [offset, count) of each level: the bottom-up pass of the subtree cull boxes

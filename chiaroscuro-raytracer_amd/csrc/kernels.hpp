@@ -231,6 +231,7 @@ int num_wf_variants();
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
 bool wf_variant_available(int variant); // compiled in (the default compile holds builds 0, 15, 18, 26)
+bool wf_perf_available(int variant);    // a performed-work instance of this trace build exists (18, 26)
 // cull boxes of this render's camera for the nrefs leaf references (+ 4 padding boxes)
 // and their unions per subtree (node_boxes[n_nodes]): leaves first, then the inner
 // nodes level by level from the deepest (levels: inner node ids grouped by depth,

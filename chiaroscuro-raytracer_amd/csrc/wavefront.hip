@@ -1047,10 +1047,14 @@ static const WfVariant kWf[] = {
     // 31: 26 whose secondary closest trace does not cull leaves (build 18's): 371.0 ms
     CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4})};
-// Build 26 with the performed-work counts (RenderArgs::perf_counters; measurement only)
-static const WfVariant kWfPerf = {
+// Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
+static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>, 8, 8, 0, 2, 1, 4};
+static const WfVariant kWfPerf18 = {
+    wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>,
+    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>, 8, 8, 0, 2, 1, 0};
+bool wf_perf_available(int variant) { return variant == 18 || variant == 26; }
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
                                    0, 0, 0};
@@ -1204,7 +1208,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
                            TraceEvents *te) {
     WfArgs W = W0;
     const WfVariant &v = A.full_counters ? kWfCount
-                         : A.perf_counters ? kWfPerf
+                         : A.perf_counters ? (A.variant == 18 ? kWfPerf18 : kWfPerf26)
                                            : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
@@ -1223,8 +1227,10 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
-        else if (A.perf_counters)
+        else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+        else if (A.perf_counters)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
         else if (v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
         else
@@ -1286,7 +1292,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
 
 int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hipStream_t st, TraceEvents *te) {
     const WfVariant &v = A.full_counters ? kWfCount
-                         : A.perf_counters ? kWfPerf
+                         : A.perf_counters ? (A.variant == 18 ? kWfPerf18 : kWfPerf26)
                                            : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
@@ -1311,8 +1317,10 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
-        else if (A.perf_counters)
+        else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+        else if (A.perf_counters)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else

@@ -614,13 +614,14 @@ def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
     assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2
 
 
+@pytest.mark.parametrize("variant", [18, 26])
 @pytest.mark.parametrize("tail_min", [0, 3000])
-def test_perf_counters_build(ca, sponza, nanobox, tail_min):
-    """The performed-work build (option perf_counters: build 26's kernels with counters,
-    cr_get_perf) renders the same bits, and its counts agree with the counting build's:
-    the secondary and shadow traces take the reference traversal (steps and leaves equal),
-    the leaf cull and the camera culls only remove triangle tests (and, for the packet
-    camera trace, steps of rays a subtree box excludes)."""
+def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
+    """The performed-work builds (option perf_counters: builds 18 / 26 with counters, cr_get_perf)
+    render the same bits, and their counts agree with the counting build's: the secondary and
+    shadow traces take the reference traversal (steps and leaves equal; build 18 also runs every
+    test, build 26's leaf cull only removes some), the packet camera trace only removes tests and
+    the steps of rays a subtree box excludes."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_tail_min", tail_min)
@@ -630,15 +631,17 @@ def test_perf_counters_build(ca, sponza, nanobox, tail_min):
             pair.dev.render(cam, p, None)
             gc, ts = pair.dev.counters(), pair.dev.trace_stats()
             pair.dev.set_option("counters", 0)
+            pair.dev.set_option("variant", variant)
             pair.dev.set_option("perf_counters", 1)
             g = pair.dev.render(cam, p, None)
             lc, perf = pair.dev.counters(), pair.dev.perf()
         finally:
             pair.dev.set_option("perf_counters", 0)
+            pair.dev.set_option("variant", -1)
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_tail_min", 0)
         o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=1)
-        assert_bitwise(g, o, "perf-counting build %dx%dx%d" % (x, y, s))
+        assert_bitwise(g, o, "perf-counting build %d %dx%dx%d" % (variant, x, y, s))
         assert {k: lc[k] for k in LEAN_KEYS} == {k: gc[k] for k in LEAN_KEYS}
         assert sum(v["queries"] for v in perf.values()) == gc["closest"] + gc["shadow"]
         for kind in ("camera", "closest", "shadow"):
@@ -649,7 +652,10 @@ def test_perf_counters_build(ca, sponza, nanobox, tail_min):
             assert pk["leaves"] <= rk["leaf"] and pk["steps"] <= rk["inner"], (kind, pk, rk)
             if kind != "camera" and tail_min == 0:
                 assert (pk["steps"], pk["leaves"]) == (rk["inner"], rk["leaf"]), (kind, pk, rk)
-                assert pk["masks"] <= pk["leaves"]
+                if variant == 18:
+                    assert pk["masks"] == 0 and pk["tests"] == rk["tritest"], (kind, pk, rk)
+                else:
+                    assert pk["masks"] <= pk["leaves"]
         if tail_min == 0:
             assert perf["tail"]["queries"] == 0
             assert perf["camera"]["tests"] < ts["camera"]["tritest"]
@@ -658,11 +664,11 @@ def test_perf_counters_build(ca, sponza, nanobox, tail_min):
 
 
 def test_perf_counters_default_build_only(ca, cornell):
-    """perf_counters instruments build 26 only: another build is refused loudly."""
+    """perf_counters instruments builds 18 and 26 only: another build is refused loudly."""
     cornell.dev.set_option("kernel", 2)
     cornell.dev.set_option("counters", 0)
     cornell.dev.set_option("perf_counters", 1)
-    cornell.dev.set_option("variant", 18)
+    cornell.dev.set_option("variant", 15)
     cam = cornell.camera(ca, 16, 16)
     try:
         with pytest.raises(RuntimeError):
@@ -671,3 +677,22 @@ def test_perf_counters_default_build_only(ca, cornell):
         cornell.dev.set_option("variant", -1)
         cornell.dev.set_option("perf_counters", 0)
         cornell.dev.set_option("counters", 1)
+
+
+def test_default_build_by_scene_size(ca, sponza, nanobox):
+    """The default trace build culls leaves (26) on the 261k-triangle sponza stand-in and not (18)
+    on the 20k-triangle nanobox stand-in (cabi.cpp LEAF_CULL_MIN_TRIS): seen through the
+    performed-work counts of the default build."""
+    masks = {}
+    for name, pair in (("sponza", sponza), ("nanobox", nanobox)):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("counters", 0)
+        pair.dev.set_option("perf_counters", 1)
+        try:
+            pair.dev.render(pair.camera(ca, 64, 36), ca.render_params(64, 36, 2, 6, 0xC41A05C0, layer=1), None)
+            perf = pair.dev.perf()
+        finally:
+            pair.dev.set_option("perf_counters", 0)
+            pair.dev.set_option("counters", 1)
+        masks[name] = perf["shadow"]["masks"] + perf["closest"]["masks"] + perf["tail"]["masks"]
+    assert masks["sponza"] > 0 and masks["nanobox"] == 0, masks
