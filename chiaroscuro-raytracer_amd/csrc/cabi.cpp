@@ -257,6 +257,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.leaf_keys = leaf_keys ? 1 : 0;
                 W.leaf_shift = c->wf_leaf_shift;
                 W.resolve_paths = c->wf_resolve_paths;
+                W.tail_overlap = c->wf_tail_overlap;
                 if (c->wf_sort) {
                     for (int q = 0; q < 2; q++)
                         for (int i = 0; i < 2; i++) {
@@ -940,6 +941,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!std::strcmp(key, "kernel") && (v == 0 || v == 1 || v == 2)) c->kernel = (int)v;
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
     else if (!std::strcmp(key, "perf_counters") && (v == 0 || v == 1)) c->perf_counters = (int)v;
+    else if (!std::strcmp(key, "wf_tail_overlap") && (v == 0 || v == 1)) c->wf_tail_overlap = (int)v;
     else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
     else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
     else if (!std::strcmp(key, "lc_min") && v >= 0 && v <= 33) c->lc_min = (uint32_t)v;

@@ -84,6 +84,10 @@ struct cr_ctx {
     // 1080p x 128 spp: 0 / 256K / 1M / 4M / 16M -> 594.7 / 591.6 / 590.2 / 592.9 / 626.5 ms;
     // rank 0 of an 8-way split: 0 / 64K / 256K / 1M / 4M -> 88.8 / 85.9 / 83.3 / 83.1 / 84.2 ms
     uint32_t wf_tail_min = 1u << 20;
+    // the tail starts beside the last shadow trace (WfArgs::tail_overlap); measured neutral (round 3:
+    // 366.5 / 367.2 vs 366.9 / 366.8 ms per pass, rank 0 of 8 57.25 vs 57.36 ms -- the tail's chains
+    // gain one shadow query each and share the GPU with that trace), so off by default
+    int wf_tail_overlap = 0;
     // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a
     // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
     // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do

@@ -218,6 +218,13 @@ struct WfArgs {
     uint32_t resolve_paths; // wf_resolve sweeps queues of >= P / this rays in path order (0: never)
     uint32_t leaf_shift; // leaf keys: the node index >> leaf_shift (depth-first numbering: a run of
                          // consecutive nodes is one region of the tree)
+    // Overlapped tail (launch_wavefront_chunk): the tail kernel for closest queue g + 1 starts beside
+    // the shadow trace of generation g.  tail_shadow_gen = g: wf_tail first traces each of its paths'
+    // generation-g shadow ray and resolves that bounce itself; ended_only = 1: the shadow trace and
+    // wf_resolve of generation g take only the paths that ended at g (bit 0 of the PS3 mark).
+    uint32_t tail_shadow_gen;
+    uint32_t ended_only;
+    int tail_overlap; // 1: hand the rest of a chunk to an overlapped tail (option "wf_tail_overlap")
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

@@ -34,6 +34,9 @@
 namespace cr {
 
 enum : uint32_t { NO_SLOT = 0xffffffffu, NO_PATH = 0xffffffffu };
+// sexcl[j]: the light triangle shadow ray j ignores, bit 31 set when the ray's path continues
+// (the overlapped tail traces those; triangle ids stay below 2^31)
+enum : uint32_t { SEXCL_CONT = 0x80000000u };
 
 // Block-aggregated append (call with the whole block, uniformly): one global
 // atomicAdd per block instead of one per wave -- same-address atomics from
@@ -249,9 +252,11 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         if (W.order) idx = W.order[idx]; // sorted queue: results still go to slot idx
                         if (PC) pc.vb += (W.order ? 4u : 0u) + 32u + (SHADOW ? 4u : 0u) + (CULL ? 8u : 0u);
                         const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
+                        // overlapped tail: a path that continues traces this ray in wf_tail
+                        if (SHADOW && W.ended_only && (W.sexcl[idx] & SEXCL_CONT)) continue;
                         o = ld3(r0);
                         d = ld3(r1);
-                        if (SHADOW) exclude = W.sexcl[idx];
+                        if (SHADOW) exclude = W.sexcl[idx] & ~SEXCL_CONT;
                         if (CULL) { // ray idx of generation 1 is path idx's camera ray
                             const float2 q = W.cxy[idx];
                             csx = q.x;
@@ -486,7 +491,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
             W.dw[(size_t)(2 * (g - 1)) * W.P + p].w = __uint_as_float(j);
             W.sray[2 * (size_t)j] = pk(sh.o, p);
             W.sray[2 * (size_t)j + 1] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
-            W.sexcl[j] = sh.light;
+            W.sexcl[j] = sh.light | (cont ? SEXCL_CONT : 0u);
             if (W.sort) {
                 W.key[0][0][j] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res * W.dir_res) + dir_bin(sh.d, W.dir_res)
                                  : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
@@ -535,7 +540,8 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
     if (W.resolve_paths && (uint64_t)n * W.resolve_paths >= (uint64_t)W.P) {
         for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < W.P; p += gridDim.x * blockDim.x) {
             const float4 s3 = PS(W, 3, p);
-            if ((__float_as_uint(s3.w) >> 1) == g) resolve_path(A, W, p, g, s3);
+            if ((__float_as_uint(s3.w) >> 1) == g && (!W.ended_only || (__float_as_uint(s3.w) & 1u)))
+                resolve_path(A, W, p, g, s3);
         }
         return;
     }
@@ -544,7 +550,11 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         if (hits[i].w == 0u) continue;
         const uint32_t p = __float_as_uint(rays[2 * (size_t)i].w);
-        resolve_path(A, W, p, g, PS(W, 3, p));
+        const float4 s3 = PS(W, 3, p);
+        // (overlapped tail: the tail may already have rewritten a continuing path's PS3 -- the mark
+        // then no longer names generation g)
+        if (W.ended_only && (__float_as_uint(s3.w) >> 1 != g || !(__float_as_uint(s3.w) & 1u))) continue;
+        resolve_path(A, W, p, g, s3);
     }
 }
 
@@ -558,6 +568,10 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
 // and kind.  Lanes refill from the queue (one atomicAdd per wave) when `refill`
 // of them are idle or none is busy; a lane with a finished query advances its
 // path at once.
+// Overlapped (W.tail_shadow_gen = g0 - 1 = gs): launched beside the shadow trace of generation gs,
+// which then takes only the paths that ended at gs; a lane first traces its path's generation-gs
+// shadow ray (slot in dw[2(gs-1)].w), resolves that bounce as wf_resolve does (same add), then
+// starts the path's closest query of g0.
 template <bool FULL, int R, int MINW, int LC = 0, bool PC = false>
 __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uint32_t g0) {
     extern __shared__ uint2 ring_lds[];
@@ -571,7 +585,9 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
     const float4 *rays = W.ray[g0 & 1];
     Ctr c = {};
     Pc pc = {};
-    uint32_t state = ST_NEED_WORK, p = 0, exclude = 0, nclosest = 0, nshadow = 0;
+    uint32_t state = ST_NEED_WORK, p = 0, exclude = 0, nclosest = 0, nshadow = 0, qidx = 0;
+    const uint32_t gs = W.tail_shadow_gen;
+    bool pend = false; // overlapped: the lane's generation-gs shadow query is in flight
     f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
     // start the next closest query of path p from (o, d); a root-box miss is a MISS at once
@@ -598,13 +614,37 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                     o = ld3(r0);
                     d = ld3(r1);
                     p = __float_as_uint(r0.w);
-                    if (p != NO_PATH) start_closest(); // dead camera ray of a partial tile: no query
+                    const uint32_t slot = (gs && p != NO_PATH)
+                                              ? __float_as_uint(W.dw[(size_t)(2 * (gs - 1)) * W.P + p].w) : NO_SLOT;
+                    if (slot != NO_SLOT) { // overlapped: this path's generation-gs shadow query first
+                        const float4 s0 = W.sray[2 * (size_t)slot], s1 = W.sray[2 * (size_t)slot + 1];
+                        if (PC) pc.vb += 36;
+                        qidx = idx;
+                        pend = true;
+                        o = ld3(s0);
+                        d = ld3(s1);
+                        exclude = W.sexcl[slot] & ~SEXCL_CONT;
+                        nshadow++;
+                        state = trav_begin(S, o, d, true, s1.w, T) ? ST_SHADOW : ST_VISIBLE;
+                    } else if (p != NO_PATH) {
+                        start_closest(); // (a dead camera ray of a partial tile: no query)
+                    }
                 }
             }
         }
         // advance every lane whose query has a result, until it has a new query or is idle
         while (state >= ST_HIT) {
-            if (state == ST_MISS) {
+            if (pend) { // overlapped: resolve bounce gs (wf_resolve's resolve_path, a path that continues)
+                float4 &dk = W.dw[(size_t)(2 * (gs - 1)) * W.P + p];
+                f3 direct = ld3(dk);
+                if (state == ST_VISIBLE) direct = add(direct, ld3(PS(W, 3, p)));
+                dk = pk(direct, 0u);
+                pend = false;
+                const float4 r0 = rays[2 * (size_t)qidx], r1 = rays[2 * (size_t)qidx + 1];
+                o = ld3(r0);
+                d = ld3(r1);
+                start_closest();
+            } else if (state == ST_MISS) {
                 finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
                 state = ST_NEED_WORK;
             } else if (state == ST_HIT) {
@@ -1221,21 +1261,21 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
     int err = 0;
     // the rest of the chunk from closest queue g on, in one launch
-    auto tail = [&](uint32_t g) {
+    auto tail = [&](uint32_t g, hipStream_t s, WfArgs Wt) {
         const size_t tlds = (size_t)8 * tblk * sizeof(uint2);
-        W.order = nullptr;
-        if ((err = trace_event(te, st, TK_TAIL, true))) return;
+        Wt.order = nullptr;
+        if ((err = trace_event(te, s, TK_TAIL, true))) return;
         if (A.full_counters)
-            hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+            hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters && v.lc == 4)
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters)
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (v.lc == 4)
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, st, A, W, g);
-        err = trace_event(te, st, TK_TAIL, false);
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+        err = trace_event(te, s, TK_TAIL, false);
     };
     // closest trace of generation g on stream s; its stack overflow rows are the
     // second half of gstack when it runs beside a shadow trace
@@ -1252,7 +1292,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     };
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
     if (W.P < W.tail_min) {
-        tail(1);
+        tail(1, st, W);
         return err ? err : (int)hipGetLastError();
     }
     closest(1, st, nullptr, W.gstack); // camera rays: path order is already coherent
@@ -1269,21 +1309,34 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         const uint32_t *order_s = order_queue(W, 0, cnt[0], st, err, pixel);
         const uint32_t *order_c = next ? order_queue(W, 1, nc, st, err, pixel) : nullptr;
         if (err) break;
-        if (next) {
+        // overlapped tail: the rest of the chunk starts beside this generation's shadow trace, tracing
+        // its own paths' shadow rays of generation g first (the paths that end at g stay with
+        // wf_trace / wf_resolve); needs NEE rays, which every hit has when the scene has lights
+        const bool overlap = !next && nc > 0 && W.tail_overlap && A.S.nlights > 0;
+        if (next || overlap) {
             if ((err = (int)hipEventRecord(ss.fork, st)) || (err = (int)hipStreamWaitEvent(ss.side, ss.fork, 0))) break;
-            closest(g + 1, ss.side, order_c, W.gstack2);
+            if (next) {
+                closest(g + 1, ss.side, order_c, W.gstack2);
+            } else {
+                WfArgs Wt = W;
+                Wt.gstack = W.gstack2;
+                Wt.tail_shadow_gen = g;
+                tail(g + 1, ss.side, Wt);
+            }
             if (err) break;
         }
         W.order = order_s;
+        W.ended_only = overlap ? 1u : 0u;
         if ((err = trace_event(te, st, TK_SHADOW, true))) break;
         hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, TK_SHADOW, false))) break;
         hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
-        if (next) {
+        W.ended_only = 0u;
+        if (next || overlap)
             if ((err = (int)hipEventRecord(ss.join, ss.side)) || (err = (int)hipStreamWaitEvent(st, ss.join, 0)))
                 break;
-        } else {
-            if (nc > 0) tail(g + 1);
+        if (!next) {
+            if (nc > 0 && !overlap) tail(g + 1, st, W);
             break;
         }
     }

@@ -258,13 +258,18 @@ def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
 
 
 @pytest.mark.parametrize("tail_min", [1 << 30, 12000, 3000])
-def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min):
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap):
     """wf_tail (the last generations of a chunk in one launch, per-path bodies
     shared with wf_shade / wf_bounce): from generation 1 (every queue is below
-    1 << 30) and from later generations, counting and lean builds."""
+    1 << 30) and from later generations, counting and lean builds; after the last shadow trace
+    (default) or overlapped (option wf_tail_overlap: the tail starts beside that trace and traces
+    its own paths' shadow rays of that generation, the shadow trace and wf_resolve keep the paths
+    that ended)."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4)), (cornell, (64, 64, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_tail_min", tail_min)
+        pair.dev.set_option("wf_tail_overlap", overlap)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
             pair.dev.set_option("counters", 0)
@@ -273,6 +278,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min):
         finally:
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_tail_min", 0)
+            pair.dev.set_option("wf_tail_overlap", 0)
         assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
         assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
