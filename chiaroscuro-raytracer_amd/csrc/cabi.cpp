@@ -258,6 +258,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.leaf_shift = c->wf_leaf_shift;
                 W.resolve_paths = c->wf_resolve_paths;
                 W.tail_overlap = c->wf_tail_overlap;
+                W.sort_g1 = c->wf_sort_g1;
+                W.cam_lean = c->wf_cam_lean;
                 if (c->wf_sort) {
                     for (int q = 0; q < 2; q++)
                         for (int i = 0; i < 2; i++) {
@@ -942,6 +944,8 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
     else if (!std::strcmp(key, "perf_counters") && (v == 0 || v == 1)) c->perf_counters = (int)v;
     else if (!std::strcmp(key, "wf_tail_overlap") && (v == 0 || v == 1)) c->wf_tail_overlap = (int)v;
+    else if (!std::strcmp(key, "wf_sort_g1") && v >= 0 && v <= 3) c->wf_sort_g1 = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_cam_lean") && (v == 0 || v == 1)) c->wf_cam_lean = (int)v;
     else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
     else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
     else if (!std::strcmp(key, "lc_min") && v >= 0 && v <= 33) c->lc_min = (uint32_t)v;

@@ -88,6 +88,8 @@ struct cr_ctx {
     // 366.5 / 367.2 vs 366.9 / 366.8 ms per pass, rank 0 of 8 57.25 vs 57.36 ms -- the tail's chains
     // gain one shadow query each and share the GPU with that trace), so off by default
     int wf_tail_overlap = 0;
+    uint32_t wf_sort_g1 = 3;        // generation-1 queues sorted: bit 0 shadow, bit 1 closest (WfArgs::sort_g1)
+    int wf_cam_lean = 1;            // WfArgs::cam_lean
     // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a
     // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
     // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do

@@ -225,6 +225,8 @@ struct WfArgs {
     uint32_t tail_shadow_gen;
     uint32_t ended_only;
     int tail_overlap; // 1: hand the rest of a chunk to an overlapped tail (option "wf_tail_overlap")
+    uint32_t sort_g1; // generation-1 queues that are sorted: bit 0 the shadow queue, bit 1 the closest queue
+    int cam_lean;     // 1: wf_camera leaves generation 1's RNG state to wf_shade (option "wf_cam_lean")
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

@@ -134,6 +134,20 @@ __device__ __forceinline__ void finish_path(const RenderArgs &A, const WfArgs &W
 //                             3 {contrib, shadow slot}  4 {next origin, -}
 __device__ __forceinline__ float4 &PS(const WfArgs &W, int slot, uint32_t p) { return W.ps[(size_t)slot * W.P + p]; }
 
+// Path state slots [slot][P]: 0 {direct, k}  1 {fcol, rng.key}  2 {normal, rng.ctr} ... (below).
+// When generation 1 runs as wavefront launches (the chunk is not handed to wf_tail at once), wf_camera
+// writes only slot 3 (the resolve mark): wf_shade derives generation 1's RNG state -- the camera
+// sample's stream after its two jitter draws -- from the path's (pixel, sample) instead of reading it.
+__device__ __forceinline__ bool camera_state_lean(const WfArgs &W) { return W.cam_lean && W.P >= W.tail_min; }
+__device__ __forceinline__ Rng camera_rng(const RenderArgs &A, const WfArgs &W, uint32_t p) {
+    const uint32_t w = W.w0 + p, item = w / A.s_count, s = A.s0 + (w - item * A.s_count);
+    uint32_t px = 0, py = 0;
+    item_pixel(A, item, px, py);
+    Rng rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
+    rng.ctr = 2u; // camera_dir's y- and x-jitter draws
+    return rng;
+}
+
 // ---------------------------------------------------------------- camera --
 __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
     __shared__ unsigned long long tl[T_N];
@@ -157,9 +171,11 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
             float2 sxy;
             const f3 d = camera_dir(A, px, py, rng, &sxy);
             if (A.cull) W.cxy[p] = sxy;
-            PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), 1u);
-            PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key);
-            PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
+            if (!camera_state_lean(W)) { // (wf_tail from generation 1 reads the state; wf_shade derives it)
+                PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), 1u);
+                PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key);
+                PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
+            }
             PS(W, 3, p) = make_float4(0.f, 0.f, 0.f, 0.f); // no resolve mark (wf_resolve)
             W.ray[1][2 * (size_t)p] = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(p));
             W.ray[1][2 * (size_t)p + 1] = pk(d, 0u);
@@ -419,7 +435,8 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
     const DevScene &S = A.S;
     const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
     textured = hs.textured;
-    Rng rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
+    const bool cam = k == 1u && camera_state_lean(W);
+    Rng rng = cam ? camera_rng(A, W, p) : Rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
     f3 contrib = mk(0.f, 0.f, 0.f), next = add(hs.p, muls(hs.normal, 0.001f));
     bool nee = false;
     if (S.nlights) {
@@ -444,6 +461,7 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
             const f3 w = divs(muls(hs.fcol, cosine), pdf * Kmax);
             W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
             PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), k + 1);
+            if (cam) PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key); // (wf_camera left it unwritten)
             PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
             org = next;
             cont = true;
@@ -1306,8 +1324,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         const uint32_t nc = g < (uint32_t)A.K ? cnt[1] : 0u;
         const bool next = nc >= W.tail_min && nc > 0; // closest g + 1 as its own launch, beside shadow g
         const bool pixel = !W.leaf_keys && !(W.world_keys && g >= (uint32_t)W.world_keys); // wf_shade's key choice
-        const uint32_t *order_s = order_queue(W, 0, cnt[0], st, err, pixel);
-        const uint32_t *order_c = next ? order_queue(W, 1, nc, st, err, pixel) : nullptr;
+        const uint32_t *order_s = (g > 1 || (W.sort_g1 & 1u)) ? order_queue(W, 0, cnt[0], st, err, pixel) : nullptr;
+        const uint32_t *order_c = (next && (g > 1 || (W.sort_g1 & 2u))) ? order_queue(W, 1, nc, st, err, pixel) : nullptr;
         if (err) break;
         // overlapped tail: the rest of the chunk starts beside this generation's shadow trace, tracing
         // its own paths' shadow rays of generation g first (the paths that end at g stay with

@@ -237,6 +237,29 @@ def test_packet_camera_eye_on_split_plane(ca, sponza, cornell, variant):
             pair.dev.set_option("variant", -1)
 
 
+@pytest.mark.parametrize("opts", [{"wf_cam_lean": 0}, {"wf_sort_g1": 0}, {"wf_sort_g1": 1}, {"wf_sort_g1": 2}])
+def test_wavefront_generation1_options_bitexact(ca, sponza, nanobox, opts):
+    """wf_camera writing generation 1's RNG state (wf_cam_lean 0) instead of wf_shade deriving it,
+    and generation-1 queues traced unsorted (wf_sort_g1 bits): the same bits and counters, with and
+    without the tail from generation 1."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_sort_min", 0)
+        for k, v in opts.items():
+            pair.dev.set_option(k, v)
+        try:
+            for tail_min in (0, 3000):
+                pair.dev.set_option("wf_tail_min", tail_min)
+                g, gc, o, oc = _render_both(ca, pair, x, y, s)
+                assert_bitwise(g, o, "%s tail_min %d %dx%dx%d" % (opts, tail_min, x, y, s))
+                assert {k: gc[k] for k in ORACLE_KEYS} == oc
+        finally:
+            pair.dev.set_option("wf_cam_lean", 1)
+            pair.dev.set_option("wf_sort_g1", 3)
+            pair.dev.set_option("wf_sort_min", 1 << 20)
+            pair.dev.set_option("wf_tail_min", 0)
+
+
 @pytest.mark.parametrize("lanes", [1, 2])
 def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
     """Two chunks in flight (wf_lanes 2: the frame's paths split in two, the second
