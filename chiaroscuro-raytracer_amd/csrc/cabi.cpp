@@ -209,12 +209,21 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             const int key_bits_pixel = key_bits;
             const uint64_t nworld = (1ull << (3 * c->wf_world_bits)) * c->wf_dir_res * c->wf_dir_res;
             while (c->wf_world_keys && key_bits < 32 && (1ull << key_bits) < nworld) key_bits++;
-            // leaf keys: (leaf node, direction bin) when they fit 32 bits
-            int leaf_bits = 1;
-            while (leaf_bits < 40 &&
-                   (1ull << leaf_bits) < (((uint64_t)A.S.n_nodes >> c->wf_leaf_shift) + 1) * c->wf_dir_res * c->wf_dir_res)
-                leaf_bits++;
+            // leaf keys: (leaf node >> wf_leaf_shift, direction bin); the direction grid is halved
+            // until the key fits 32 bits (the sponza stand-in keeps 128 x 128 bins at shift 1)
+            auto leaf_width = [&](uint64_t dres) {
+                int b = 1;
+                while (b < 40 && (1ull << b) < (((uint64_t)A.S.n_nodes >> c->wf_leaf_shift) + 1) * dres * dres) b++;
+                return b;
+            };
+            uint32_t dres_l = c->wf_dir_res;
+            while (dres_l > 8 && leaf_width(dres_l) > 32) dres_l >>= 1;
+            const int leaf_bits = leaf_width(dres_l);
             const bool leaf_keys = c->wf_leaf_keys && leaf_bits <= 32;
+            // the shadow queues' leaf keys may use another direction grid (option "wf_dir_res_shadow")
+            uint32_t dres_s = c->wf_dir_res_shadow ? c->wf_dir_res_shadow : dres_l;
+            while (dres_s > 1 && leaf_width(dres_s) > 32) dres_s >>= 1;
+            const int leaf_bits_s = leaf_width(dres_s);
             // (leaf keys replace the pixel and world keys in every queue: their width alone sets the
             // digit passes)
             if (leaf_keys) key_bits = leaf_bits;
@@ -249,7 +258,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.sort_lib = c->wf_sort_lib;
                 W.sort_min = c->wf_sort_min;
                 W.sort_tile = c->wf_sort_tile;
-                W.dir_res = c->wf_dir_res;
+                W.dir_res = leaf_keys ? dres_l : c->wf_dir_res;
+                W.dir_res_s = leaf_keys ? dres_s : c->wf_dir_res;
+                W.key_bits_s = leaf_keys ? leaf_bits_s : key_bits;
                 W.world_keys = nworld <= (1ull << 32) ? c->wf_world_keys : 0;
                 W.world_bits = c->wf_world_bits;
                 W.tail_min = c->wf_tail_min;
@@ -260,6 +271,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.tail_overlap = c->wf_tail_overlap;
                 W.sort_g1 = c->wf_sort_g1;
                 W.cam_lean = c->wf_cam_lean;
+                W.tail_waves = c->wf_tail_waves;
                 if (c->wf_sort) {
                     for (int q = 0; q < 2; q++)
                         for (int i = 0; i < 2; i++) {
@@ -946,6 +958,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_tail_overlap") && (v == 0 || v == 1)) c->wf_tail_overlap = (int)v;
     else if (!std::strcmp(key, "wf_sort_g1") && v >= 0 && v <= 3) c->wf_sort_g1 = (uint32_t)v;
     else if (!std::strcmp(key, "wf_cam_lean") && (v == 0 || v == 1)) c->wf_cam_lean = (int)v;
+    else if (!std::strcmp(key, "wf_tail_waves") && v >= 4 && v <= 6) c->wf_tail_waves = (int)v;
     else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
     else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
     else if (!std::strcmp(key, "lc_min") && v >= 0 && v <= 33) c->lc_min = (uint32_t)v;
@@ -964,6 +977,8 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_sort_tile") && v >= 0 && v <= 5) c->wf_sort_tile = (uint32_t)v;
     else if (!std::strcmp(key, "wf_dir_res") && v >= 1 && v <= 256 && (v & (v - 1)) == 0)
         c->wf_dir_res = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_dir_res_shadow") && v >= 0 && v <= 256 && (v & (v - 1)) == 0)
+        c->wf_dir_res_shadow = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
 #ifdef CR_SORT_LIB
     else if (!std::strcmp(key, "wf_sort_lib") && (v == 0 || v == 1)) c->wf_sort_lib = (int)v;

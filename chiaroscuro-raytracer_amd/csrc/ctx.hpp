@@ -77,7 +77,8 @@ struct cr_ctx {
     uint32_t wf_sort_tile = 4;      // key: log2 pixel sub-tile edge
     // direction bins per octahedral axis: 32 -> 64 575.6 -> 570.2 ms per pass, rank 0 of 8 79.6 -> 78.0
     // (world bits 5 / 7 and 16 bins measured slower; 7 bits x 64 bins: 31-bit keys, 607 ms)
-    uint32_t wf_dir_res = 64;       // key: direction bins per octahedral axis
+    uint32_t wf_dir_res = 128;      // key: direction bins per octahedral axis (round 3: 128 at leaf shift 1,
+                                    // 365.1 vs 367.1 ms per pass; halved for leaf keys until they fit 32 bits)
     int wf_world_keys = 2;          // key: world-space origins for queues starting at hits of gen >= 2
     uint32_t wf_world_bits = 6;     // key: Morton bits per axis of the origin
     // closest queues shorter than this finish in one wf_tail launch (0: never).  Sweep, sponza
@@ -90,6 +91,8 @@ struct cr_ctx {
     int wf_tail_overlap = 0;
     uint32_t wf_sort_g1 = 3;        // generation-1 queues sorted: bit 0 shadow, bit 1 closest (WfArgs::sort_g1)
     int wf_cam_lean = 1;            // WfArgs::cam_lean
+    int wf_tail_waves = 4;          // WfArgs::tail_waves
+    uint32_t wf_dir_res_shadow = 0; // shadow queues' direction bins per axis with leaf keys (0: wf_dir_res)
     // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a
     // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
     // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do
@@ -104,7 +107,7 @@ struct cr_ctx {
     // 2 interleaved rounds: pixel / world keys 409.5 -> leaf keys 396.4 ms per pass; coarser
     // regions (node index >> 3 / 6 / 9) 405.2 / 418.7 / 440.2 vs 401.6 ms, 32 direction bins 409.3
     int wf_leaf_keys = 1;
-    uint32_t wf_leaf_shift = 0; // ... its node index >> this
+    uint32_t wf_leaf_shift = 1; // ... its node index >> this (a leaf and its sibling share a key region)
     // sweep (1080p x 128 spp, 2 rounds): 0 / 1 / 2 / 4 / 8 / 16 / 64 -> 399.2 / 394.6 / 394.8 / 394.8 / 393.8 / 393.6 / 394.5 ms
     uint32_t wf_resolve_paths = 16; // wf_resolve in path order for queues of at least P / this rays (0: never)
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene

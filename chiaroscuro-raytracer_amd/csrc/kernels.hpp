@@ -227,6 +227,9 @@ struct WfArgs {
     int tail_overlap; // 1: hand the rest of a chunk to an overlapped tail (option "wf_tail_overlap")
     uint32_t sort_g1; // generation-1 queues that are sorted: bit 0 the shadow queue, bit 1 the closest queue
     int cam_lean;     // 1: wf_camera leaves generation 1's RNG state to wf_shade (option "wf_cam_lean")
+    uint32_t dir_res_s; // leaf keys: direction bins per axis of the SHADOW queues' keys
+    int key_bits_s;     // significant bits of the shadow queues' keys
+    int tail_waves;     // waves per SIMD of the lean tail launch (4, 5, 6)
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

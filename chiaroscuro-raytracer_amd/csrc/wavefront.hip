@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
             W.sray[2 * (size_t)j + 1] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
             W.sexcl[j] = sh.light | (cont ? SEXCL_CONT : 0u);
             if (W.sort) {
-                W.key[0][0][j] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res * W.dir_res) + dir_bin(sh.d, W.dir_res)
+                W.key[0][0][j] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res_s * W.dir_res_s) + dir_bin(sh.d, W.dir_res_s)
                                  : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
                                                                                  : sort_key(A, W, p, sh.d);
                 W.perm[0][0][j] = j;
@@ -1203,7 +1203,7 @@ static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStre
     if (!W.sort || err || n < W.sort_min) return nullptr;
     uint32_t *keys[2] = {W.key[set][0], W.key[set][1]}, *vals[2] = {W.perm[set][0], W.perm[set][1]};
     size_t tb = W.sort_tmp_bytes;
-    const int bits = pixel ? W.key_bits_pixel : W.key_bits;
+    const int bits = pixel ? W.key_bits_pixel : (set == 0 ? W.key_bits_s : W.key_bits);
     const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, W.sort_lib != 0);
     if (sel < 0) {
         err = (int)hipErrorUnknown;
@@ -1244,6 +1244,14 @@ static int trace_event(TraceEvents *te, hipStream_t st, int kind, bool start) {
 // Tail kernel builds: lean and counting; 4 waves/SIMD (the path bodies need more
 // registers than the trace kernels' 64).
 enum { TAIL_MINW = 4 };
+// lean tail launch at `waves` per SIMD (option "wf_tail_waves"; 4, 5 or 6)
+template <int LC> static void launch_tail_lean(int waves, uint32_t blk, int num_cus, size_t lds, hipStream_t s,
+                                               const RenderArgs &A, const WfArgs &W, uint32_t g) {
+    const uint32_t cus = (uint32_t)(num_cus > 0 ? num_cus : 256);
+    if (waves == 5) hipLaunchKernelGGL((wf_tail<false, 8, 5, LC>), dim3(cus * 5), dim3(blk), lds, s, A, W, g);
+    else if (waves == 6) hipLaunchKernelGGL((wf_tail<false, 8, 6, LC>), dim3(cus * 6), dim3(blk), lds, s, A, W, g);
+    else hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, LC>), dim3(cus * TAIL_MINW), dim3(blk), lds, s, A, W, g);
+}
 void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks) {
     block = 256;
     blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * TAIL_MINW;
@@ -1290,9 +1298,9 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         else if (A.perf_counters)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (v.lc == 4)
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+            launch_tail_lean<4>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
         else
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+            launch_tail_lean<0>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
         err = trace_event(te, s, TK_TAIL, false);
     };
     // closest trace of generation g on stream s; its stack overflow rows are the

@@ -57,7 +57,7 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir, leaf):
         finally:
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_sort_tile", 4)
-            pair.dev.set_option("wf_dir_res", 64)
+            pair.dev.set_option("wf_dir_res", 128)
             pair.dev.set_option("wf_leaf_keys", 1)
         assert_bitwise(g, o, "sorted wavefront %dx%dx%d" % (x, y, s))
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
@@ -237,11 +237,14 @@ def test_packet_camera_eye_on_split_plane(ca, sponza, cornell, variant):
             pair.dev.set_option("variant", -1)
 
 
-@pytest.mark.parametrize("opts", [{"wf_cam_lean": 0}, {"wf_sort_g1": 0}, {"wf_sort_g1": 1}, {"wf_sort_g1": 2}])
+@pytest.mark.parametrize("opts", [{"wf_cam_lean": 0}, {"wf_sort_g1": 0}, {"wf_sort_g1": 1}, {"wf_sort_g1": 2},
+                                  {"wf_tail_waves": 5}, {"wf_tail_waves": 6}, {"wf_dir_res_shadow": 1},
+                                  {"wf_dir_res_shadow": 4}])
 def test_wavefront_generation1_options_bitexact(ca, sponza, nanobox, opts):
     """wf_camera writing generation 1's RNG state (wf_cam_lean 0) instead of wf_shade deriving it,
-    and generation-1 queues traced unsorted (wf_sort_g1 bits): the same bits and counters, with and
-    without the tail from generation 1."""
+    generation-1 queues traced unsorted (wf_sort_g1 bits), the tail at 5 / 6 waves per SIMD, shadow
+    queue keys with fewer direction bins: the same bits and counters, with and without the tail
+    from generation 1."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_sort_min", 0)
@@ -256,6 +259,8 @@ def test_wavefront_generation1_options_bitexact(ca, sponza, nanobox, opts):
         finally:
             pair.dev.set_option("wf_cam_lean", 1)
             pair.dev.set_option("wf_sort_g1", 3)
+            pair.dev.set_option("wf_tail_waves", 4)
+            pair.dev.set_option("wf_dir_res_shadow", 0)
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_tail_min", 0)
 
