@@ -149,7 +149,8 @@ class ChiaroSceneInfo(C.Structure):
 TRACE_KINDS = ("camera", "closest", "shadow", "tail")  # cr_trace_stats order
 DIAG_NAMES = ("rounds", "lanes", "distinct", "records", "maxcount", "lanetests", "fit64", "fit128",
               "urounds", "tests", "geomiss", "rep1", "rep4", "rep8")  # cr_get_diag order (DIAG_* in kernels.hpp)
-PERF_NAMES = ("queries", "steps", "leaves", "masks", "tests", "vbytes", "sbytes", "waves")  # cr_get_perf (PERF_*)
+PERF_NAMES = ("queries", "steps", "leaves", "masks", "tests", "vbytes", "sbytes", "waves",
+              "drounds", "diters", "dlanes", "dtests")  # cr_get_perf (PERF_* in kernels.hpp)
 
 
 class CrTraceStats(C.Structure):

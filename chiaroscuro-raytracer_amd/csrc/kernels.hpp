@@ -9,7 +9,7 @@ enum { MODE_BLEND = 0, MODE_TILES = 1 };
 // float4 per triangle record.  3 (48 B, 1.5 lines per test on average) beat 4
 // (one 64-B line per test, +33% footprint): 561 vs 547 Mray/s, sponza 8 spp.
 enum { REC_STRIDE = 3 };
-enum { CTR_N = 22, CTR_SLOTS = 96 }; // Ctr fields (cr_counters order); device counter buffer entries
+enum { CTR_N = 22, CTR_SLOTS = 112 }; // Ctr fields (cr_counters order); device counter buffer entries
 // Wavefront trace launches by kind (cr_trace_stats order): camera rays (generation-1
 // closest trace), closest traces of later generations, shadow traces, the tail kernel.
 enum { TK_CAMERA = 0, TK_CLOSEST = 1, TK_SHADOW = 2, TK_TAIL = 3, TK_N = 4 };
@@ -39,7 +39,7 @@ enum {
 // per trace kind, slots CTR_PERF + PERF_N * kind + PERF_*.  What the kernels actually execute
 // and load -- after the cull boxes, leaf cull records and packet traversal skipped work --
 // where the counting build (full_counters) counts the reference algorithm's work.
-enum { CTR_PERF = 64, PERF_N = 8 };
+enum { CTR_PERF = 64, PERF_N = 12 };
 enum {
     PERF_QUERIES = 0, // queries started (ray fetched from the queue)
     PERF_STEPS = 1,   // inner-node decisions, per ray
@@ -49,6 +49,10 @@ enum {
     PERF_VBYTES = 5,  // bytes of vector-memory loads and stores (per lane) of the trace
     PERF_SBYTES = 6,  // bytes of scalar-memory loads (per wave)
     PERF_WAVES = 7,   // wave iterations: traversal rounds (wf_trace, tail) / node fetches (packet)
+    PERF_DROUNDS = 8, // divergent leaf rounds of the leaf-cull loop with a test to run (wave)
+    PERF_DITERS = 9,  //   their loop iterations (the largest lane mask's popcount, summed; wave)
+    PERF_DLANES = 10, //   lanes with a test, summed (wave)
+    PERF_DTESTS = 11, //   tests, summed (lane)
 };
 
 // Zero bytes appended after every texture: the reference's getColorAt reads one

@@ -77,15 +77,28 @@ __device__ __forceinline__ uint64_t prof_now() { return __builtin_amdgcn_s_memti
 struct Pc {
     uint32_t q, steps, leaves, masks, tests, waves;
     uint64_t vb, sb;
+    uint32_t drounds, diters, dlanes, dtests;
 };
 __device__ __forceinline__ void pc_load(Pc *pc, bool scalar, uint32_t bytes) {
     if (!pc) return;
     if (!scalar) pc->vb += bytes;
     else if (wave_leader()) pc->sb += bytes;
 }
+// Per-wave LDS of the dealt shadow-leaf tests (trav_round's DEAL): owner lane per start position, the
+// start positions' mask, the accepted tests' mask (bit = worker rank).
+struct DealLds {
+    unsigned long long smask, rmask;
+    uint8_t tab[64];
+};
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Call with the whole wave converged: the lane sums go to ctrs[0 .. PERF_N).
 __device__ __forceinline__ void pc_flush(unsigned long long *ctrs, const Pc &pc) {
-    const unsigned long long v[PERF_N] = {pc.q, pc.steps, pc.leaves, pc.masks, pc.tests, pc.vb, pc.sb, pc.waves};
+    const unsigned long long v[PERF_N] = {pc.q,     pc.steps,   pc.leaves, pc.masks,  pc.tests,  pc.vb,
+                                          pc.sb,    pc.waves,   pc.drounds, pc.diters, pc.dlanes, pc.dtests};
 #pragma unroll
     for (int i = 0; i < PERF_N; i++) {
         unsigned long long x = v[i];
@@ -300,13 +313,14 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // LC (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a leaf's tests run only
 // for the references its cull record (leafcull.hpp) cannot exclude for this ray and segment.
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0, bool REV = false>
+          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0, bool REV = false, bool DEAL = false>
 __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
-                                               Prof *pf = nullptr, Pc *pc = nullptr, const float *rcp_lds = nullptr) {
+                                               Prof *pf = nullptr, Pc *pc = nullptr, const float *rcp_lds = nullptr,
+                                               DealLds *deal = nullptr) {
     uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
     if (pf) pt0 = prof_now();
     if (pc && wave_leader()) pc->waves++;
@@ -324,6 +338,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
     static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
     static_assert(!REV || (BF && !FULL), "far-first order: lean BF builds (shadow queries only)");
+    static_assert(!DEAL || (LC && !FULL), "dealt leaf tests: lean leaf-cull builds (shadow queries only)");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -715,8 +730,83 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             if (!((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f)))
                 if (!test(lrec(first + j))) break;
         }
+    } else if (DEAL && count <= (uint32_t)LC_MAXREFS) {
+        // DEAL (shadow queries): the divergent leaf's tests -- the set bits of every lane's mask --
+        // dealt out over the lanes of this branch, one test per lane and chunk, instead of each lane
+        // walking its own bits (the loop would run as often as the largest mask; measured lane
+        // efficiency 0.22).  A shadow leaf's answer is "some test accepts", whatever the order, so
+        // an owner is occluded when any of its workers' tests accepted (rank-space mask in LDS).
+        const uint32_t lane = tid & 63u;
+        const uint64_t act = __ballot(1), lbelow = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const uint32_t A = (uint32_t)__popcll(act), rank = (uint32_t)__popcll(act & lbelow);
+        const uint32_t cnt = (uint32_t)__builtin_popcount(lmask);
+        uint32_t pre = 0, total = 0; // exclusive prefix of the counts over the branch's lanes (5-bit counts)
+#pragma unroll
+        for (int b = 0; b < 5; b++) {
+            const uint64_t m = __ballot((cnt >> b) & 1u);
+            pre += (uint32_t)__popcll(m & lbelow) << b;
+            total += (uint32_t)__popcll(m) << b;
+        }
+        DealLds &dl = deal[tid >> 6];
+        for (uint32_t base = 0; base < total; base += A) { // wave-uniform
+            const int sp0 = (int)pre - (int)base;
+            const bool ov = cnt && sp0 < (int)A && sp0 + (int)cnt > 0; // my tests meet this chunk
+            const uint32_t sp = ov ? (uint32_t)max(sp0, 0) : 0u;
+            if (rank == 0) {
+                dl.smask = 0ull;
+                dl.rmask = 0ull;
+            }
+            wave_fence();
+            if (ov) {
+                dl.tab[sp] = (uint8_t)lane;
+                atomicOr(&dl.smask, 1ull << sp);
+            }
+            wave_fence();
+            // my test: chunk position = rank; its owner starts at the highest start position <= rank
+            const uint64_t sm = dl.smask;
+            const uint64_t upto = rank >= 63u ? ~0ull : ((2ull << rank) - 1ull);
+            const uint32_t spos = 63u - (uint32_t)__clzll(sm & upto);
+            const int owner = (int)dl.tab[spos];
+            const uint32_t pre_o = (uint32_t)__shfl((int)pre, owner, 64);
+            const uint32_t mask_o = (uint32_t)__shfl((int)lmask, owner, 64);
+            const uint32_t first_o = (uint32_t)__shfl((int)first, owner, 64);
+            const uint32_t excl_o = (uint32_t)__shfl((int)exclude, owner, 64);
+            const f3 oo = mk(__shfl(o.x, owner, 64), __shfl(o.y, owner, 64), __shfl(o.z, owner, 64));
+            const f3 dd = mk(__shfl(d.x, owner, 64), __shfl(d.y, owner, 64), __shfl(d.z, owner, 64));
+            const float tmax_o = __shfl(T.tmax, owner, 64);
+            bool acc = false;
+            if (base + rank < total) {
+                uint32_t mm = mask_o;
+                for (uint32_t k = base + rank - pre_o; k; k--) mm &= mm - 1u; // the owner's k-th reference
+                const TriRec r = lrec(first_o + (uint32_t)__builtin_ctz(mm));
+                if (pc) pc->tests++;
+                float ux, uy, tt;
+                acc = rec_id(r) != excl_o && tri_test_wave(oo, dd, r, tmax_o, ux, uy, tt);
+            }
+            if (acc) atomicOr(&dl.rmask, 1ull << rank);
+            wave_fence();
+            if (ov) {
+                const uint32_t r1 = min((uint32_t)(sp0 + (int)cnt), A);
+                const uint32_t w = r1 - sp;
+                const uint64_t range = (w >= 64u ? ~0ull : ((1ull << w) - 1ull)) << sp;
+                occluded = occluded | ((dl.rmask & range) != 0ull);
+            }
+            wave_fence();
+        }
     } else if (LC && count <= (uint32_t)LC_MAXREFS) { // the mask's references, pipelined one ahead
         uint32_t m = lmask;
+        if (pc) { // the divergent leaf loop's shape: iterations = the largest lane mask
+            const uint32_t pop = (uint32_t)__builtin_popcount(m);
+            const uint32_t lanes = (uint32_t)__popcll(__ballot(pop > 0));
+            uint32_t mx = 0;
+            while (__ballot(pop > mx)) mx++;
+            if (lanes && wave_leader()) {
+                pc->drounds++;
+                pc->diters += mx;
+                pc->dlanes += lanes;
+            }
+            pc->dtests += pop;
+        }
         TriRec nx;
         if (m) nx = lrec(first + (uint32_t)__builtin_ctz(m));
         while (m) {

@@ -200,8 +200,10 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
           bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0,
-          bool PROF = false, bool PC = false, bool RL = false, bool REV = false>
+          bool PROF = false, bool PC = false, bool RL = false, bool REV = false, bool DEAL = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
+    static_assert(!DEAL || SHADOW, "dealt leaf tests: shadow queries only");
+    __shared__ DealLds deal_lds[DEAL ? 4 : 1];
     static_assert(!REV || SHADOW, "far-first order: shadow queries only");
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
@@ -308,9 +310,10 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC, REV>(A.lc_debug, A.lc_min, 
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC, REV, DEAL>(A.lc_debug, A.lc_min, 
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
-                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr, RL ? rl : nullptr);
+                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr, RL ? rl : nullptr,
+                DEAL ? deal_lds : nullptr);
             if (r != busy_st) {
                 if (PC) pc.vb += SHADOW ? 4u : 16u;
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
@@ -1104,7 +1107,14 @@ static const WfVariant kWf[] = {
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 7}),
     // 31: 26 whose secondary closest trace does not cull leaves (build 18's): 371.0 ms
     CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4})};
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}),
+    // 32: 26 whose shadow trace deals a divergent leaf's tests out over the lanes of the round (the
+    //     leaf-cull loop runs 6.0 iterations per divergent round at lane efficiency 0.22, cr_get_perf):
+    //     bit-exact, but 368.9 / 369.2 vs 362.1 / 362.4 ms (shadow 54.4 vs 52.6 ms: 11 lane shuffles and
+    //     LDS traffic per dealt test, 14 VGPR spills)
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, false, false, false, true>,
+     8, 8, 0, 2, 1, 4})};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,

@@ -253,9 +253,10 @@ int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
 int cr_get_diag(cr_ctx *ctx, uint64_t *out, int n);
 /* Performed work of the last render with option "perf_counters" 1 (the default trace build 26
  * instantiated with counters; measurement only): per trace kind k (0 camera, 1 closest, 2 shadow,
- * 3 tail) the PERF_N = 8 values out[8k + i] -- queries, inner-node steps, leaves reached, leaf
+ * 3 tail) the PERF_N = 12 values out[12k + i] -- queries, inner-node steps, leaves reached, leaf
  * cull records evaluated, triangle tests executed (all per ray), bytes of vector-memory loads and
- * stores (per lane), bytes of scalar-memory loads (per wave), wave iterations (PERF_* in
+ * stores (per lane), bytes of scalar-memory loads (per wave), wave iterations, and the shape of
+ * the divergent leaf-cull loop: rounds, iterations, lanes with a test, tests (PERF_* in
  * csrc/kernels.hpp).  Where the counting build ("counters" 1) counts the reference algorithm's
  * work, these count what the culling kernels actually do.  Up to n values. */
 int cr_get_perf(cr_ctx *ctx, uint64_t *out, int n);
