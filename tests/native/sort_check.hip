@@ -50,7 +50,7 @@ static int run(uint32_t n, int bits, uint64_t seed, bool lib, std::vector<uint32
 }
 
 int main() {
-    const uint32_t sizes[] = {0, 1, 63, 64, 4095, 4096, 4097, 12289, 100000, 1048577, 3000001};
+    const uint32_t sizes[] = {0, 1, 63, 64, 4095, 4096, 4097, 12289, 16383, 16384, 16385, 100000, 1048577, 3000001};
     const int widths[] = {1, 7, 8, 12, 25, 30, 32};
     int cases = 0, bad = 0, lib_diff = 0;
     for (uint32_t n : sizes)

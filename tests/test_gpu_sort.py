@@ -1,6 +1,6 @@
 """GPU check of the wavefront queue sort (csrc/raysort.hip): the hand-written
 stable radix sort equals std::stable_sort and hipcub's DeviceRadixSort on
-random and clustered keys, at tile edges (4095 / 4096 / 4097 pairs) and key
+random and clustered keys, at tile edges (4095 / 4096 / 4097 pairs; 16383 / 16384 / 16385) and key
 widths 1..32.  (The image never depends on the order -- the render parity
 tests force sorting of every queue -- but the coherence the sort buys does.)"""
 import json
@@ -22,5 +22,5 @@ def test_queue_sort_is_stable_and_exact(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     res = json.loads(r.stdout.strip().splitlines()[-1])
     print(res, r.stderr[-2000:])
-    assert res["mismatch"] == 0 and res["differs_from_hipcub"] == 0 and res["cases"] == 154, res
+    assert res["mismatch"] == 0 and res["differs_from_hipcub"] == 0 and res["cases"] == 196, res
     assert r.returncode == 0
