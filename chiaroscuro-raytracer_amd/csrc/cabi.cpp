@@ -959,6 +959,18 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_sort_g1") && v >= 0 && v <= 3) c->wf_sort_g1 = (uint32_t)v;
     else if (!std::strcmp(key, "wf_cam_lean") && (v == 0 || v == 1)) c->wf_cam_lean = (int)v;
     else if (!std::strcmp(key, "wf_tail_waves") && v >= 4 && v <= 6) c->wf_tail_waves = (int)v;
+    else if (!std::strcmp(key, "wf_side_priority") && (v == 0 || v == 1)) {
+        // the second stream (closest trace g + 1 beside shadow trace g) at the device's highest
+        // stream priority (1) or the default (0): which persistent grid takes the CUs first
+        int lo = 0, hi = 0;
+        if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+            hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess)
+            return CR_E_HIP;
+        hipStream_t s = nullptr;
+        if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, v ? hi : lo) != hipSuccess) return CR_E_HIP;
+        hipStreamDestroy(c->wfs.side);
+        c->wfs.side = s;
+    }
     else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
     else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
     else if (!std::strcmp(key, "lc_min") && v >= 0 && v <= 33) c->lc_min = (uint32_t)v;

@@ -242,11 +242,34 @@ __device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_R
 }
 template <bool SC, int FORM = 0>
 __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
+    if (FORM == 3 && !(SC && wave_uniform(node))) {
+        // the packed record of a divergent leaf in two halves, one group each (12 instead of 24
+        // VGPRs at the peak): group 0 = float4 0..2, group 1 = 3..5, masks in the low bytes
+        const uint32_t all = count >= 32 ? 0xffffffffu : ((1u << count) - 1u);
+        if (!lc_unit(d.x, d.y, d.z) || count > (uint32_t)LC_MAXREFS_P) return all;
+        const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
+        const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+        const float4 *p = (const float4 *)((const char *)S.lcullp + node * (uint32_t)(16 * LC_RECP));
+        const float4 a0 = p[0], a1 = p[1], a2 = p[2];
+        const uint32_t m0 = lc_lowbyte(a0.w) | lc_lowbyte(a1.w) << 8, m1lo = lc_lowbyte(a2.w);
+        uint32_t keep = 0u;
+        if (m0 && !lc_group_skip_fixed(ov, dv, inv, tmax, LcFloat4{a0.x, a0.y, a0.z, a0.w},
+                                       LcFloat4{a1.x, a1.y, a1.z, a1.w}, LcFloat4{a2.x, a2.y, a2.z, a2.w}))
+            keep = m0;
+        asm volatile("" ::: "memory"); // the second half's loads after the first half's test
+        const float4 a3 = p[3], a4 = p[4], a5 = p[5];
+        const uint32_t m1 = m1lo | lc_lowbyte(a3.w) << 8;
+        keep |= lc_lowbyte(a4.w) | lc_lowbyte(a5.w) << 8;
+        if (m1 && !lc_group_skip_fixed(ov, dv, inv, tmax, LcFloat4{a3.x, a3.y, a3.z, a3.w},
+                                       LcFloat4{a4.x, a4.y, a4.z, a4.w}, LcFloat4{a5.x, a5.y, a5.z, a5.w}))
+            keep |= m1;
+        return keep & all;
+    }
     LcFloat4 rec[LC_REC];
-    constexpr int NR = FORM == 2 ? LC_RECP : LC_REC;
-    const float4 *recs = FORM == 2 ? S.lcullp : (FORM == 1 ? S.lcullf : S.lcull);
+    constexpr int NR = FORM >= 2 ? LC_RECP : LC_REC;
+    const float4 *recs = FORM >= 2 ? S.lcullp : (FORM == 1 ? S.lcullf : S.lcull);
     if (SC && wave_uniform(node)) {
-        if (FORM == 2) sload_lcullp(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
+        if (FORM >= 2) sload_lcullp(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
         else sload_lcull(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
     } else {
         const float4 *p = (const float4 *)((const char *)recs + node * (uint32_t)(16 * NR));
@@ -259,7 +282,7 @@ __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, 
     const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
     // v_rcp_f32: within 1 ulp of 1/d (the check allows 2, tests/native/leafcull_check.cpp)
     const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
-    if (FORM == 2) return leaf_cull_mask_packed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
+    if (FORM >= 2) return leaf_cull_mask_packed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
     if (FORM == 1) return leaf_cull_mask_fixed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
     return leaf_cull_mask(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, S.db, rec, count);
 }
@@ -506,9 +529,9 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         // LC 3: the fixed-pad records; leaves below lc_min: every reference, no check
         if (pc && count >= lc_min) {
             pc->masks++;
-            pc_load(pc, SC && wave_uniform(T.node), 16u * (LC == 4 ? LC_RECP : LC_REC));
+            pc_load(pc, SC && wave_uniform(T.node), 16u * (LC >= 4 ? LC_RECP : LC_REC));
         }
-        lmask = count >= lc_min ? leaf_mask<SC, LC == 4 ? 2 : (LC == 3 ? 1 : 0)>(S, T.node, count, o, d, T.tmax)
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 5 ? 3 : (LC == 4 ? 2 : (LC == 3 ? 1 : 0))>(S, T.node, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }

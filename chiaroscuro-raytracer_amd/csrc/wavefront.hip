@@ -1114,7 +1114,15 @@ static const WfVariant kWf[] = {
     //     LDS traffic per dealt test, 14 VGPR spills)
     CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, false, false, false, true>,
-     8, 8, 0, 2, 1, 4})};
+     8, 8, 0, 2, 1, 4}),
+    // 33: 29 (the exact short division from RN(1/d) in VGPRs) with a divergent leaf's cull record
+    //     loaded and tested one group at a time (the record's peak register use halved; the leaf loop's
+    //     one-ahead record pipeline is the other peak): 378.4 vs 362.4 ms, shadow 55.3 vs 52.5 ms
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 5>,
+     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 5>, 8, 8, 0, 2, 1, 4}),
+    // 34: 26 with the cull record loaded one group at a time (no FD): 375.7 ms, shadow 55.0 ms
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 5>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 5>, 8, 8, 0, 2, 1, 4})};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--nranks", default="1,2,4,8")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE", help="cr_set_option (experiments)")
+    ap.add_argument("--tile", type=int, default=32, help="tile edge of the split (bench.py: 32)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -44,9 +45,10 @@ def main():
     for r in range(args.rounds):
         for n in (int(x) for x in args.nranks.split(",")):
             for rank in range(n):
-                p = ca.render_params(i["xres"], i["yres"], spp, i["k"], i["seed"], rank=rank, nranks=n)
-                tiles = torch.zeros((ca.Device.tiles_for_rank(p, rank), 32, 32, 3), dtype=torch.float32,
-                                    device="cuda")
+                p = ca.render_params(i["xres"], i["yres"], spp, i["k"], i["seed"], rank=rank, nranks=n,
+                                     tile=args.tile)
+                tiles = torch.zeros((ca.Device.tiles_for_rank(p, rank), args.tile, args.tile, 3),
+                                    dtype=torch.float32, device="cuda")
                 dev.render_tiles_device(cam, p, tiles.data_ptr())
                 torch.cuda.synchronize()
                 c = dev.counters()
@@ -61,7 +63,8 @@ def main():
                           round(ms[slow], 2), "slowest_rank": slow, "rank0_ms": round(ms[0], 2),
                           "imbalance": round(ms[slow] / (sum(ms.values()) / n), 3),
                           "projected_mray_s": round(rays / ms[slow] / 1e3, 1), "ideal_ms": round(base / n, 2),
-                          "projected_speedup": round(base / ms[slow], 2)}), flush=True)
+                          "projected_speedup": round(base / ms[slow], 2),
+                          "rank_mrays": [round(ranks[rk][0][1] / 1e6, 2) for rk in sorted(ranks)]}), flush=True)
 
 
 if __name__ == "__main__":
