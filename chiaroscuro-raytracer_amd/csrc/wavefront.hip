@@ -1013,6 +1013,7 @@ struct WfVariant {
     int lc;     // the tail kernel's leaf cull form (trav_round's LC; 0: none)
     int rl;     // the secondary and shadow traces keep RN(1/d) in LDS (12 B per thread after the ring)
     int closest_waves; // the secondary closest trace's waves per SIMD when not waves_per_simd (0: the same)
+    int shadow_waves;  // the shadow trace's (0: the same)
 };
 #define CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, PL)                                                     \
     {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
@@ -1122,7 +1123,15 @@ static const WfVariant kWf[] = {
      wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 5>, 8, 8, 0, 2, 1, 4}),
     // 34: 26 with the cull record loaded one group at a time (no FD): 375.7 ms, shadow 55.0 ms
     CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 5>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 5>, 8, 8, 0, 2, 1, 4})};
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 5>, 8, 8, 0, 2, 1, 4}),
+    // 35: 26 whose shadow trace runs at 7 waves / SIMD (68 VGPRs, no spills) with the exact short
+    //     division (FD): 369.9 vs 363.7 ms (shadow 53.3 vs 52.5 ms); the division saves 2.5% of the
+    //     7-wave trace, the eighth wave is worth more
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 7, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 0, 7}),
+    // 36: 26 whose shadow trace runs at 7 waves / SIMD (no FD): 375.1 ms (shadow 54.6 ms)
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 7, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 0, 7})};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
@@ -1298,6 +1307,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     const uint32_t cblocks =
         (!A.full_counters && v.closest_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.closest_waves : blocks;
+    const uint32_t sblocks =
+        (!A.full_counters && v.shadow_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.shadow_waves : blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds =
@@ -1372,7 +1383,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         W.order = order_s;
         W.ended_only = overlap ? 1u : 0u;
         if ((err = trace_event(te, st, TK_SHADOW, true))) break;
-        hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, st, A, W, g);
+        hipLaunchKernelGGL(v.shadow, dim3(sblocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, TK_SHADOW, false))) break;
         hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
         W.ended_only = 0u;
@@ -1395,6 +1406,8 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     const uint32_t cblocks =
         (!A.full_counters && v.closest_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.closest_waves : blocks;
+    const uint32_t sblocks =
+        (!A.full_counters && v.shadow_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.shadow_waves : blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     for (int i = 0; i < nl; i++)
         if (L[i].W.gstride < blk * blocks || L[i].W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
@@ -1485,7 +1498,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         WfArgs Ws = r.W;
         Ws.order = order_s;
         if ((err = trace_event(te, ln.st, TK_SHADOW, true))) return true;
-        hipLaunchKernelGGL(v.shadow, dim3(blocks), dim3(blk), lds, ln.st, A, Ws, g);
+        hipLaunchKernelGGL(v.shadow, dim3(sblocks), dim3(blk), lds, ln.st, A, Ws, g);
         if ((err = trace_event(te, ln.st, TK_SHADOW, false))) return true;
         hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, g);
         if (next) {
