@@ -453,6 +453,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     };
     // LC 2: a leaf whose references are all excluded is passed like an empty leaf -- the lane
     // pops and descends to its next leaf in the same round, so the round's tests run on every lane
+    uint32_t passes = 0; // LC 6 / 7: empty leaves passed in this round
     for (;;) {
     culled = false;
     if (FAT) { // two levels per dependent load: a node's record carries its children's
@@ -531,11 +532,15 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             pc->masks++;
             pc_load(pc, SC && wave_uniform(T.node), 16u * (LC >= 4 ? LC_RECP : LC_REC));
         }
-        lmask = count >= lc_min ? leaf_mask<SC, LC == 5 ? 3 : (LC == 4 ? 2 : (LC == 3 ? 1 : 0))>(S, T.node, count, o, d, T.tmax)
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 5 ? 3 : (LC == 4 || LC >= 6 ? 2 : (LC == 3 ? 1 : 0))>(S, T.node, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }
-    if (LC == 2 && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp) { // (LC 2 only)
+    // LC 6 / 7 (packed records): at most 1 / 3 such passes per round, so the lanes with tests do not
+    // wait on the longest chain of empty leaves
+    if ((LC == 2 || LC >= 6) && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp &&
+        (LC == 2 || passes < (LC == 6 ? 1u : 3u))) {
+        passes++;
         pop_entry();
         continue;
     }

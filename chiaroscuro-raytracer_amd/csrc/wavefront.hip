@@ -1131,7 +1131,17 @@ static const WfVariant kWf[] = {
      wf_trace<true, false, 8, 7, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 0, 7}),
     // 36: 26 whose shadow trace runs at 7 waves / SIMD (no FD): 375.1 ms (shadow 54.6 ms)
     CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 7, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 0, 7})};
+     wf_trace<true, false, 8, 7, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 0, 7}),
+    // 37 / 38: 26 whose shadow-trace lanes pass up to 1 / 3 leaves with every reference excluded (or
+    //     none) and descend to the next in the same round (build 20 passed any number: 2x slower):
+    //     bit-exact; 364.0 / 380.7 vs 363.4 ms per pass (shadow 53.0 / 57.4 vs 52.8 ms)
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>, 8, 8, 0, 2, 1, 4}),
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 7>, 8, 8, 0, 2, 1, 4}),
+    // 39: 37 whose secondary closest trace passes up to 1 such leaf too: 363.5 ms (neutral)
+    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>, 8, 8, 0, 2, 1, 4})};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,

@@ -6,6 +6,7 @@ glibc's sinf / cosf algorithm (equal to the host libm on every |x| < 120), so
 pixels, ray-query results and the query counters must be identical -- also
 against the oracle calling libm itself (test_parity_vs_libm_trig_oracle).
 """
+import os
 import numpy as np
 import pytest
 
@@ -18,6 +19,8 @@ ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit",
 # compiles with make ALL_VARIANTS=1): the plain reference build 0, 15 (the packet camera
 # trace's fallback), round 2's default 18 and the default 26 (leaf cull records)
 TRACE_BUILDS = [0, 15, 18, 26]
+# builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="37 38"
+TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 
 
 @pytest.fixture(scope="module")
