@@ -136,9 +136,12 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // the leaf cull (26) pays on large scenes only (round 3, 1080p): sponza stand-in (261k triangles)
     // 391.5 -> 366 ms per pass, nanobox stand-in (20k) 167.6 -> 171.0, cornell_box (36) 147.9 -> 149.3
     // -- on small trees a leaf's references lie close to its cell and the record costs more than
-    // the tests it removes -- so scenes below LEAF_CULL_MIN_TRIS triangles default to 18
+    // the tests it removes -- so scenes below LEAF_CULL_MIN_TRIS triangles default to 18;
+    // 40 / 42 = 26 / 18 whose camera packet divides by the rays' RN(1/d) (exact short division,
+    // round 3): camera trace 41.1 -> 37.1 ms on the sponza stand-in, 24.1 -> 22.1 on nanobox,
+    // 3.54 -> 3.55 on cornell_box (short packets: the reciprocals cost what they save)
     A.variant = c->variant >= 0 ? c->variant
-                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 26 : 18)
+                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 40 : 42)
                                  : 0;
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)

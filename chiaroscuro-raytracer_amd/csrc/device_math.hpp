@@ -62,6 +62,15 @@ __device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
     if (fabsf(q0) >= 0x1p-60f && fabsf(q0) <= 0x1p60f) return __builtin_fmaf(__builtin_fmaf(-q0, b, a), y, q0);
     return a / b;
 }
+// div_by_rcp for wave-wide use (the packet camera trace): the range test is one wave-uniform
+// branch, the full division runs for the whole wave only when some lane is out of range.
+__device__ __forceinline__ float div_by_rcp_wave(float a, float b, float y) {
+    const float q0 = a * y;
+    float q = __builtin_fmaf(__builtin_fmaf(-q0, b, a), y, q0);
+    const bool in = fabsf(q0) >= 0x1p-60f && fabsf(q0) <= 0x1p60f;
+    if (__ballot(!in)) q = in ? q : a / b;
+    return q;
+}
 // RN(1/a): hardware reciprocal (1 ulp) + one Newton step with fma.  Checked
 // exhaustively over every float with 2^-100 <= |a| <= 2^100 on gfx950
 // (tests/test_gpu_numerics.py).

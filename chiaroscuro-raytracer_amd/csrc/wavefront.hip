@@ -751,7 +751,9 @@ enum : uint32_t { PACKET_DEPTH = 256 }; // >= the deepest tree cr_upload_scene a
 // end; a ray going to the far child only is parked with tmax = its tmin.  Only active
 // rays' intervals change, so an inactive ray's tmax still holds its value for the next
 // entry it owns.
-template <int R, int S, bool PC = false>
+// FD: the split distance by the exact short division from the ray's RN(1/d) per axis, kept in
+// VGPRs (div_by_rcp: Markstein's correction, the full division outside its checked range).
+template <int R, int S, bool PC = false, bool FD = false>
 __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint32_t pring_lds[]; // [R][blockDim][S] per-ray tmax bits at push
     __shared__ uint32_t pnode[4][PACKET_DEPTH];
@@ -767,6 +769,11 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
     uint4 *hits = W.hit[1];
     const f3 eye = mk(A.cam[0], A.cam[1], A.cam[2]); // every camera ray's origin (wf_camera)
     const float4 *cnode = A.cull_node, *cref = A.cull;
+    // FD: the eye's offsets to the root box (ray_box_inv's first operands), wave-uniform -- kept in
+    // SGPRs so the compiler does not hoist them into VGPRs it then spills
+    auto rfl = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    const float box_lo[3] = {rfl(Sc.bmin.x - eye.x), rfl(Sc.bmin.y - eye.y), rfl(Sc.bmin.z - eye.z)};
+    const float box_hi[3] = {rfl(Sc.bmax.x - eye.x), rfl(Sc.bmax.y - eye.y), rfl(Sc.bmax.z - eye.z)};
     const uint32_t INACTIVE = 0xffffffffu;
     Ctr c = {};
     Pc pc = {};
@@ -788,13 +795,14 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
         }
         uint32_t idx[S];
         bool live[S], active[S], found[S];
-        f3 d[S];
+        f3 d[S], y[S];
         float tmin[S], tmax[S], csx[S], csy[S];
 #pragma unroll
         for (int s = 0; s < S; s++) {
             idx[s] = base + 64u * s + lane;
             live[s] = idx[s] < hi;
             d[s] = mk(0.f, 0.f, 1.f);
+            y[s] = mk(0.f, 0.f, 0.f);
             tmin[s] = tmax[s] = csx[s] = csy[s] = 0.f;
             found[s] = false;
             if (live[s]) {
@@ -811,7 +819,24 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                     csy[s] = q.y;
                     issued++;
                     Trav T;
-                    if (trav_begin(Sc, eye, d[s], false, 0.f, T)) {
+                    bool in;
+                    if (FD) { // trav_begin's root-box clip and T.r with the uniform offsets above
+                        // (rcp_rn_wave == 1.f / d bit for bit; the same products, min and max)
+                        const f3 inv = mk(rcp_rn_wave(d[s].x), rcp_rn_wave(d[s].y), rcp_rn_wave(d[s].z));
+                        const float txmin = box_lo[0] * inv.x, txmax = box_hi[0] * inv.x;
+                        const float tymin = box_lo[1] * inv.y, tymax = box_hi[1] * inv.y;
+                        const float tzmin = box_lo[2] * inv.z, tzmax = box_hi[2] * inv.z;
+                        T.tmin = std_max(std_max(std_min(txmin, txmax), std_min(tymin, tymax)), std_min(tzmin, tzmax));
+                        T.tmax = std_min(std_min(std_max(txmin, txmax), std_max(tymin, tymax)), std_max(tzmin, tzmax));
+                        in = !(T.tmax < 0 || T.tmax < T.tmin);
+                        const float nan = __builtin_nanf("");
+                        y[s] = mk(fabsf(d[s].x) >= 0x1p-40f && fabsf(d[s].x) <= 0x1p40f ? inv.x : nan,
+                                  fabsf(d[s].y) >= 0x1p-40f && fabsf(d[s].y) <= 0x1p40f ? inv.y : nan,
+                                  fabsf(d[s].z) >= 0x1p-40f && fabsf(d[s].z) <= 0x1p40f ? inv.z : nan);
+                    } else {
+                        in = trav_begin(Sc, eye, d[s], false, 0.f, T);
+                    }
+                    if (in) {
                         tmin[s] = T.tmin;
                         tmax[s] = T.tmax;
                     } else {
@@ -959,7 +984,8 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
 #pragma unroll
                 for (int s = 0; s < S; s++) {
                     if (PC) pc.steps += active[s] ? 1u : 0u;
-                    tsp[s] = split_distance(split, oa, comp(d[s], a));
+                    tsp[s] = FD ? div_by_rcp_wave(split - oa, comp(d[s], a), comp(y[s], a))
+                                : split_distance(split, oa, comp(d[s], a));
                     crosses[s] = !(tsp[s] >= tmax[s]) & !(tsp[s] < 0.f); // !near_only
                     after[s] = !(tsp[s] <= tmin[s]);                     // far_only = crosses & !after
                     to_near[s] = active[s] & (!crosses[s] | after[s]);
@@ -1027,7 +1053,8 @@ struct WfVariant {
 #define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
 // The trace builds, by index (cr_set_option "variant").  The default compile holds the
 // plain reference build 0, build 15 (the packet camera trace's fallback for an eye on a
-// split plane), build 18 (round 2's default) and build 26 (the default); every measured
+// split plane), builds 18 and 26 (round 2's and round 3's defaults) and the defaults 40 / 42 (26 /
+// 18 with the exact short division in the camera packet); every measured
 // and superseded build -- each is described below and in DESIGN.md §3 / §6 -- compiles
 // with `make ALL_VARIANTS=1` and is an empty entry (rejected at render) otherwise.
 #define CR_WF_NONE {nullptr, nullptr, nullptr, 8, 8, 0, 0, 0, 0}
@@ -1141,7 +1168,17 @@ static const WfVariant kWf[] = {
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 7>, 8, 8, 0, 2, 1, 4}),
     // 39: 37 whose secondary closest trace passes up to 1 such leaf too: 363.5 ms (neutral)
     CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>, 8, 8, 0, 2, 1, 4})};
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>, 8, 8, 0, 2, 1, 4}),
+    // 40: 26 whose camera packet divides by the rays' RN(1/d) kept in VGPRs (FD; the packet's
+    //     spills are outside its loops): camera trace 41.0 -> 37.7 ms, 363.1 -> 360.0 ms per pass
+    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
+    // 41: 40 with packets of 64 rays (one per lane: no spills): camera 49.6 ms
+    CR_WF_OPT({wf_trace_packet<8, 1, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}),
+    // 42: 18 with 40's camera packet (the default below LEAF_CULL_MIN_TRIS triangles)
+    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0}};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
@@ -1149,7 +1186,17 @@ static const WfVariant kWfPerf26 = {
 static const WfVariant kWfPerf18 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>,
     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>, 8, 8, 0, 2, 1, 0};
-bool wf_perf_available(int variant) { return variant == 18 || variant == 26; }
+// ... and builds 40 / 42 (26 / 18 with the FD camera packet: the same work, the division shortened)
+static const WfVariant kWfPerf40 = {
+    wf_trace_packet<8, 2, true, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
+    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>, 8, 8, 0, 2, 1, 4};
+static const WfVariant kWfPerf42 = {
+    wf_trace_packet<8, 2, true, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>,
+    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>, 8, 8, 0, 2, 1, 0};
+bool wf_perf_available(int variant) { return variant == 18 || variant == 26 || variant == 40 || variant == 42; }
+static const WfVariant &perf_variant(int variant) {
+    return variant == 18 ? kWfPerf18 : variant == 40 ? kWfPerf40 : variant == 42 ? kWfPerf42 : kWfPerf26;
+}
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
                                    0, 0, 0};
@@ -1311,7 +1358,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
                            TraceEvents *te) {
     WfArgs W = W0;
     const WfVariant &v = A.full_counters ? kWfCount
-                         : A.perf_counters ? (A.variant == 18 ? kWfPerf18 : kWfPerf26)
+                         : A.perf_counters ? perf_variant(A.variant)
                                            : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
@@ -1410,7 +1457,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
 
 int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hipStream_t st, TraceEvents *te) {
     const WfVariant &v = A.full_counters ? kWfCount
-                         : A.perf_counters ? (A.variant == 18 ? kWfPerf18 : kWfPerf26)
+                         : A.perf_counters ? perf_variant(A.variant)
                                            : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);

@@ -51,7 +51,7 @@ def main(src, dst, spp=128):
     kinds = {}
     for k, v in out.items():
         m = re.search(r"wf_trace<([^>]*)>", k)
-        if re.search(r"wf_trace_packet<[^>]*true>", k) or re.search(r"wf_trace<[^>]*, true>", k):
+        if re.search(r"wf_trace_packet<\d+, \d+, true", k) or re.search(r"wf_trace<[^>]*, true>", k):
             continue  # the performed-work counting instances (bench.py's perf pass)
         if "wf_trace_packet" in k:  # the packet build's camera-ray trace (lean)
             kind = "camera"

@@ -32,7 +32,8 @@ def is_counting(name: str) -> bool:
     # (and the performed-work counting instances of bench.py's perf pass: last template argument
     # PC; profile runs pass --no-perf-pass, so these are not expected)
     return (re.search(r"(wf_trace|render_dynamic)<\w+, true,", name) is not None or "wf_tail<true" in name or
-            re.search(r"(wf_trace|wf_trace_packet|wf_tail)<[^()]*, true>\(", name) is not None)
+            re.search(r"(wf_trace|wf_tail)<[^()]*, true>\(", name) is not None or
+            re.search(r"wf_trace_packet<\d+, \d+, true", name) is not None)  # packet: PC is the third argument
 
 
 def main():
