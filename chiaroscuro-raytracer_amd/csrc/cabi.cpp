@@ -139,9 +139,11 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // the tests it removes -- so scenes below LEAF_CULL_MIN_TRIS triangles default to 18;
     // 40 / 42 = 26 / 18 whose camera packet divides by the rays' RN(1/d) (exact short division,
     // round 3): camera trace 41.1 -> 37.1 ms on the sponza stand-in, 24.1 -> 22.1 on nanobox,
-    // 3.54 -> 3.55 on cornell_box (short packets: the reciprocals cost what they save)
+    // 3.54 -> 3.55 on cornell_box (short packets: the reciprocals cost what they save);
+    // 43 / 44 = 40 / 42 with the short division in the shadow trace too: 358.2 -> 356.4 ms, nanobox
+    // 163.7 -> 162.4 ms
     A.variant = c->variant >= 0 ? c->variant
-                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 40 : 42)
+                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 43 : 44)
                                  : 0;
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
@@ -177,6 +179,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         const bool chunked = chunk < p->spp;
         // wavefront: a second stack-overflow area for the closest trace that runs beside a
         // shadow trace, per lane
+        if (cr::persistent_gstack_bytes(c->stack_depth, A.gstride) >= (1ull << 32)) // (gstack_at's 32-bit offsets)
+            return fail(c, CR_E_INVALID, "stack-overflow area above 4 GiB");
         if (int r = grow(c, &c->d_gstack, c->gstack_bytes,
                          (wf ? 2 * c->wf_lanes : 1) * cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
             return r;

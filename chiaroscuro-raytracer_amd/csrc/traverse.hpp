@@ -108,6 +108,13 @@ __device__ __forceinline__ void pc_flush(unsigned long long *ctrs, const Pc &pc)
     }
 }
 
+// A lane's stack-overflow entry at `depth` ([depth][gstride] rows): a 32-bit byte offset from the
+// wave-uniform base, so the access uses scalar-base addressing and no 64-bit per-lane pointer is kept
+// live (the compiler spilled one); cr_render checks that an area stays below 4 GiB.
+__device__ __forceinline__ uint2 &gstack_at(uint2 *gstk, uint32_t depth, uint32_t gstride, uint32_t gid) {
+    return *(uint2 *)((char *)gstk + (depth * gstride + gid) * 8u);
+}
+
 // Root-box clip (kdtree.cpp:196-208, 276-283); false: the query ends without a hit.
 __device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool shadow, float limit, Trav &T) {
     const f3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
@@ -399,7 +406,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             if (push) {
                 const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
                 if (pc && T.nl == R) pc->vb += 8;
-                if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
+                if (T.nl == R) gstack_at(gstk, T.sp - R, gstride, gid) = ring[slot]; // spill the oldest
                 ring[slot] = REV ? make_uint2(child + 1u - below, __float_as_uint(T.tmin))
                                  : make_uint2(child + below, __float_as_uint(T.tmax));
             }
@@ -414,7 +421,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         } else {
             const uint2 e = make_uint2(child + below, __float_as_uint(T.tmax));
             const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
-            if (T.nl == R) gstk[(size_t)(T.sp - R) * gstride + gid] = ring[slot]; // spill the oldest
+            if (T.nl == R) gstack_at(gstk, T.sp - R, gstride, gid) = ring[slot]; // spill the oldest
             else T.nl++;
             ring[slot] = e;
             T.sp++;
@@ -439,7 +446,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             e = ring[(T.sp & (R - 1)) * bdim + tid];
             T.nl--;
         } else {
-            e = gstk[(size_t)T.sp * gstride + gid];
+            e = gstack_at(gstk, T.sp, gstride, gid);
             if (pc) pc->vb += 8;
         }
         T.node = e.x;

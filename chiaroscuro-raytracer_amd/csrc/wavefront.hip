@@ -225,7 +225,8 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     Ctr c = {};
     Diag dg = {};
     dg.on = FULL && ((A.diag_kinds >> (SHADOW ? TK_SHADOW : (CAM ? TK_CAMERA : TK_CLOSEST))) & 1u);
-    uint32_t state = ST_NEED_WORK, idx = 0, exclude = 0, issued = 0;
+    uint32_t state = ST_NEED_WORK, idx = 0, exclude = 0;
+    uint32_t issued = 0; // the wave's queries (wave-uniform: an SGPR, not a VGPR per lane)
     f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f);
     float csx = 0.f, csy = 0.f;
     Trav T = {0u, 0u, 0u, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
@@ -253,6 +254,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                     break;
                 }
                 const uint32_t leader = (uint32_t)__ffsll((long long)m) - 1u;
+                bool iss = false;
                 const uint32_t lo = xp ? (uint32_t)((uint64_t)n * part / WF_XCDS) : 0u;
                 const uint32_t hi = xp ? (uint32_t)((uint64_t)n * (part + 1) / WF_XCDS) : n;
                 uint32_t base = 0;
@@ -270,8 +272,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         if (W.order) idx = W.order[idx]; // sorted queue: results still go to slot idx
                         if (PC) pc.vb += (W.order ? 4u : 0u) + 32u + (SHADOW ? 4u : 0u) + (CULL ? 8u : 0u);
                         const float4 r0 = rays[2 * (size_t)idx], r1 = rays[2 * (size_t)idx + 1];
-                        // overlapped tail: a path that continues traces this ray in wf_tail
-                        if (SHADOW && W.ended_only && (W.sexcl[idx] & SEXCL_CONT)) continue;
+                        // overlapped tail: a path that continues traces this ray in wf_tail (the lane
+                        // stays idle and takes another; no `continue`: every lane reaches the count below)
+                        if (!(SHADOW && W.ended_only && (W.sexcl[idx] & SEXCL_CONT))) {
                         o = ld3(r0);
                         d = ld3(r1);
                         if (SHADOW) exclude = W.sexcl[idx] & ~SEXCL_CONT;
@@ -282,7 +285,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         }
                         if (!SHADOW && __float_as_uint(r0.w) == NO_PATH) {
                             W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
-                        } else if (issued++, trav_begin(S, o, d, SHADOW, r1.w, T)) {
+                        } else if (iss = true, trav_begin(S, o, d, SHADOW, r1.w, T)) {
                             state = busy_st;
                             if (RL) {
                                 rl[threadIdx.x] = T.r.x;
@@ -297,8 +300,10 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                             if (PC) pc.vb += 16;
                             W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u);
                         }
+                        }
                     }
                 }
+                issued = __builtin_amdgcn_readfirstlane(issued + (uint32_t)__popcll(__ballot(iss)));
             }
             if (PROF) {
                 prefill += prof_now() - pr0;
@@ -332,9 +337,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
     }
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
     else c.closest = issued;
-    flush_counters(A.counters, c, 0u);
+    flush_counters(A.counters, c, SHADOW ? 2u : 1u); // (the count is the wave's already)
     if (PC) {
-        pc.q = issued;
+        pc.q = lane == 0 ? issued : 0u;
         pc_flush(A.counters + CTR_PERF + PERF_N * (SHADOW ? TK_SHADOW : (CAM ? TK_CAMERA : TK_CLOSEST)), pc);
     }
     if (FULL) { // per-instantiation split of the §8d work counters (bench roofline)
@@ -864,7 +869,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             if (nl == (uint32_t)R) { // spill the oldest
                 if (PC) pc.vb += 8;
                 uint2 e = make_uint2(ring[slot * S], S == 2 ? ring[slot * S + (S - 1)] : 0u);
-                gstk[(size_t)(sp - R) * gstride + gid] = e;
+                gstack_at(gstk, sp - R, gstride, gid) = e;
             } else {
                 nl++;
             }
@@ -885,7 +890,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                     nl--;
                 } else {
                     if (PC) pc.vb += 8;
-                    const uint2 ge = gstk[(size_t)sp * gstride + gid];
+                    const uint2 ge = gstack_at(gstk, sp, gstride, gid);
                     e[0] = ge.x;
                     if (S == 2) e[S - 1] = ge.y;
                 }
@@ -1053,8 +1058,9 @@ struct WfVariant {
 #define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
 // The trace builds, by index (cr_set_option "variant").  The default compile holds the
 // plain reference build 0, build 15 (the packet camera trace's fallback for an eye on a
-// split plane), builds 18 and 26 (round 2's and round 3's defaults) and the defaults 40 / 42 (26 /
-// 18 with the exact short division in the camera packet); every measured
+// split plane), builds 18 and 26 (round 2's and round 3's defaults), 40 / 42 (26 / 18 with the exact
+// short division in the camera packet) and the defaults 43 / 44 (40 / 42 with it in the shadow trace
+// too); every measured
 // and superseded build -- each is described below and in DESIGN.md §3 / §6 -- compiles
 // with `make ALL_VARIANTS=1` and is an empty entry (rejected at render) otherwise.
 #define CR_WF_NONE {nullptr, nullptr, nullptr, 8, 8, 0, 0, 0, 0}
@@ -1178,7 +1184,14 @@ static const WfVariant kWf[] = {
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}),
     // 42: 18 with 40's camera packet (the default below LEAF_CULL_MIN_TRIS triangles)
     {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0}};
+     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0},
+    // 43 / 44 (the defaults): 40 / 42 whose shadow trace divides by the ray's RN(1/d) in VGPRs too (FD;
+    //     no spills at 8 waves once the stack-overflow pointer and the query count stopped occupying
+    //     VGPRs): 357.5 / 355.3 vs 358.4 / 358.1 ms per pass, nanobox 162.4 vs 163.7 ms (shadow 30.7 -> 29.9)
+    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
+    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
+     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0}};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
@@ -1193,9 +1206,15 @@ static const WfVariant kWfPerf40 = {
 static const WfVariant kWfPerf42 = {
     wf_trace_packet<8, 2, true, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>,
     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>, 8, 8, 0, 2, 1, 0};
-bool wf_perf_available(int variant) { return variant == 18 || variant == 26 || variant == 40 || variant == 42; }
+// (43 / 44 count through 40 / 42's instances: their shadow trace's short division does the same work)
+bool wf_perf_available(int variant) {
+    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44;
+}
 static const WfVariant &perf_variant(int variant) {
-    return variant == 18 ? kWfPerf18 : variant == 40 ? kWfPerf40 : variant == 42 ? kWfPerf42 : kWfPerf26;
+    return variant == 18 ? kWfPerf18
+           : (variant == 40 || variant == 43) ? kWfPerf40
+           : (variant == 42 || variant == 44) ? kWfPerf42
+                                              : kWfPerf26;
 }
 static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
                                    wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,

@@ -251,8 +251,8 @@ int cr_set_option(cr_ctx *ctx, const char *key, int64_t value);
  * shapes (what staging a wave's leaves in LDS would load) and a per-lane census of
  * repeated any-segment triangle misses.  Up to n of the DIAG_* values (csrc/kernels.hpp). */
 int cr_get_diag(cr_ctx *ctx, uint64_t *out, int n);
-/* Performed work of the last render with option "perf_counters" 1 (trace builds 18 / 26 / 40 / 42
- * -- the defaults are 40 and 42 -- instantiated with counters; measurement only): per trace kind k (0 camera, 1 closest, 2 shadow,
+/* Performed work of the last render with option "perf_counters" 1 (trace builds 18 / 26 / 40 / 42 /
+ * 43 / 44 -- the defaults are 43 and 44 -- instantiated with counters; measurement only): per trace kind k (0 camera, 1 closest, 2 shadow,
  * 3 tail) the PERF_N = 12 values out[12k + i] -- queries, inner-node steps, leaves reached, leaf
  * cull records evaluated, triangle tests executed (all per ray), bytes of vector-memory loads and
  * stores (per lane), bytes of scalar-memory loads (per wave), wave iterations, and the shape of

@@ -17,9 +17,9 @@ pytestmark = pytest.mark.gpu
 ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths")
 # the wavefront trace builds of the default compile (wavefront.hip kWf; every measured build
 # compiles with make ALL_VARIANTS=1): the plain reference build 0, 15 (the packet camera
-# trace's fallback), round 2's default 18, 26 (leaf cull records) and the defaults 40 / 42 (26 / 18
-# with the exact short division in the camera packet)
-TRACE_BUILDS = [0, 15, 18, 26, 40, 42]
+# trace's fallback), round 2's default 18, 26 (leaf cull records), 40 / 42 (26 / 18 with the exact
+# short division in the camera packet) and the defaults 43 / 44 (40 / 42 with it in the shadow trace)
+TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
 # builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="37 38"
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 
@@ -652,7 +652,7 @@ def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
     assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2
 
 
-@pytest.mark.parametrize("variant", [18, 26, 40, 42])
+@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44])
 @pytest.mark.parametrize("tail_min", [0, 3000])
 def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
     """The performed-work builds (option perf_counters: builds 18 / 26 / 40 / 42 with counters, cr_get_perf)
@@ -690,7 +690,7 @@ def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
             assert pk["leaves"] <= rk["leaf"] and pk["steps"] <= rk["inner"], (kind, pk, rk)
             if kind != "camera" and tail_min == 0:
                 assert (pk["steps"], pk["leaves"]) == (rk["inner"], rk["leaf"]), (kind, pk, rk)
-                if variant in (18, 42):
+                if variant in (18, 42, 44):
                     assert pk["masks"] == 0 and pk["tests"] == rk["tritest"], (kind, pk, rk)
                 else:
                     assert pk["masks"] <= pk["leaves"]
@@ -702,7 +702,7 @@ def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
 
 
 def test_perf_counters_default_build_only(ca, cornell):
-    """perf_counters instruments builds 18, 26, 40 and 42 only: another build is refused loudly."""
+    """perf_counters instruments builds 18, 26 and 40-44 (not 41) only: another build is refused loudly."""
     cornell.dev.set_option("kernel", 2)
     cornell.dev.set_option("counters", 0)
     cornell.dev.set_option("perf_counters", 1)
@@ -718,7 +718,7 @@ def test_perf_counters_default_build_only(ca, cornell):
 
 
 def test_default_build_by_scene_size(ca, sponza, nanobox):
-    """The default trace build culls leaves (40) on the 261k-triangle sponza stand-in and not (42)
+    """The default trace build culls leaves (43) on the 261k-triangle sponza stand-in and not (44)
     on the 20k-triangle nanobox stand-in (cabi.cpp LEAF_CULL_MIN_TRIS): seen through the
     performed-work counts of the default build."""
     masks = {}
