@@ -176,7 +176,7 @@ int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t s
 // (one 64-B line each): closest [WF_XBASE + (g*8 + x)*WF_XSTRIDE], shadow after WF_G*8 of those
 enum : uint32_t { WF_G = 66, WF_XCDS = 8, WF_XSTRIDE = 16, WF_XBASE = 4 * WF_G,
                   WF_CNT = WF_XBASE + 2 * WF_G * WF_XCDS * WF_XSTRIDE };
-enum { WF_STATE = 5 };            // path-state float4 slots per path
+enum { WF_STATE = 6 };            // path-state float4 slots per path (wavefront.hip PS)
 struct WfArgs {
     uint32_t P;       // path slots of this chunk
     uint32_t w0;      // first work item of the chunk
@@ -284,7 +284,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hi
                            TraceEvents *te = nullptr);
 // raysort.hip: stable radix sort of (key, value) pairs; lib: hipcub's instead
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
-               hipStream_t st, bool lib = false);
+               hipStream_t st, bool lib = false, bool iota = false);
 size_t wf_sort_tmp_bytes(uint32_t n, int key_bits, bool lib = false);
 // Persistent grid geometry chosen by launch_render (block threads, blocks).
 void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);

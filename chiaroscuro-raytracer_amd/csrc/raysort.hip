@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_downsweep(const uint32_t *keys_
         const uint32_t i = tile_item(wave, r, lane);
         const bool ok = i < count;
         key[r] = ok ? keys_in[base + i] : 0u;
-        val[r] = ok ? vals_in[base + i] : 0u;
+        val[r] = ok ? (vals_in ? vals_in[base + i] : base + i) : 0u; // (no vals_in: the identity)
         const uint32_t d = (key[r] >> shift) & (RS_BINS - 1);
         const uint64_t m_ok = __ballot(ok);
         uint64_t peers = m_ok;
@@ -222,8 +222,11 @@ static size_t rs_tmp_bytes(uint32_t n) {
 // keys/vals are double buffers of n entries; returns the index (0/1) of the buffer
 // holding the sorted permutation, or -1 on error.  tmp == nullptr asks for the
 // temp size in tmp_bytes.  lib: hipcub's DeviceRadixSort instead (comparison).
+// iota: vals[0] is not read -- the first digit pass takes the identity 0..n-1 (the
+// queue's own order), so the producer need not write it (hand-written sort only).
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
-               hipStream_t st, bool lib) {
+               hipStream_t st, bool lib, bool iota) {
+    if (iota && (lib || end_bit <= 0)) return -1;
     if (lib) {
 #ifdef CR_SORT_LIB
         hipcub::DoubleBuffer<uint32_t> k(keys[0], keys[1]), v(vals[0], vals[1]);
@@ -250,8 +253,9 @@ int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, vo
         hipLaunchKernelGGL(rs_scan_sums, dim3(nseg), dim3(RS_THREADS), 0, st, H, m, sums);
         hipLaunchKernelGGL(rs_scan_top, dim3(1), dim3(RS_THREADS), 0, st, sums, nseg);
         hipLaunchKernelGGL(rs_scan_apply, dim3(nseg), dim3(RS_THREADS), 0, st, H, m, sums);
-        hipLaunchKernelGGL(rs_downsweep, dim3(ntiles), dim3(RS_THREADS), 0, st, keys[sel], vals[sel], keys[sel ^ 1],
-                           vals[sel ^ 1], n, (uint32_t)shift, ntiles, H);
+        hipLaunchKernelGGL(rs_downsweep, dim3(ntiles), dim3(RS_THREADS), 0, st, keys[sel],
+                           (iota && shift == 0) ? (const uint32_t *)nullptr : vals[sel], keys[sel ^ 1], vals[sel ^ 1], n,
+                           (uint32_t)shift, ntiles, H);
     }
     if (hipGetLastError() != hipSuccess) return -1;
     return sel;

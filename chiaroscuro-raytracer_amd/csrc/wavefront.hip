@@ -130,14 +130,20 @@ __device__ __forceinline__ void finish_path(const RenderArgs &A, const WfArgs &W
     out[2] = acc.z;
 }
 
-// Path state slots [slot][P]: 0 {direct, k}  1 {fcol, rng.key}  2 {normal, rng.ctr}
-//                             3 {contrib, shadow slot}  4 {next origin, -}
+// Path state slots [slot][P]: 0 {direct, -}  1 {fcol, -}  2 {normal, -}  (wf_tail's bounce only)
+//                             3 {contrib, shadow slot / resolve mark}  4 {next origin, -}
+//                             5 {k, rng.key, rng.ctr, -}: the control words, one 16-B slot (the
+//                               per-generation kernels write only this one, not slots 0-2)
 __device__ __forceinline__ float4 &PS(const WfArgs &W, int slot, uint32_t p) { return W.ps[(size_t)slot * W.P + p]; }
+enum { PS_CTL = 5 };
+__device__ __forceinline__ void ctl_store(const WfArgs &W, uint32_t p, uint32_t k, const Rng &rng) {
+    PS(W, PS_CTL, p) = make_float4(__uint_as_float(k), __uint_as_float(rng.key), __uint_as_float(rng.ctr), 0.f);
+}
 
-// Path state slots [slot][P]: 0 {direct, k}  1 {fcol, rng.key}  2 {normal, rng.ctr} ... (below).
-// When generation 1 runs as wavefront launches (the chunk is not handed to wf_tail at once), wf_camera
-// writes only slot 3 (the resolve mark): wf_shade derives generation 1's RNG state -- the camera
-// sample's stream after its two jitter draws -- from the path's (pixel, sample) instead of reading it.
+// Path state (PS above).  When generation 1 runs as wavefront launches (the chunk is not handed to
+// wf_tail at once), wf_camera writes only slot 3 (the resolve mark): wf_shade derives generation 1's
+// RNG state -- the camera sample's stream after its two jitter draws -- from the path's (pixel, sample)
+// instead of reading it.
 __device__ __forceinline__ bool camera_state_lean(const WfArgs &W) { return W.cam_lean && W.P >= W.tail_min; }
 __device__ __forceinline__ Rng camera_rng(const RenderArgs &A, const WfArgs &W, uint32_t p) {
     const uint32_t w = W.w0 + p, item = w / A.s_count, s = A.s0 + (w - item * A.s_count);
@@ -171,11 +177,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
             float2 sxy;
             const f3 d = camera_dir(A, px, py, rng, &sxy);
             if (A.cull) W.cxy[p] = sxy;
-            if (!camera_state_lean(W)) { // (wf_tail from generation 1 reads the state; wf_shade derives it)
-                PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), 1u);
-                PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key);
-                PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
-            }
+            if (!camera_state_lean(W)) ctl_store(W, p, 1u, rng); // (wf_tail from generation 1 reads it)
             PS(W, 3, p) = make_float4(0.f, 0.f, 0.f, 0.f); // no resolve mark (wf_resolve)
             W.ray[1][2 * (size_t)p] = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(p));
             W.ray[1][2 * (size_t)p + 1] = pk(d, 0u);
@@ -372,10 +374,11 @@ struct ShadowRay {
 __device__ __forceinline__ bool shade_path(const RenderArgs &A, const WfArgs &W, uint32_t p, f3 ro, uint4 h,
                                            bool &textured, ShadowRay &sh) {
     const DevScene &S = A.S;
-    const uint32_t k = __float_as_uint(PS(W, 0, p).w);
+    const float4 ctl = PS(W, PS_CTL, p);
+    const uint32_t k = __float_as_uint(ctl.x);
     const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
     textured = hs.textured;
-    Rng rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
+    Rng rng{__float_as_uint(ctl.y), __float_as_uint(ctl.z)};
     f3 contrib = mk(0.f, 0.f, 0.f), next = add(hs.p, muls(hs.normal, 0.001f));
     bool nee = false;
     if (S.nlights) {
@@ -388,9 +391,10 @@ __device__ __forceinline__ bool shade_path(const RenderArgs &A, const WfArgs &W,
         sh.light = e.light;
         nee = true;
     }
-    PS(W, 0, p) = pk(hs.direct, k);
-    PS(W, 1, p) = pk(hs.fcol, rng.key);
-    PS(W, 2, p) = pk(hs.normal, rng.ctr);
+    PS(W, 0, p) = pk(hs.direct, 0u);
+    PS(W, 1, p) = pk(hs.fcol, 0u);
+    PS(W, 2, p) = pk(hs.normal, 0u);
+    ctl_store(W, p, k, rng);
     PS(W, 4, p) = pk(next, 0u);
     PS(W, 3, p) = pk(contrib, NO_SLOT);
     return nee;
@@ -402,11 +406,11 @@ __device__ __forceinline__ bool shade_path(const RenderArgs &A, const WfArgs &W,
 // closest ray (org, wi) of its next bounce; otherwise the path is finished.
 __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W, uint32_t p, bool visible, f3 &org,
                                             f3 &wi) {
-    const float4 s0 = PS(W, 0, p), s1 = PS(W, 1, p), s2 = PS(W, 2, p), s3 = PS(W, 3, p);
-    const uint32_t k = __float_as_uint(s0.w);
+    const float4 s0 = PS(W, 0, p), s1 = PS(W, 1, p), s2 = PS(W, 2, p), s3 = PS(W, 3, p), ctl = PS(W, PS_CTL, p);
+    const uint32_t k = __float_as_uint(ctl.x);
     f3 direct = ld3(s0);
     const f3 fcol = ld3(s1), normal = ld3(s2);
-    Rng rng{__float_as_uint(s1.w), __float_as_uint(s2.w)};
+    Rng rng{__float_as_uint(ctl.y), __float_as_uint(ctl.z)};
     if (visible) direct = add(direct, ld3(s3));
     if ((int)k == A.K) {
         finish_path(A, W, p, k, direct);
@@ -425,8 +429,7 @@ __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W
     const f3 w = divs(muls(fcol, cosine), pdf * Kmax);
     W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(direct, 0u);
     W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
-    PS(W, 0, p) = pk(direct, k + 1);
-    PS(W, 2, p).w = __uint_as_float(rng.ctr);
+    ctl_store(W, p, k + 1, rng);
     org = ld3(PS(W, 4, p));
     return true;
 }
@@ -444,7 +447,13 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
     const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
     textured = hs.textured;
     const bool cam = k == 1u && camera_state_lean(W);
-    Rng rng = cam ? camera_rng(A, W, p) : Rng{__float_as_uint(PS(W, 1, p).w), __float_as_uint(PS(W, 2, p).w)};
+    Rng rng;
+    if (cam) {
+        rng = camera_rng(A, W, p);
+    } else {
+        const float4 ctl = PS(W, PS_CTL, p);
+        rng = Rng{__float_as_uint(ctl.y), __float_as_uint(ctl.z)};
+    }
     f3 contrib = mk(0.f, 0.f, 0.f), next = add(hs.p, muls(hs.normal, 0.001f));
     bool nee = false;
     if (S.nlights) {
@@ -468,9 +477,7 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
             const float cosine = fabsf(dot(hs.normal, wi));
             const f3 w = divs(muls(hs.fcol, cosine), pdf * Kmax);
             W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
-            PS(W, 0, p) = pk(mk(0.f, 0.f, 0.f), k + 1);
-            if (cam) PS(W, 1, p) = pk(mk(0.f, 0.f, 0.f), rng.key); // (wf_camera left it unwritten)
-            PS(W, 2, p) = pk(mk(0.f, 0.f, 0.f), rng.ctr);
+            ctl_store(W, p, k + 1, rng);
             org = next;
             cont = true;
         }
@@ -522,7 +529,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
                 W.key[0][0][j] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res_s * W.dir_res_s) + dir_bin(sh.d, W.dir_res_s)
                                  : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
                                                                                  : sort_key(A, W, p, sh.d);
-                W.perm[0][0][j] = j;
+                if (W.sort_lib) W.perm[0][0][j] = j; // (raysort.hip takes the identity itself)
             }
         }
         const uint32_t jc = block_append(cnt_closest(W, g + 1), cont, app);
@@ -533,7 +540,7 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
                 W.key[1][0][jc] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res * W.dir_res) + dir_bin(wi, W.dir_res)
                                   : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
                                                                                   : sort_key(A, W, p, wi);
-                W.perm[1][0][jc] = jc;
+                if (W.sort_lib) W.perm[1][0][jc] = jc;
             }
         }
         tally(tl, T_HIT, hit);
@@ -671,7 +678,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                 d = ld3(r1);
                 start_closest();
             } else if (state == ST_MISS) {
-                finish_path(A, W, p, __float_as_uint(PS(W, 0, p).w), mk(A.bg[0], A.bg[1], A.bg[2]));
+                finish_path(A, W, p, __float_as_uint(PS(W, PS_CTL, p).x), mk(A.bg[0], A.bg[1], A.bg[2]));
                 state = ST_NEED_WORK;
             } else if (state == ST_HIT) {
                 bool textured = false;
@@ -1191,7 +1198,10 @@ static const WfVariant kWf[] = {
     {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
      wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
     {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
-     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0}};
+     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0},
+    // 45: 43 with FD in the secondary closest trace too (3 loop-invariant lane values spilled)
+    CR_WF_OPT({wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>,
+     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4})};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
@@ -1307,7 +1317,7 @@ static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStre
     uint32_t *keys[2] = {W.key[set][0], W.key[set][1]}, *vals[2] = {W.perm[set][0], W.perm[set][1]};
     size_t tb = W.sort_tmp_bytes;
     const int bits = pixel ? W.key_bits_pixel : (set == 0 ? W.key_bits_s : W.key_bits);
-    const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, W.sort_lib != 0);
+    const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, W.sort_lib != 0, W.sort_lib == 0);
     if (sel < 0) {
         err = (int)hipErrorUnknown;
         return nullptr;

@@ -13,14 +13,16 @@
 
 #include "../../chiaroscuro-raytracer_amd/csrc/raysort.hip"
 
-static int run(uint32_t n, int bits, uint64_t seed, bool lib, std::vector<uint32_t> &ko, std::vector<uint32_t> &vo) {
+// iota: the values are not uploaded (vals[0] holds garbage) and the sort takes the identity
+static int run(uint32_t n, int bits, uint64_t seed, bool lib, std::vector<uint32_t> &ko, std::vector<uint32_t> &vo,
+               bool iota = false) {
     std::mt19937_64 rng(seed);
     std::vector<uint32_t> k(n), v(n);
     const uint32_t mask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
     for (uint32_t i = 0; i < n; i++) {
         k[i] = (uint32_t)rng() & mask;
         if (seed & 1) k[i] &= ~0x0f0u; // clustered keys: many equal digits
-        v[i] = i;
+        v[i] = iota ? 0xdeadbeefu : i;
     }
     uint32_t *d[4];
     for (auto &p : d)
@@ -29,10 +31,10 @@ static int run(uint32_t n, int bits, uint64_t seed, bool lib, std::vector<uint32
     hipMemcpy(d[2], v.data(), (size_t)n * 4, hipMemcpyHostToDevice);
     uint32_t *keys[2] = {d[0], d[1]}, *vals[2] = {d[2], d[3]};
     size_t tb = 0;
-    cr::sort_queue(keys, vals, n, bits, nullptr, tb, nullptr, lib);
+    cr::sort_queue(keys, vals, n, bits, nullptr, tb, nullptr, lib, false);
     void *tmp = nullptr;
     if (hipMalloc(&tmp, tb ? tb : 16) != hipSuccess) return 2;
-    const int sel = cr::sort_queue(keys, vals, n, bits, tmp, tb, nullptr, lib);
+    const int sel = cr::sort_queue(keys, vals, n, bits, tmp, tb, nullptr, lib, iota);
     if (sel < 0 || hipDeviceSynchronize() != hipSuccess) return 3;
     ko.resize(n);
     vo.resize(n);
@@ -66,6 +68,14 @@ int main() {
                 }
                 if (n <= 100000 && run(n, bits, seed * 977 + n + bits, true, k1, v1) == 0 && (k0 != k1 || v0 != v1))
                     lib_diff++;
+                // the identity taken by the first pass instead of uploaded values: the same result
+                if (n == 0) continue;
+                std::vector<uint32_t> k2, v2;
+                cases++;
+                if (run(n, bits, seed * 977 + n + bits, false, k2, v2, true) || k2 != k0 || v2 != v0) {
+                    bad++;
+                    fprintf(stderr, "iota mismatch n=%u bits=%d seed=%llu\n", n, bits, (unsigned long long)seed);
+                }
             }
     printf("{\"cases\": %d, \"mismatch\": %d, \"differs_from_hipcub\": %d}\n", cases, bad, lib_diff);
     return bad ? 1 : 0;
