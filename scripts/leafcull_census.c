@@ -25,23 +25,158 @@ typedef struct {
 /* a leaf's triangles split into up to KMAX normal groups, each with its own cone and box
  * (cull per group); 'risky' = degenerate triangles, always tested */
 enum { KMAX = 4, KCFG = 4 };
+#ifndef SUBMODE
+#define SUBMODE 1
+#endif
+#ifndef SUBK
+#define SUBK 4
+#endif
 typedef struct {
     int ng, risky;
     int size[KMAX];
     double ax[KMAX][3], ct[KMAX], st[KMAX], g[KMAX], E[KMAX], box[KMAX][6];
 } Groups;
 
+/* normal groups (k-means on normal lines, k = 1..KCFG) of a list of triangles */
+static void make_groups(const float *pos, const uint32_t *ids, uint32_t c, Groups *out) {
+        double *N = (double *)malloc(sizeof(double) * 3 * c), *Ev = (double *)malloc(sizeof(double) * c),
+               *Gv = (double *)malloc(sizeof(double) * c);
+        int *ok = (int *)malloc(sizeof(int) * c), *lab = (int *)malloc(sizeof(int) * c);
+        for (uint32_t j = 0; j < c; j++) {
+            const float *p = pos + 9 * (size_t)ids[j];
+            double e1[3], e2[3];
+            for (int i = 0; i < 3; i++) {
+                e1[i] = (double)(p[3 + i] - p[i]);
+                e2[i] = (double)(p[6 + i] - p[i]);
+            }
+            double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+            double nl = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+            Ev[j] = fmax(fabs(e1[0]) + fabs(e1[1]) + fabs(e1[2]), fabs(e2[0]) + fabs(e2[1]) + fabs(e2[2]));
+            ok[j] = nl > 0;
+            Gv[j] = ok[j] ? Ev[j] * Ev[j] / nl : 0;
+            for (int i = 0; i < 3; i++) N[3 * j + i] = ok[j] ? nv[i] / nl : 0;
+        }
+        for (int k = 0; k < KCFG; k++) {
+            Groups *G = out + k;
+            const int K = k + 1;
+            double C[KMAX][3];
+            int nc = 0;
+            /* farthest-point init on normal lines, then k-means (sign-free) */
+            for (uint32_t j = 0; j < c && nc == 0; j++)
+                if (ok[j]) {
+                    for (int i = 0; i < 3; i++) C[0][i] = N[3 * j + i];
+                    nc = 1;
+                }
+            while (nc && nc < K) {
+                double worst = 2;
+                int wj = -1;
+                for (uint32_t j = 0; j < c; j++) {
+                    if (!ok[j]) continue;
+                    double best = 0;
+                    for (int q = 0; q < nc; q++)
+                        best = fmax(best, fabs(N[3 * j] * C[q][0] + N[3 * j + 1] * C[q][1] + N[3 * j + 2] * C[q][2]));
+                    if (best < worst) {
+                        worst = best;
+                        wj = (int)j;
+                    }
+                }
+                if (wj < 0 || worst > 0.999999) break;
+                for (int i = 0; i < 3; i++) C[nc][i] = N[3 * wj + i];
+                nc++;
+            }
+            for (int it = 0; it < 10 && nc; it++) {
+                double M[KMAX][9];
+                memset(M, 0, sizeof(M));
+                for (uint32_t j = 0; j < c; j++) {
+                    if (!ok[j]) continue;
+                    int bq = 0;
+                    double best = -1;
+                    for (int q = 0; q < nc; q++) {
+                        double v = fabs(N[3 * j] * C[q][0] + N[3 * j + 1] * C[q][1] + N[3 * j + 2] * C[q][2]);
+                        if (v > best) {
+                            best = v;
+                            bq = q;
+                        }
+                    }
+                    lab[j] = bq;
+                    for (int a = 0; a < 3; a++)
+                        for (int b = 0; b < 3; b++) M[bq][3 * a + b] += N[3 * j + a] * N[3 * j + b];
+                }
+                for (int q = 0; q < nc; q++) {
+                    double v[3] = {C[q][0], C[q][1], C[q][2]};
+                    for (int r = 0; r < 30; r++) {
+                        double w[3] = {M[q][0] * v[0] + M[q][1] * v[1] + M[q][2] * v[2],
+                                       M[q][3] * v[0] + M[q][4] * v[1] + M[q][5] * v[2],
+                                       M[q][6] * v[0] + M[q][7] * v[1] + M[q][8] * v[2]};
+                        double l = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+                        if (!(l > 0)) break;
+                        for (int i = 0; i < 3; i++) v[i] = w[i] / l;
+                    }
+                    for (int i = 0; i < 3; i++) C[q][i] = v[i];
+                }
+            }
+            G->ng = nc;
+            G->risky = 0;
+            for (int q = 0; q < nc; q++) {
+                G->size[q] = 0;
+                G->ct[q] = 1;
+                G->g[q] = G->E[q] = 0;
+                for (int i = 0; i < 3; i++) {
+                    G->ax[q][i] = C[q][i];
+                    G->box[q][i] = INFINITY;
+                    G->box[q][3 + i] = -INFINITY;
+                }
+            }
+            for (uint32_t j = 0; j < c; j++) {
+                if (!ok[j] || !nc) {
+                    G->risky++;
+                    continue;
+                }
+                int bq = 0;
+                double best = -1;
+                for (int q = 0; q < nc; q++) {
+                    double v = fabs(N[3 * j] * C[q][0] + N[3 * j + 1] * C[q][1] + N[3 * j + 2] * C[q][2]);
+                    if (v > best) {
+                        best = v;
+                        bq = q;
+                    }
+                }
+                G->size[bq]++;
+                G->ct[bq] = fmin(G->ct[bq], fmax(0.0, best - 1e-9));
+                G->g[bq] = fmax(G->g[bq], Gv[j]);
+                G->E[bq] = fmax(G->E[bq], Ev[j]);
+                const float *p = pos + 9 * (size_t)ids[j];
+                for (int v = 0; v < 3; v++)
+                    for (int i = 0; i < 3; i++) {
+                        G->box[bq][i] = fmin(G->box[bq][i], p[3 * v + i]);
+                        G->box[bq][3 + i] = fmax(G->box[bq][3 + i], p[3 * v + i]);
+                    }
+            }
+            for (int q = 0; q < nc; q++) G->st[q] = sqrt(1 - G->ct[q] * G->ct[q]);
+        }
+        free(N);
+        free(Ev);
+        free(Gv);
+        free(ok);
+        free(lab);
+}
+
+
 typedef struct {
     const uint32_t *is_leaf, *axis, *child, *first, *count, *refs;
     const float *split, *box, *pos; /* pos: 9 floats per triangle */
     double *lbox;                   /* per node: tight box of the leaf's triangles (min3 max3) */
+    double *sbox;                   /* per node: union of the leaf boxes of its subtree */
+    double spad;                    /* relative pad of the padded subtree variant (x scene extent) */
     Cone *cone;
     Groups *grp; /* [node][KCFG]: 1..KCFG groups */
+    Groups *sgrp; /* [node]: SUBK groups over the subtree's references */
 } Tree;
 
 enum { S_QUERIES, S_LEAVES, S_TESTS, S_LEAF_EMPTY, S_CULL0_LEAVES, S_CULL0_TESTS, S_CULLP_LEAVES, S_CULLP_TESTS,
        S_OCCLUDED, S_CONE_LEAVES, S_CONE_TESTS, S_CONE_FAIL, S_G1_TESTS, S_G2_TESTS, S_G3_TESTS, S_G4_TESTS,
-       S_N };
+       S_INNER, S_SUB_ROOTS, S_SUB_INNER, S_SUB_LEAVES, S_SUB_TESTS, S_SUBP_ROOTS, S_SUBP_INNER, S_SUBP_LEAVES,
+       S_SUBP_TESTS, S_SUBG_ROOTS, S_SUBG_INNER, S_SUBG_LEAVES, S_SUBG_TESTS, S_N };
 
 
 static int mt(const float o[3], const float d[3], const float *tri, float tmax, float *tout) {
@@ -231,9 +366,53 @@ static void leaf_census(const Tree *T, uint32_t n, const float o[3], const float
 
 /* returns 1 when the shadow query is occluded / the closest query hit */
 static int node(const Tree *T, uint32_t n, const float o[3], const float d[3], float tmin, float tmax, int shadow,
-                uint32_t excl, float *best, uint64_t *st) {
+                uint32_t excl, float *best, uint64_t *st, int sub, int subp, int subg, int entry) {
+    /* subtree census: would a box test of the subtree's triangle union against [0, tmax]
+     * skip this node (sub: unpadded, an upper bound; subp: padded by spad) */
+    {
+        const double *sb = T->sbox + 6 * (size_t)n;
+        if (!sub && !seg_box(o, d, 0.0, (double)tmax, sb, sb + 3)) {
+            sub = 1;
+            st[S_SUB_ROOTS]++;
+        }
+        if (!subp) {
+            double lo[3], hi[3];
+            for (int i = 0; i < 3; i++) {
+                lo[i] = sb[i] - T->spad;
+                hi[i] = sb[3 + i] + T->spad;
+            }
+            if (!seg_box(o, d, -T->spad, (double)tmax * (1 + 1e-5) + T->spad, lo, hi)) {
+                subp = 1;
+                st[S_SUBP_ROOTS]++;
+            }
+        }
+    }
+    /* entry: 0 root, 1 near-only / far-only step, 2 near child of a split, 3 far child of a split (the pop) */
+    if (!subg && (T->is_leaf[n] ? T->count[n] > 0 : 1) &&
+        (SUBMODE == 1 || entry == 0 || (SUBMODE == 2 && entry == 3) || (SUBMODE == 3 && entry >= 2))) {
+        const Groups *G = T->sgrp + n;
+        int skip = G->ng > 0 && !G->risky;
+        for (int q = 0; q < G->ng && skip; q++)
+            if (!group_skip(o, d, tmax, G->ax[q], G->ct[q], G->st[q], G->g[q], G->E[q], G->box[q])) skip = 0;
+        if (skip) {
+            subg = 1;
+            st[S_SUBG_ROOTS]++;
+        }
+    }
     if (T->is_leaf[n]) {
+        if (subg) {
+            st[S_SUBG_LEAVES]++;
+            st[S_SUBG_TESTS] += T->count[n];
+        }
         st[S_LEAVES]++;
+        if (sub) {
+            st[S_SUB_LEAVES]++;
+            st[S_SUB_TESTS] += T->count[n];
+        }
+        if (subp) {
+            st[S_SUBP_LEAVES]++;
+            st[S_SUBP_TESTS] += T->count[n];
+        }
         leaf_census(T, n, o, d, tmax, st);
         int hit = 0;
         for (uint32_t j = 0; j < T->count[n]; j++) {
@@ -249,24 +428,28 @@ static int node(const Tree *T, uint32_t n, const float o[3], const float d[3], f
         }
         return hit;
     }
+    st[S_INNER]++;
+    if (sub) st[S_SUB_INNER]++;
+    if (subp) st[S_SUBP_INNER]++;
+    if (subg) st[S_SUBG_INNER]++;
     const uint32_t a = T->axis[n];
     const float pos = T->split[n];
     const float ts = (pos - o[a]) / d[a];
     const int below = o[a] < pos || (o[a] == pos && d[a] <= 0);
     const uint32_t nearc = T->child[n] + (1 - below), farc = T->child[n] + below;
-    if (ts >= tmax || ts < 0) return node(T, nearc, o, d, tmin, tmax, shadow, excl, best, st);
-    if (ts <= tmin) return node(T, farc, o, d, tmin, tmax, shadow, excl, best, st);
+    if (ts >= tmax || ts < 0) return node(T, nearc, o, d, tmin, tmax, shadow, excl, best, st, sub, subp, subg, 1);
+    if (ts <= tmin) return node(T, farc, o, d, tmin, tmax, shadow, excl, best, st, sub, subp, subg, 1);
     if (!shadow) *best = ts;
-    if (node(T, nearc, o, d, tmin, ts, shadow, excl, best, st)) return 1;
+    if (node(T, nearc, o, d, tmin, ts, shadow, excl, best, st, sub, subp, subg, 2)) return 1;
     if (!shadow) *best = tmax;
-    return node(T, farc, o, d, ts, tmax, shadow, excl, best, st);
+    return node(T, farc, o, d, ts, tmax, shadow, excl, best, st, sub, subp, subg, 3);
 }
 
 void census(uint32_t nn, const uint32_t *is_leaf, const uint32_t *axis, const float *split, const uint32_t *child,
             const uint32_t *first, const uint32_t *count, const uint32_t *refs, const float *box, const float *pos,
             uint32_t nr, const float *orig, const float *dir, const float *dist, const uint32_t *excl, int shadow,
-            uint64_t *out) {
-    Tree T = {is_leaf, axis, child, first, count, refs, split, box, pos, NULL};
+            uint64_t *out, double spad_rel) {
+    Tree T = {is_leaf, axis, child, first, count, refs, split, box, pos, NULL, NULL, 0.0, NULL, NULL, NULL};
     T.lbox = (double *)malloc(sizeof(double) * 6 * (size_t)nn);
     for (uint32_t n = 0; n < nn; n++) {
         double *b = T.lbox + 6 * (size_t)n;
@@ -281,6 +464,22 @@ void census(uint32_t nn, const uint32_t *is_leaf, const uint32_t *axis, const fl
                     b[3 + i] = fmax(b[3 + i], p[3 * v + i]);
                 }
         }
+    }
+    T.sbox = (double *)malloc(sizeof(double) * 6 * (size_t)nn);
+    memcpy(T.sbox, T.lbox, sizeof(double) * 6 * (size_t)nn);
+    for (uint32_t n = nn; n-- > 0;) /* children follow their parent in DFS order */
+        if (!is_leaf[n])
+            for (int c = 0; c < 2; c++) {
+                const double *b = T.sbox + 6 * (size_t)(child[n] + c);
+                for (int i = 0; i < 3; i++) {
+                    T.sbox[6 * (size_t)n + i] = fmin(T.sbox[6 * (size_t)n + i], b[i]);
+                    T.sbox[6 * (size_t)n + 3 + i] = fmax(T.sbox[6 * (size_t)n + 3 + i], b[3 + i]);
+                }
+            }
+    {
+        double ext = 0;
+        for (int i = 0; i < 3; i++) ext = fmax(ext, (double)box[3 + i] - box[i]);
+        T.spad = ext * spad_rel;
     }
     T.cone = (Cone *)calloc(nn, sizeof(Cone));
     for (uint32_t n = 0; n < nn; n++) {
@@ -342,127 +541,41 @@ void census(uint32_t nn, const uint32_t *is_leaf, const uint32_t *axis, const fl
 #pragma omp parallel for schedule(dynamic, 64)
     for (uint32_t n = 0; n < nn; n++) {
         if (!is_leaf[n] || !count[n]) continue;
-        const uint32_t c = count[n];
-        double *N = (double *)malloc(sizeof(double) * 3 * c), *Ev = (double *)malloc(sizeof(double) * c),
-               *Gv = (double *)malloc(sizeof(double) * c);
-        int *ok = (int *)malloc(sizeof(int) * c), *lab = (int *)malloc(sizeof(int) * c);
-        for (uint32_t j = 0; j < c; j++) {
-            const float *p = pos + 9 * (size_t)refs[first[n] + j];
-            double e1[3], e2[3];
-            for (int i = 0; i < 3; i++) {
-                e1[i] = (double)(p[3 + i] - p[i]);
-                e2[i] = (double)(p[6 + i] - p[i]);
+        make_groups(pos, refs + first[n], count[n], T.grp + (size_t)n * KCFG);
+    }
+    /* subtree groups: the same over every reference of the subtree's leaves */
+    T.sgrp = (Groups *)calloc((size_t)nn, sizeof(Groups));
+#pragma omp parallel for schedule(dynamic, 1)
+    for (uint32_t n = 0; n < nn; n++) {
+        if (is_leaf[n]) {
+            if (count[n]) {
+                Groups G4[KCFG];
+                make_groups(pos, refs + first[n], count[n], G4);
+                T.sgrp[n] = G4[SUBK - 1];
             }
-            double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
-            double nl = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
-            Ev[j] = fmax(fabs(e1[0]) + fabs(e1[1]) + fabs(e1[2]), fabs(e2[0]) + fabs(e2[1]) + fabs(e2[2]));
-            ok[j] = nl > 0;
-            Gv[j] = ok[j] ? Ev[j] * Ev[j] / nl : 0;
-            for (int i = 0; i < 3; i++) N[3 * j + i] = ok[j] ? nv[i] / nl : 0;
+            continue;
         }
-        for (int k = 0; k < KCFG; k++) {
-            Groups *G = T.grp + (size_t)n * KCFG + k;
-            const int K = k + 1;
-            double C[KMAX][3];
-            int nc = 0;
-            /* farthest-point init on normal lines, then k-means (sign-free) */
-            for (uint32_t j = 0; j < c && nc == 0; j++)
-                if (ok[j]) {
-                    for (int i = 0; i < 3; i++) C[0][i] = N[3 * j + i];
-                    nc = 1;
-                }
-            while (nc && nc < K) {
-                double worst = 2;
-                int wj = -1;
-                for (uint32_t j = 0; j < c; j++) {
-                    if (!ok[j]) continue;
-                    double best = 0;
-                    for (int q = 0; q < nc; q++)
-                        best = fmax(best, fabs(N[3 * j] * C[q][0] + N[3 * j + 1] * C[q][1] + N[3 * j + 2] * C[q][2]));
-                    if (best < worst) {
-                        worst = best;
-                        wj = (int)j;
-                    }
-                }
-                if (wj < 0 || worst > 0.999999) break;
-                for (int i = 0; i < 3; i++) C[nc][i] = N[3 * wj + i];
-                nc++;
+        uint32_t cap = 1024, c = 0, sp = 0, stk[256];
+        uint32_t *ids = (uint32_t *)malloc(sizeof(uint32_t) * cap);
+        stk[sp++] = n;
+        while (sp) {
+            uint32_t m = stk[--sp];
+            if (!is_leaf[m]) {
+                stk[sp++] = child[m];
+                stk[sp++] = child[m] + 1;
+                continue;
             }
-            for (int it = 0; it < 10 && nc; it++) {
-                double M[KMAX][9];
-                memset(M, 0, sizeof(M));
-                for (uint32_t j = 0; j < c; j++) {
-                    if (!ok[j]) continue;
-                    int bq = 0;
-                    double best = -1;
-                    for (int q = 0; q < nc; q++) {
-                        double v = fabs(N[3 * j] * C[q][0] + N[3 * j + 1] * C[q][1] + N[3 * j + 2] * C[q][2]);
-                        if (v > best) {
-                            best = v;
-                            bq = q;
-                        }
-                    }
-                    lab[j] = bq;
-                    for (int a = 0; a < 3; a++)
-                        for (int b = 0; b < 3; b++) M[bq][3 * a + b] += N[3 * j + a] * N[3 * j + b];
-                }
-                for (int q = 0; q < nc; q++) {
-                    double v[3] = {C[q][0], C[q][1], C[q][2]};
-                    for (int r = 0; r < 30; r++) {
-                        double w[3] = {M[q][0] * v[0] + M[q][1] * v[1] + M[q][2] * v[2],
-                                       M[q][3] * v[0] + M[q][4] * v[1] + M[q][5] * v[2],
-                                       M[q][6] * v[0] + M[q][7] * v[1] + M[q][8] * v[2]};
-                        double l = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-                        if (!(l > 0)) break;
-                        for (int i = 0; i < 3; i++) v[i] = w[i] / l;
-                    }
-                    for (int i = 0; i < 3; i++) C[q][i] = v[i];
-                }
+            for (uint32_t j = 0; j < count[m]; j++) {
+                if (c == cap) ids = (uint32_t *)realloc(ids, sizeof(uint32_t) * (cap *= 2));
+                ids[c++] = refs[first[m] + j];
             }
-            G->ng = nc;
-            G->risky = 0;
-            for (int q = 0; q < nc; q++) {
-                G->size[q] = 0;
-                G->ct[q] = 1;
-                G->g[q] = G->E[q] = 0;
-                for (int i = 0; i < 3; i++) {
-                    G->ax[q][i] = C[q][i];
-                    G->box[q][i] = INFINITY;
-                    G->box[q][3 + i] = -INFINITY;
-                }
-            }
-            for (uint32_t j = 0; j < c; j++) {
-                if (!ok[j] || !nc) {
-                    G->risky++;
-                    continue;
-                }
-                int bq = 0;
-                double best = -1;
-                for (int q = 0; q < nc; q++) {
-                    double v = fabs(N[3 * j] * C[q][0] + N[3 * j + 1] * C[q][1] + N[3 * j + 2] * C[q][2]);
-                    if (v > best) {
-                        best = v;
-                        bq = q;
-                    }
-                }
-                G->size[bq]++;
-                G->ct[bq] = fmin(G->ct[bq], fmax(0.0, best - 1e-9));
-                G->g[bq] = fmax(G->g[bq], Gv[j]);
-                G->E[bq] = fmax(G->E[bq], Ev[j]);
-                const float *p = pos + 9 * (size_t)refs[first[n] + j];
-                for (int v = 0; v < 3; v++)
-                    for (int i = 0; i < 3; i++) {
-                        G->box[bq][i] = fmin(G->box[bq][i], p[3 * v + i]);
-                        G->box[bq][3 + i] = fmax(G->box[bq][3 + i], p[3 * v + i]);
-                    }
-            }
-            for (int q = 0; q < nc; q++) G->st[q] = sqrt(1 - G->ct[q] * G->ct[q]);
         }
-        free(N);
-        free(Ev);
-        free(Gv);
-        free(ok);
-        free(lab);
+        if (c) {
+            Groups G4[KCFG];
+            make_groups(pos, ids, c, G4);
+            T.sgrp[n] = G4[SUBK - 1];
+        }
+        free(ids);
     }
     memset(out, 0, sizeof(uint64_t) * S_N);
 #pragma omp parallel
@@ -493,13 +606,15 @@ void census(uint32_t nn, const uint32_t *is_leaf, const uint32_t *axis, const fl
                 tmax = dist[r] < tmax ? dist[r] : tmax;
             }
             float best = tmax;
-            if (node(&T, 0, o, d, tmin, tmax, shadow, excl ? excl[r] : 0xffffffffu, &best, st) && shadow)
+            if (node(&T, 0, o, d, tmin, tmax, shadow, excl ? excl[r] : 0xffffffffu, &best, st, 0, 0, 0, 0) && shadow)
                 st[S_OCCLUDED]++;
         }
 #pragma omp critical
         for (int i = 0; i < S_N; i++) out[i] += st[i];
     }
     free(T.lbox);
+    free(T.sbox);
     free(T.cone);
     free(T.grp);
+    free(T.sgrp);
 }

@@ -20,7 +20,9 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT / "chiaroscuro-raytracer_amd"), str(ROOT / "oracle")]
 os.environ.setdefault("CHIARO_QUIET", "1")
 NAMES = ("queries", "leaves", "tests", "leaf_empty", "cull0_leaves", "cull0_tests", "cullp_leaves", "cullp_tests",
-         "occluded", "cone_leaves", "cone_tests", "cone_fail", "g1_tests", "g2_tests", "g3_tests", "g4_tests")
+         "occluded", "cone_leaves", "cone_tests", "cone_fail", "g1_tests", "g2_tests", "g3_tests", "g4_tests",
+         "inner", "sub_roots", "sub_inner", "sub_leaves", "sub_tests", "subp_roots", "subp_inner", "subp_leaves",
+         "subp_tests", "subg_roots", "subg_inner", "subg_leaves", "subg_tests")
 
 
 def main():
@@ -28,9 +30,12 @@ def main():
     ap.add_argument("--config", default="sponza")
     ap.add_argument("--res", default="320x180")
     ap.add_argument("--spp", type=int, default=2)
+    ap.add_argument("--subk", type=int, default=4, help="normal groups per subtree record (census)")
+    ap.add_argument("--submode", type=int, default=1, help="1 every node, 2 pops only, 3 both children of splits")
+    ap.add_argument("--spad", type=float, default=1e-4, help="subtree census pad, x scene extent")
     args = ap.parse_args()
     so = "/tmp/leafcull_census.so"
-    subprocess.run(["gcc", "-O2", "-fopenmp", "-shared", "-fPIC", "-o", so, str(ROOT / "scripts/leafcull_census.c"),
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-DSUBK=%d" % args.subk, "-DSUBMODE=%d" % args.submode, "-shared", "-fPIC", "-o", so, str(ROOT / "scripts/leafcull_census.c"),
                     "-lm"], check=True)
     L = C.CDLL(so)
     import chiaroscuro_amd as ca
@@ -88,7 +93,7 @@ def main():
         L.census(C.c_uint32(len(kd["is_leaf"])), u32(kd["is_leaf"]), u32(kd["axis"]), f32(kd["split"]),
                  u32(kd["child"]), u32(kd["leaf_first"]), u32(kd["leaf_count"]), u32(kd["refs"]), f32(kd["box"]),
                  f32(pos), C.c_uint32(len(o)), f32(keep[0]), f32(keep[1]), f32(keep[2]), u32(keep[3]),
-                 C.c_int(int(shadow)), st.ctypes.data_as(C.c_void_p))
+                 C.c_int(int(shadow)), st.ctypes.data_as(C.c_void_p), C.c_double(args.spad))
         s = dict(zip(NAMES, (int(x) for x in st)))
         s["cull0_test_frac"] = round(s["cull0_tests"] / max(s["tests"], 1), 4)
         s["cullp_test_frac"] = round(s["cullp_tests"] / max(s["tests"], 1), 4)
@@ -98,6 +103,10 @@ def main():
         for k in (1, 2, 3, 4):
             s["g%d_test_frac" % k] = round(s["g%d_tests" % k] / max(s["tests"], 1), 4)
         s["tests_per_query"] = round(s["tests"] / max(s["queries"], 1), 1)
+        for k in ("sub", "subp", "subg"):
+            s[k + "_inner_frac"] = round(s[k + "_inner"] / max(s["inner"], 1), 4)
+            s[k + "_leaf_frac"] = round(s[k + "_leaves"] / max(s["leaves"], 1), 4)
+        s["inner_per_query"] = round(s["inner"] / max(s["queries"], 1), 1)
         return s
 
     out["shadow"] = run(so_, sd, dist, li, True)
