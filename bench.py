@@ -261,6 +261,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-perf-pass", action="store_true",
                     help="skip the untimed performed-work pass (profiling runs: its kernels are not the timed ones)")
+    ap.add_argument("--layers-per-pass", type=int, default=2,
+                    help="progressive layers per render pass where they fit one path chunk (1 = one per pass)")
     ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")
     args = ap.parse_args()
@@ -316,15 +318,29 @@ def run_rank(args, world, backend):
               "trace_ms": [0.0] * 4, "trace_launches": [0] * 4}
     wavefront = args.kernel in (-1, 2)
 
-    def step(layer, record):
+    # layers per render pass: a rank's share of the frame renders two progressive layers in one
+    # pass where their paths fit one chunk (N >= 2; the whole frame at N = 1 does not), so the
+    # generations' latency-bound ends are paid once per two layers; bit-identical to one per pass
+    p1 = ca.render_params(xres, yres, spp, k, seed, layer=1, rank=rank, nranks=world, tile=tile)
+    nl_pass = dev.layers_per_pass(p1, args.layers_per_pass) if hasattr(dev, "layers_per_pass") else 1
+    if dist:  # every rank must run the same passes (the gathers pair up)
+        t = torch.tensor([nl_pass], dtype=torch.int64, device=backend.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        nl_pass = int(t.item())
+
+    def step(layer, n, record):
+        """Layers layer .. layer + n - 1 (n <= nl_pass) as one pass."""
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
-        fr.render_layer(cam, p, stream)
+        if n == 1:
+            fr.render_layer(cam, p, stream)
+        else:
+            fr.render_layers(cam, p, n, stream)
         if record:
             c = dev.counters()
             totals["rays"] += c["closest"] + c["shadow"]
             totals["kernel_ms"] += dev.last_kernel_ms()
             totals["px"] += c["pixels"]
-            totals["launches"] += 1
+            totals["launches"] += n  # layers: kernel_ms / launches is the render time per layer
             if wavefront:
                 ts = dev.trace_stats()
                 for i, kind in enumerate(ca.TRACE_KINDS):
@@ -337,18 +353,24 @@ def run_rank(args, world, backend):
     dev.set_option("counters", 0)
     layer = 1
     first_timed = args.warmup + 1
-    for w in range(args.warmup):
-        step(layer, False)
-        layer += 1
+    w = 0
+    while w < args.warmup:
+        n = min(nl_pass, args.warmup - w)
+        step(layer, n, False)
+        layer += n
+        w += n
         if rank == 0:
             log("warmup %d done" % w)
     if dist:
         dist.barrier()
     backend.synchronize()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(layer, True)
-        layer += 1
+    s = 0
+    while s < args.steps:
+        n = min(nl_pass, args.steps - s)
+        step(layer, n, True)
+        layer += n
+        s += n
         if rank == 0:
             log("step %d: %.3fs elapsed" % (s, time.perf_counter() - t0))
     backend.synchronize()
@@ -533,7 +555,7 @@ def run_rank(args, world, backend):
             "config": {"workload": label, "spp_per_step": spp, "k": k, "tile": tile,
                        "parallelism": "tile-split x%d" % world, "gather": args.gather if world > 1 else None,
                        "rays": int(rays_all),
-                       "rank_render_ms": rank_render_ms,
+                       "rank_render_ms": rank_render_ms, "layers_per_pass": nl_pass,
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": roofline,
             "cpu_baseline": cpu,

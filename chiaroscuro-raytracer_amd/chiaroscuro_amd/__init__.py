@@ -182,7 +182,8 @@ HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "c
                "cr_device_count", "cr_group_create", "cr_group_destroy", "cr_group_last_error", "cr_group_size", "cr_group_ok",
                "cr_group_upload_scene", "cr_group_set_option", "cr_group_render", "cr_group_get_counters",
                "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap", "cr_set_accumulator",
-               "cr_group_set_accumulator")
+               "cr_group_set_accumulator", "cr_layers_per_pass", "cr_render_layers_device",
+               "cr_render_tiles_layers_device")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
                 "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
@@ -236,6 +237,10 @@ def libs():
     _sig(hip, "cr_render", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), FP])
     _sig(hip, "cr_render_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
     _sig(hip, "cr_render_tiles_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
+    _sig(hip, "cr_layers_per_pass", C.c_uint32, [P, C.POINTER(CrRenderParams), C.c_uint32])
+    _sig(hip, "cr_render_layers_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P, P])
+    _sig(hip, "cr_render_tiles_layers_device", C.c_int,
+         [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P, P])
     _sig(hip, "cr_blend_tiles_device", C.c_int, [P, C.POINTER(CrRenderParams), P, P, P])
     _sig(hip, "cr_tiles_for_rank", C.c_uint32, [C.POINTER(CrRenderParams), C.c_uint32])
     _sig(hip, "cr_tile_origin", C.c_int, [C.POINTER(CrRenderParams), C.c_uint32, C.c_uint32,
@@ -508,6 +513,24 @@ class Device:
     def render_tiles_device(self, cam, p, d_tiles_ptr: int, stream: int = 0):
         self._chk(libs()[0].cr_render_tiles_device(self._c, C.byref(cam), C.byref(p), C.c_void_p(d_tiles_ptr),
                                                    C.c_void_p(stream)), "cr_render_tiles_device")
+
+    def layers_per_pass(self, p, want: int) -> int:
+        """How many of `want` progressive layers (from p.layer) fit one render pass."""
+        return int(libs()[0].cr_layers_per_pass(self._c, C.byref(p), want))
+
+    def render_layers_device(self, cam, p, nlayers: int, d_frame_ptr: int, stream: int = 0):
+        """Layers p.layer .. p.layer + nlayers - 1 in one pass, blended in order into d_frame
+        (bit-identical to nlayers render_device calls)."""
+        self._chk(libs()[0].cr_render_layers_device(self._c, C.byref(cam), C.byref(p), nlayers,
+                                                    C.c_void_p(d_frame_ptr), C.c_void_p(stream)),
+                  "cr_render_layers_device")
+
+    def render_tiles_layers_device(self, cam, p, nlayers: int, d_tiles_ptr: int, stream: int = 0):
+        """Layers p.layer .. + nlayers - 1 in one pass; layer j's tile means at
+        d_tiles + j * max_tiles * tile * tile * 3 floats."""
+        self._chk(libs()[0].cr_render_tiles_layers_device(self._c, C.byref(cam), C.byref(p), nlayers,
+                                                          C.c_void_p(d_tiles_ptr), C.c_void_p(stream)),
+                  "cr_render_tiles_layers_device")
 
     def blend_tiles_device(self, p, d_gathered_ptr: int, d_frame_ptr: int, stream: int = 0):
         self._chk(libs()[0].cr_blend_tiles_device(self._c, C.byref(p), C.c_void_p(d_gathered_ptr),

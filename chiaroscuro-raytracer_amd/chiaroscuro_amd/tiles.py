@@ -84,6 +84,7 @@ class DistributedFrame:
         split = nranks > 1 and gather == "torch"
         self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), **f32) if split else None
         self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), **f32) if split and rank == 0 else None
+        self.tiles_multi = None  # [nlayers][max_tiles][tile][tile][3] of render_layers
         if nranks > 1 and gather == "cabi":
             uid = [dev.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
@@ -128,6 +129,35 @@ class DistributedFrame:
             raise ValueError(err)
         return int(layers.item())
 
+    def render_layers(self, cam, params, nlayers: int, stream: int = 0):
+        """Layers params.layer .. + nlayers - 1 as ONE render pass of my tiles
+        (cr_render_layers_device / cr_render_tiles_layers_device: bit-identical to
+        nlayers render_layer calls), then per layer the gather and blend.  nlayers
+        must fit one pass (Device.layers_per_pass); the library's own gather
+        ("cabi") renders layer by layer."""
+        import torch
+        L = self.layout
+        if nlayers == 1 or (L.nranks > 1 and self.gather == "cabi"):
+            for j in range(nlayers):
+                self.render_layer(cam, _with_layer(params, params.layer + j), stream)
+            return
+        if (params.rank, params.nranks, params.tile or 32, params.xres, params.yres) != \
+                (self.rank, L.nranks, L.tile, L.xres, L.yres):
+            raise ValueError("render_layers: params do not match this frame's partition")
+        if L.nranks == 1:
+            self.dev.render_layers_device(cam, params, nlayers, self.frame.data_ptr(), stream)
+            return
+        if self.tiles_multi is None or self.tiles_multi.shape[0] < nlayers:
+            self.tiles_multi = torch.zeros((nlayers,) + tuple(self.tiles.shape), dtype=self.tiles.dtype,
+                                           device=self.tiles.device)
+        self.dev.render_tiles_layers_device(cam, params, nlayers, self.tiles_multi.data_ptr(), stream)
+        for j in range(nlayers):
+            self.dist.gather(self.tiles_multi[j], [self.gathered[r] for r in range(L.nranks)] if self.rank == 0
+                             else None, dst=0)
+            if self.rank == 0:
+                self.dev.blend_tiles_device(_with_layer(params, params.layer + j), self.gathered.data_ptr(),
+                                            self.frame.data_ptr(), stream)
+
     def render_layer(self, cam, params, stream: int = 0):
         """params: chiaroscuro_amd.render_params(..., layer=L, rank, nranks, tile)."""
         L = self.layout
@@ -144,3 +174,10 @@ class DistributedFrame:
         self.dist.gather(self.tiles, [self.gathered[r] for r in range(L.nranks)] if self.rank == 0 else None, dst=0)
         if self.rank == 0:
             self.dev.blend_tiles_device(params, self.gathered.data_ptr(), self.frame.data_ptr(), stream)
+
+
+def _with_layer(params, layer: int):
+    """A copy of render params (a ctypes struct) with another layer."""
+    q = type(params).from_buffer_copy(params)
+    q.layer = layer
+    return q

@@ -93,6 +93,8 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.bg[2] = p->background[2];
     A.seed = p->seed;
     A.layer = p->layer;
+    A.nl = 1;
+    A.layer_stride = 0;
     A.rank = p->rank;
     A.nranks = p->nranks;
     A.tile = tile_of(p);
@@ -150,13 +152,28 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
 }
 
-int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st) {
+// path slots one wavefront chunk may hold: ~45% of the free HBM (the grown buffers included)
+uint64_t wf_path_cap(cr_ctx *c, int k) {
+    size_t freeb = 0, totalb = 0;
+    if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) return ~0ull;
+    return (uint64_t)((freeb + c->wf_bytes + c->wf2_bytes) * 0.45) / cr::wf_bytes_per_path(k);
+}
+
+int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st,
+               uint32_t nl) {
     if (!cam || !out) return fail(c, CR_E_INVALID, "null camera/output");
     int rc = check_params(c, p);
     if (rc) return rc;
+    if (nl < 1 || (nl > 1 && (c->kernel != 2 || c->wf_lanes != 1)))
+        return fail(c, CR_E_INVALID, "layers per pass: >= 1, and > 1 only with the wavefront kernel in one lane");
     HIPCHK(hipSetDevice(c->device));
     cr::RenderArgs A{};
     fill_args(c, A, cam, p, out, mode);
+    // nl layers in one pass: every item holds nl * spp samples (layer p->layer + s / spp)
+    const uint64_t spp_pass = (uint64_t)p->spp * nl;
+    if (spp_pass >= (1ull << 31)) return fail(c, CR_E_INVALID, "layers x spp too large");
+    A.nl = nl;
+    A.layer_stride = (uint64_t)cr_tiles_for_rank(p, 0) * A.tile * A.tile * 3;
     if (c->kernel == 2 && !c->full_counters && !cr::wf_variant_available(A.variant))
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
                                          " is not compiled in (make ALL_VARIANTS=1)");
@@ -175,8 +192,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         const uint64_t per_sample = (uint64_t)A.n_items * 12u;
         uint64_t chunk = std::max<uint64_t>(1, c->sample_buf / std::max<uint64_t>(per_sample, 1));
         chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(1, (1ull << 31) / std::max<uint32_t>(A.n_items, 1)));
-        chunk = std::min<uint64_t>(chunk, p->spp);
-        const bool chunked = chunk < p->spp;
+        chunk = std::min<uint64_t>(chunk, spp_pass);
+        const bool chunked = chunk < spp_pass;
+        if (nl > 1 && chunked) return fail(c, CR_E_INVALID, "layers per pass: the samples do not fit one buffer");
         // wavefront: a second stack-overflow area for the closest trace that runs beside a
         // shadow trace, per lane
         if (cr::persistent_gstack_bytes(c->stack_depth, A.gstride) >= (1ull << 32)) // (gstack_at's 32-bit offsets)
@@ -201,10 +219,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             uint64_t P = (uint64_t)A.n_items * chunk;
             if (lanes == 2) P = (P + 1) / 2;
             P = std::min<uint64_t>(P, c->wf_paths);
-            size_t freeb = 0, totalb = 0;
-            if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-                const uint64_t cap = (uint64_t)((freeb + c->wf_bytes + c->wf2_bytes) * 0.45) /
-                                     cr::wf_bytes_per_path(p->k) / (uint64_t)lanes;
+            {
+                const uint64_t cap = wf_path_cap(c, p->k) / (uint64_t)lanes;
                 P = std::max<uint64_t>(std::min<uint64_t>(P, cap), std::min<uint64_t>(P, 1u << 20));
             }
             const size_t f4 = 16 * (size_t)P;
@@ -318,9 +334,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             if (int e = cr::launch_cam_cull(A, c->n_refs, (float4 *)c->d_cull, (float4 *)c->d_cull_node, c->d_levels,
                                             (const uint32_t(*)[2])c->levels.data(), (int)c->levels.size(), st))
                 return hip_fail(c, (hipError_t)e, "cull-box kernel launch");
-        for (uint32_t s0 = 0; s0 < p->spp; s0 += (uint32_t)chunk) {
+        for (uint32_t s0 = 0; s0 < spp_pass; s0 += (uint32_t)chunk) {
             A.s0 = s0;
-            A.s_count = (uint32_t)std::min<uint64_t>(chunk, p->spp - s0);
+            A.s_count = (uint32_t)std::min<uint64_t>(chunk, spp_pass - s0);
             A.n_work = A.n_items * A.s_count;
             int e = 0;
             if (wf && lanes == 2) {
@@ -340,7 +356,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
                 e = cr::launch_persistent(A, c->waves_per_cu, c->num_cus, st);
             }
-            if (!e) e = cr::launch_sum_samples(A, s0 == 0, s0 + A.s_count == p->spp, st);
+            if (!e) e = cr::launch_sum_samples(A, s0 == 0, s0 + A.s_count == spp_pass, st);
             if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
         }
         HIPCHK(hipEventRecord(c->ev1, st));
@@ -788,6 +804,34 @@ int cr_render_tiles_device(cr_ctx *c, const cr_camera *cam, const cr_render_para
     if (!c) return CR_E_INVALID;
     if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
     return run_render(c, cam, p, d_tiles, cr::MODE_TILES, (hipStream_t)stream);
+}
+
+uint32_t cr_layers_per_pass(cr_ctx *c, const cr_render_params *p, uint32_t want) {
+    if (!c || c->device < 0 || !c->has_scene || !p || want < 1 || check_params(c, p) != CR_OK) return 1;
+    if (c->kernel != 2 || c->wf_lanes != 1 || c->full_counters) return 1;
+    if (hipSetDevice(c->device) != hipSuccess) return 1;
+    const uint64_t items = (uint64_t)cr_tiles_for_rank(p, p->rank) * tile_of(p) * tile_of(p);
+    const uint64_t paths_cap = std::min<uint64_t>(c->wf_paths, wf_path_cap(c, p->k));
+    uint32_t nl = want;
+    // one chunk of paths, one sample buffer, a 31-bit work index
+    while (nl > 1 && (items * p->spp * nl > paths_cap || items * 12u * p->spp * nl > c->sample_buf ||
+                      items * p->spp * nl >= (1ull << 31)))
+        nl--;
+    return nl;
+}
+
+int cr_render_layers_device(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                            float *d_frame, void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    return run_render(c, cam, p, d_frame, cr::MODE_BLEND, (hipStream_t)stream, nlayers);
+}
+
+int cr_render_tiles_layers_device(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                                  float *d_tiles, void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    return run_render(c, cam, p, d_tiles, cr::MODE_TILES, (hipStream_t)stream, nlayers);
 }
 
 int cr_blend_tiles_device(cr_ctx *c, const cr_render_params *p, const float *d_gathered, float *d_frame,

@@ -136,7 +136,9 @@ int grow(cr_ctx *c, void **buf, size_t &cap, size_t need);
 // one render pass of p's tiles (MODE_TILES: compact [tiles][T][T][3] batch means
 // into out) or of the whole frame blended into out (MODE_BLEND), on stream st;
 // returns after the pass, counters and trace stats are read back
-int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st);
+// nl > 1 (wavefront kernel): layers p->layer .. p->layer + nl - 1 in one pass (cr_render_layers_device)
+int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st,
+               uint32_t nl = 1);
 // group.cpp: the communicator and buffers of the multi-process split (cr_destroy)
 void release_dist(cr_ctx *c);
 } // namespace crx

@@ -116,6 +116,11 @@ struct RenderArgs {
     int K;
     float bg[3];
     uint32_t seed, layer;
+    // layers rendered by this pass (wavefront kernel): layers layer .. layer + nl - 1, their samples
+    // one run per item ("virtual" sample s -> layer + s / spp, sample s % spp); MODE_TILES writes
+    // layer j's tile means at out + j * layer_stride floats
+    uint32_t nl;
+    uint64_t layer_stride;
     uint32_t rank, nranks, tile, tiles_x;
     uint32_t n_items;     // my_tiles * tile * tile
     uint32_t stack_depth;

@@ -247,9 +247,18 @@ __global__ void __launch_bounds__(256) sum_samples(RenderArgs A, int first, int 
         f3 temp = mk(0.f, 0.f, 0.f);
         if (!first) temp = mk(A.run[3 * (size_t)item], A.run[3 * (size_t)item + 1], A.run[3 * (size_t)item + 2]);
         const float *sm = A.samples + 3 * (size_t)item * A.s_count;
-        for (uint32_t s = 0; s < A.s_count; s++) temp = add(temp, mk(sm[3 * s], sm[3 * s + 1], sm[3 * s + 2]));
+        // A.nl layers in one pass (never sample-chunked): each layer's run of A.spp samples is
+        // summed in sample order and blended / written as its own layer, in layer order
+        for (uint32_t j = 0; j + 1 < A.nl; j++) {
+            for (uint32_t s = j * A.spp; s < (j + 1) * A.spp; s++)
+                temp = add(temp, mk(sm[3 * s], sm[3 * s + 1], sm[3 * s + 2]));
+            write_pixel(A, px, py, item, temp, j);
+            temp = mk(0.f, 0.f, 0.f);
+        }
+        const uint32_t s_first = (A.nl - 1) * A.spp;
+        for (uint32_t s = s_first; s < A.s_count; s++) temp = add(temp, mk(sm[3 * s], sm[3 * s + 1], sm[3 * s + 2]));
         if (last) {
-            write_pixel(A, px, py, item, temp);
+            write_pixel(A, px, py, item, temp, A.nl - 1);
         } else {
             A.run[3 * (size_t)item] = temp.x;
             A.run[3 * (size_t)item + 1] = temp.y;
@@ -257,7 +266,8 @@ __global__ void __launch_bounds__(256) sum_samples(RenderArgs A, int first, int 
         }
     }
     const uint64_t b = __ballot(valid && last);
-    if (b && (threadIdx.x & 63u) == 0) atomicAdd(&A.counters[T_PIXELS], (unsigned long long)__popcll(b));
+    // (pixels written: one per layer of the pass)
+    if (b && (threadIdx.x & 63u) == 0) atomicAdd(&A.counters[T_PIXELS], (unsigned long long)__popcll(b) * A.nl);
 }
 
 // Variants (cr_set_option "variant"): LDS ring depth R, software-pipelined leaf

@@ -163,19 +163,29 @@ __device__ __forceinline__ bool item_pixel(const RenderArgs &A, uint32_t item, u
     return x < A.xres && y < A.yres;
 }
 
-__device__ __forceinline__ void write_pixel(const RenderArgs &A, uint32_t x, uint32_t y, uint32_t item, f3 temp) {
+// The RNG stream of a path: pixel and sample s of this pass, which holds A.nl layers' samples as
+// one run per item (s / spp = the layer's offset from A.layer); A.nl = 1: the layer itself.
+__device__ __forceinline__ Rng path_rng(const RenderArgs &A, uint32_t pixel, uint32_t s) {
+    const uint32_t j = A.nl > 1 ? s / A.spp : 0u;
+    return rng_make(A.seed, A.layer + j, pixel, s - j * A.spp);
+}
+
+// lj: the layer's offset in this pass (layer A.layer + lj)
+__device__ __forceinline__ void write_pixel(const RenderArgs &A, uint32_t x, uint32_t y, uint32_t item, f3 temp,
+                                            uint32_t lj = 0) {
     const float inv = 1.f / (float)A.spp;
+    const uint32_t layer = A.layer + lj;
     if (A.mode == MODE_TILES) {
         const f3 m = muls(temp, inv);
-        float *o = A.out + 3 * (size_t)item;
+        float *o = A.out + (size_t)lj * A.layer_stride + 3 * (size_t)item;
         o[0] = m.x;
         o[1] = m.y;
         o[2] = m.z;
     } else {
         float *o = A.out + 3 * ((size_t)y * A.xres + x);
         // rayTracer.cpp:64  (old * (L-1) + temp * invSamples) / L
-        const f3 old = (A.layer > 1) ? mk(o[0], o[1], o[2]) : mk(0.f, 0.f, 0.f);
-        const f3 nw = divs(add(muls(old, (float)(A.layer - 1)), muls(temp, inv)), (float)A.layer);
+        const f3 old = (layer > 1) ? mk(o[0], o[1], o[2]) : mk(0.f, 0.f, 0.f);
+        const f3 nw = divs(add(muls(old, (float)(layer - 1)), muls(temp, inv)), (float)layer);
         o[0] = nw.x;
         o[1] = nw.y;
         o[2] = nw.z;

@@ -149,7 +149,7 @@ __device__ __forceinline__ Rng camera_rng(const RenderArgs &A, const WfArgs &W, 
     const uint32_t w = W.w0 + p, item = w / A.s_count, s = A.s0 + (w - item * A.s_count);
     uint32_t px = 0, py = 0;
     item_pixel(A, item, px, py);
-    Rng rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
+    Rng rng = path_rng(A, py * A.xres + px, s);
     rng.ctr = 2u; // camera_dir's y- and x-jitter draws
     return rng;
 }
@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
         // ray p of generation 1 is path p's camera ray (no compaction: the few
         // partial-tile paths get a dead ray, path = NO_PATH)
         if (valid) { // rayTracer.cpp:58-62: jittered camera ray of sample s
-            Rng rng = rng_make(A.seed, A.layer, py * A.xres + px, s);
+            Rng rng = path_rng(A, py * A.xres + px, s);
             float2 sxy;
             const f3 d = camera_dir(A, px, py, rng, &sxy);
             if (A.cull) W.cxy[p] = sxy;

@@ -210,6 +210,23 @@ int cr_render_tiles_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_pa
 int cr_blend_tiles_device(cr_ctx *ctx, const cr_render_params *p, const float *d_gathered, float *d_frame,
                           void *stream);
 uint32_t cr_tiles_for_rank(const cr_render_params *p, uint32_t rank);
+
+/* Several progressive layers in ONE render pass (wavefront kernel): layers p->layer ..
+ * p->layer + nlayers - 1 of the loop at src/rayTracer.cpp:18-33, each with its own samples and
+ * RNG streams, so the result is bit-identical to nlayers calls of cr_render_device /
+ * cr_render_tiles_device.  The paths of all layers share one chunk, so the latency-bound ends of
+ * the generations (and the per-render cull boxes) are paid once per pass instead of per layer --
+ * what a rank's small share of the frame needs when the frame is split over GPUs.
+ * cr_layers_per_pass: how many of `want` layers fit one path chunk and one sample buffer (1 when
+ * the kernel, lanes or counting build do not allow more); a larger nlayers is refused
+ * (CR_E_INVALID).  cr_render_layers_device blends the layers in order into d_frame;
+ * cr_render_tiles_layers_device writes layer j's batch means at
+ * d_tiles + j * cr_tiles_for_rank(p, 0) * tile * tile * 3 floats. */
+uint32_t cr_layers_per_pass(cr_ctx *ctx, const cr_render_params *p, uint32_t want);
+int cr_render_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                            float *d_frame, void *stream);
+int cr_render_tiles_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                                  float *d_tiles, void *stream);
 /* Pixel origin of rank's local tile `local` (slot rank + local * nranks of the frame's
  * row-major tile slots; with nranks > 1 each tile row is rotated by its index, so a
  * rank's tiles spread over every column class). */

@@ -2,7 +2,8 @@
 without N GPUs): renders EVERY rank's tiles of an N-way split one after another
 and reports each rank's pass time; a strong-scaling step ends with the slowest
 rank, so the projected speedup is t(1) / max over ranks of t(rank), for N in
---nranks.
+--nranks.  --layers L renders up to L progressive layers per pass (what fits one path
+chunk: cr_layers_per_pass, 1 for the whole frame), as bench.py does; times are per layer.
     python scripts/rank_time.py [--config sponza] [--nranks 1,2,4,8] [--rounds 2]
 """
 import argparse
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE", help="cr_set_option (experiments)")
     ap.add_argument("--tile", type=int, default=32, help="tile edge of the split (bench.py: 32)")
+    ap.add_argument("--layers", type=int, default=2, help="layers per pass where they fit (bench.py: 2)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -47,12 +49,14 @@ def main():
             for rank in range(n):
                 p = ca.render_params(i["xres"], i["yres"], spp, i["k"], i["seed"], rank=rank, nranks=n,
                                      tile=args.tile)
-                tiles = torch.zeros((ca.Device.tiles_for_rank(p, rank), args.tile, args.tile, 3),
+                nl = dev.layers_per_pass(p, args.layers)
+                tiles = torch.zeros((nl, ca.Device.tiles_for_rank(p, 0), args.tile, args.tile, 3),
                                     dtype=torch.float32, device="cuda")
-                dev.render_tiles_device(cam, p, tiles.data_ptr())
+                dev.render_tiles_layers_device(cam, p, nl, tiles.data_ptr())
                 torch.cuda.synchronize()
                 c = dev.counters()
-                res.setdefault(n, {}).setdefault(rank, []).append((dev.last_kernel_ms(), c["closest"] + c["shadow"]))
+                res.setdefault(n, {}).setdefault(rank, []).append(
+                    (dev.last_kernel_ms() / nl, (c["closest"] + c["shadow"]) / nl, nl))
     base = None
     for n, ranks in sorted(res.items()):
         ms = {rk: statistics.median(x[0] for x in xs) for rk, xs in ranks.items()}
@@ -64,6 +68,7 @@ def main():
                           "imbalance": round(ms[slow] / (sum(ms.values()) / n), 3),
                           "projected_mray_s": round(rays / ms[slow] / 1e3, 1), "ideal_ms": round(base / n, 2),
                           "projected_speedup": round(base / ms[slow], 2),
+                          "layers_per_pass": ranks[0][0][2],
                           "rank_mrays": [round(ranks[rk][0][1] / 1e6, 2) for rk in sorted(ranks)]}), flush=True)
 
 

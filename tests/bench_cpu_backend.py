@@ -84,6 +84,30 @@ class OracleDevice:
         f = _view(frame_ptr, (p.yres, p.xres, 3))
         f[...] = mean if p.layer == 1 else (f * np.float32(p.layer - 1) + mean) / np.float32(p.layer)
 
+    # several layers per pass: the oracle renders them one by one (the GPU path renders them in
+    # one pass, bit-identical); counters and time add up over the pass
+    def layers_per_pass(self, p, want):
+        return want
+
+    def _layers(self, p, n, one):
+        from chiaroscuro_amd.tiles import _with_layer
+        tot, ms = {}, 0.0
+        for j in range(n):
+            one(j, _with_layer(p, p.layer + j))
+            ms += self.last_ms
+            for key, v in self.last.items():
+                tot[key] = tot.get(key, 0) + v
+        self.last, self.last_ms = tot, ms
+
+    def render_tiles_layers_device(self, cam, p, n, ptr, stream=0):
+        from chiaroscuro_amd.tiles import TileLayout
+        lay = TileLayout(p.xres, p.yres, p.nranks, p.tile)
+        stride = lay.max_tiles * lay.tile * lay.tile * 3 * 4
+        self._layers(p, n, lambda j, q: self.render_tiles_device(cam, q, ptr + j * stride, stream))
+
+    def render_layers_device(self, cam, p, n, frame_ptr, stream=0):
+        self._layers(p, n, lambda j, q: self.render_device(cam, q, frame_ptr, stream))
+
     def counters(self):
         return dict(self.last)
 

@@ -20,7 +20,7 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-RES, SPP, WARMUP, STEPS = (40, 24), 2, 1, 2
+RES, SPP, WARMUP, STEPS = (40, 24), 2, 1, 3
 
 
 def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
@@ -38,6 +38,9 @@ def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
     assert line["n_gpus"] == 2 and line["steps"] == STEPS and line["backend"] == "cpu-oracle"
     assert len(line["config"]["rank_render_ms"]) == 2 and all(v > 0 for v in line["config"]["rank_render_ms"])
     assert line["config"]["parallelism"] == "tile-split x2"
+    # two layers per render pass (DistributedFrame.render_layers: one pass, a gather + blend per
+    # layer), then the odd step as a single-layer pass
+    assert line["config"]["layers_per_pass"] == 2
     # the oracle's frame and rays over the same layers (warmup layers included in the frame)
     sc = scenes.config_rtc("cornell")
     s = ca.Scene(sc, "xres", str(RES[0]), "yres", str(RES[1]))

@@ -734,3 +734,79 @@ def test_default_build_by_scene_size(ca, sponza, nanobox):
             pair.dev.set_option("counters", 1)
         masks[name] = perf["shadow"]["masks"] + perf["closest"]["masks"] + perf["tail"]["masks"]
     assert masks["sponza"] > 0 and masks["nanobox"] == 0, masks
+
+
+@pytest.mark.parametrize("tail_min", [0, 1 << 30])
+def test_layers_per_pass_bitexact(ca, sponza, nanobox, tail_min):
+    """Several progressive layers in ONE render pass (cr_render_layers_device /
+    cr_render_tiles_layers_device: the paths of all layers in one chunk, each with its
+    layer's RNG streams, src/rayTracer.cpp:18-33) equal one pass per layer bit for bit:
+    the blended frame against the oracle's layers 1..3, and each layer's tile means
+    against render_tiles_device of that layer alone (3 ranks, tile 16, ragged edges);
+    wavefront generations and the tail kernel from generation 1."""
+    import torch
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (70, 45, 4))):
+        dev = pair.dev
+        cam = pair.camera(ca, x, y)
+        dev.set_option("kernel", 2)
+        dev.set_option("counters", 0)
+        dev.set_option("wf_tail_min", tail_min)
+        try:
+            p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=1)
+            assert dev.layers_per_pass(p, 3) == 3
+            frame = torch.zeros((y, x, 3), dtype=torch.float32, device="cuda")
+            dev.render_layers_device(cam, p, 3, frame.data_ptr())
+            torch.cuda.synchronize()
+            c3 = dev.counters()
+            o = None
+            rays = 0
+            for layer in (1, 2, 3):
+                o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
+                rays += oc["closest"] + oc["shadow"]
+            assert_bitwise(frame.cpu().numpy(), o, "3 layers in one pass %dx%dx%d" % (x, y, s))
+            assert c3["closest"] + c3["shadow"] == rays and c3["pixels"] == 3 * x * y
+            tile, nr = 16, 3
+            for r in range(nr):
+                q = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=2, rank=r, nranks=nr, tile=tile)
+                mt = ca.Device.tiles_for_rank(q, 0)
+                both = torch.full((2, mt, tile, tile, 3), -1.0, dtype=torch.float32, device="cuda")
+                dev.render_tiles_layers_device(cam, q, 2, both.data_ptr())
+                for j in range(2):
+                    one = torch.full((mt, tile, tile, 3), -1.0, dtype=torch.float32, device="cuda")
+                    dev.render_tiles_device(cam, ca.render_params(x, y, s, 6, 0xC41A05C0, layer=2 + j, rank=r,
+                                                                  nranks=nr, tile=tile), one.data_ptr())
+                    torch.cuda.synchronize()
+                    assert_bitwise(both[j].cpu().numpy(), one.cpu().numpy(), "rank %d layer %d tiles" % (r, 2 + j))
+        finally:
+            dev.set_option("wf_tail_min", 0)
+            dev.set_option("counters", 1)
+            torch.cuda.synchronize()
+
+
+def test_layers_per_pass_limits(ca, cornell):
+    """cr_layers_per_pass caps the layers at what fits one sample buffer (option
+    sample_buf_bytes) and is 1 for the counting build and the other kernels; a pass of
+    more layers than fit, or with another kernel, is refused with an error, not chunked."""
+    import torch
+    dev = cornell.dev
+    cam = cornell.camera(ca, 32, 32)
+    p = ca.render_params(32, 32, 4, 6, 5)
+    frame = torch.zeros((32, 32, 3), dtype=torch.float32, device="cuda")
+    assert dev.layers_per_pass(p, 4) == 1  # counting build
+    dev.set_option("counters", 0)
+    try:
+        dev.set_option("kernel", 2)
+        assert dev.layers_per_pass(p, 4) == 4
+        dev.set_option("sample_buf_bytes", 32 * 32 * 12 * 4 * 2)  # two layers' samples
+        assert dev.layers_per_pass(p, 4) == 2
+        with pytest.raises(RuntimeError):
+            dev.render_layers_device(cam, p, 3, frame.data_ptr())
+        dev.set_option("kernel", 0)
+        assert dev.layers_per_pass(p, 4) == 1
+        with pytest.raises(RuntimeError):
+            dev.render_layers_device(cam, p, 2, frame.data_ptr())
+    finally:
+        dev.set_option("sample_buf_bytes", 4 << 30)
+        dev.set_option("kernel", 2)
+        dev.set_option("counters", 1)
+        torch.cuda.synchronize()
