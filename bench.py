@@ -245,7 +245,7 @@ def load_backend():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (= rank processes) of one node, default 1")
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza", help="cornell | cornell_box | sponza | sponza_4k")
     ap.add_argument("--spp", type=int, default=0, help="override samples per step (default: config's)")
@@ -261,8 +261,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-perf-pass", action="store_true",
                     help="skip the untimed performed-work pass (profiling runs: its kernels are not the timed ones)")
-    ap.add_argument("--layers-per-pass", type=int, default=2,
-                    help="progressive layers per render pass where they fit one path chunk (1 = one per pass)")
+    ap.add_argument("--layers-per-pass", type=int, default=8,
+                    help="progressive layers per render pass group (DistributedFrame.plan_layers; 1 = one per pass)")
     ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")
     args = ap.parse_args()
@@ -318,34 +318,42 @@ def run_rank(args, world, backend):
               "trace_ms": [0.0] * 4, "trace_launches": [0] * 4}
     wavefront = args.kernel in (-1, 2)
 
-    # layers per render pass: a rank's share of the frame renders two progressive layers in one
-    # pass where their paths fit one chunk (N >= 2; the whole frame at N = 1 does not), so the
-    # generations' latency-bound ends are paid once per two layers; bit-identical to one per pass
+    # layers per render pass: up to --layers-per-pass progressive layers are rendered as one
+    # pass group -- each pass holds the paths of all of them for a share of the frame (a rank's
+    # tiles; on one GPU the frame is cut into the fewest tile-split pieces whose paths fit one
+    # chunk), so the per-pass latency-bound generation ends are paid once per group and each
+    # pass traces several layers' samples of a smaller screen region (more coherent, L2-resident
+    # work); bit-identical to one layer per pass (tests/test_gpu_parity.py)
+    dev.set_option("counters", 0)  # (the timed, lean build: the counting build renders one layer per pass)
     p1 = ca.render_params(xres, yres, spp, k, seed, layer=1, rank=rank, nranks=world, tile=tile)
-    nl_pass = dev.layers_per_pass(p1, args.layers_per_pass) if hasattr(dev, "layers_per_pass") else 1
+    nl_pass, _ = fr.plan_layers(p1, args.layers_per_pass)
     if dist:  # every rank must run the same passes (the gathers pair up)
         t = torch.tensor([nl_pass], dtype=torch.int64, device=backend.device)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         nl_pass = int(t.item())
+    groups = []
 
     def step(layer, n, record):
-        """Layers layer .. layer + n - 1 (n <= nl_pass) as one pass."""
+        """Layers layer .. layer + n - 1 (n <= nl_pass) as one pass group."""
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
-        if n == 1:
+        n, pieces = fr.plan_layers(p, n)
+        if n == 1 and pieces == 1:
             fr.render_layer(cam, p, stream)
         else:
-            fr.render_layers(cam, p, n, stream)
+            fr.render_layers(cam, p, n, stream, pieces=pieces)
         if record:
-            c = dev.counters()
+            groups.append((n, pieces))
+            st = fr.last_stats()
+            c = st["counters"]
             totals["rays"] += c["closest"] + c["shadow"]
-            totals["kernel_ms"] += dev.last_kernel_ms()
+            totals["kernel_ms"] += st["kernel_ms"]
             totals["px"] += c["pixels"]
             totals["launches"] += n  # layers: kernel_ms / launches is the render time per layer
-            if wavefront:
-                ts = dev.trace_stats()
+            if wavefront and st["trace"]:
                 for i, kind in enumerate(ca.TRACE_KINDS):
-                    totals["trace_ms"][i] += ts[kind]["ms"]
-                    totals["trace_launches"][i] += ts[kind]["launches"]
+                    totals["trace_ms"][i] += st["trace"][kind]["ms"]
+                    totals["trace_launches"][i] += st["trace"][kind]["launches"]
+        return n
 
     # Timed launches count only rays; the node/leaf/triangle counters of SURVEY §8d
     # (algorithmic bytes) come from one extra, untimed launch of the counting
@@ -355,8 +363,7 @@ def run_rank(args, world, backend):
     first_timed = args.warmup + 1
     w = 0
     while w < args.warmup:
-        n = min(nl_pass, args.warmup - w)
-        step(layer, n, False)
+        n = step(layer, min(nl_pass, args.warmup - w), False)
         layer += n
         w += n
         if rank == 0:
@@ -367,8 +374,7 @@ def run_rank(args, world, backend):
     t0 = time.perf_counter()
     s = 0
     while s < args.steps:
-        n = min(nl_pass, args.steps - s)
-        step(layer, n, True)
+        n = step(layer, min(nl_pass, args.steps - s), True)
         layer += n
         s += n
         if rank == 0:
@@ -556,6 +562,7 @@ def run_rank(args, world, backend):
                        "parallelism": "tile-split x%d" % world, "gather": args.gather if world > 1 else None,
                        "rays": int(rays_all),
                        "rank_render_ms": rank_render_ms, "layers_per_pass": nl_pass,
+                       "pass_groups": [list(g) for g in groups],
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": roofline,
             "cpu_baseline": cpu,

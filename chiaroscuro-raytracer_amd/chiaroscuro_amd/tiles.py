@@ -85,6 +85,7 @@ class DistributedFrame:
         self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), **f32) if split else None
         self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), **f32) if split and rank == 0 else None
         self.tiles_multi = None  # [nlayers][max_tiles][tile][tile][3] of render_layers
+        self._stats_begin()
         if nranks > 1 and gather == "cabi":
             uid = [dev.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
@@ -129,28 +130,59 @@ class DistributedFrame:
             raise ValueError(err)
         return int(layers.item())
 
-    def render_layers(self, cam, params, nlayers: int, stream: int = 0):
-        """Layers params.layer .. + nlayers - 1 as ONE render pass of my tiles
-        (cr_render_layers_device / cr_render_tiles_layers_device: bit-identical to
-        nlayers render_layer calls), then per layer the gather and blend.  nlayers
-        must fit one pass (Device.layers_per_pass); the library's own gather
-        ("cabi") renders layer by layer."""
+    def plan_layers(self, params, want: int):
+        """(layers, pieces) of one render pass group starting at params.layer: up to
+        `want` progressive layers rendered together.  Every pass holds the paths of
+        `layers` layers of a share of the frame; a pass is filled best when that share is
+        small, so on ONE rank the frame is cut into `pieces` (the ranks of a pieces-way
+        tile split, each rendered as its own pass of all the layers) -- the smallest
+        number whose paths fit one chunk (Device.layers_per_pass).  With several ranks
+        a rank's share is its tiles (pieces = 1) and `layers` what fits it."""
+        L = self.layout
+        want = max(1, int(want))
+        if not hasattr(self.dev, "layers_per_pass") or (L.nranks > 1 and self.gather == "cabi"):
+            return 1, 1
+        if L.nranks > 1:
+            return self.dev.layers_per_pass(params, want), 1
+        for nl in range(want, 0, -1):
+            for m in range(1, min(64, L.ntiles) + 1):
+                q = _with_layer(params, params.layer)
+                q.rank, q.nranks = 0, m
+                if self.dev.layers_per_pass(q, nl) == nl:
+                    return nl, m
+        return 1, 1
+
+    def render_layers(self, cam, params, nlayers: int, stream: int = 0, pieces: int = 1):
+        """Layers params.layer .. + nlayers - 1 as ONE render pass of my tiles (of each of
+        `pieces` frame pieces on a single rank) -- cr_render_layers_device /
+        cr_render_tiles_layers_device, bit-identical to nlayers render_layer calls --
+        then per layer the gather and blend.  (nlayers, pieces) from plan_layers; the
+        library's own gather ("cabi") renders layer by layer.  last_stats() sums the
+        passes' counters."""
         import torch
         L = self.layout
-        if nlayers == 1 or (L.nranks > 1 and self.gather == "cabi"):
+        self._stats_begin()
+        if nlayers == 1 and pieces == 1 or (L.nranks > 1 and self.gather == "cabi"):
             for j in range(nlayers):
-                self.render_layer(cam, _with_layer(params, params.layer + j), stream)
+                self._render_one(cam, _with_layer(params, params.layer + j), stream)
             return
         if (params.rank, params.nranks, params.tile or 32, params.xres, params.yres) != \
                 (self.rank, L.nranks, L.tile, L.xres, L.yres):
             raise ValueError("render_layers: params do not match this frame's partition")
         if L.nranks == 1:
-            self.dev.render_layers_device(cam, params, nlayers, self.frame.data_ptr(), stream)
+            for k in range(pieces):  # piece k: rank k of a pieces-way split, blended in place
+                q = _with_layer(params, params.layer)
+                q.rank, q.nranks = k, pieces
+                self.dev.render_layers_device(cam, q, nlayers, self.frame.data_ptr(), stream)
+                self._stats_add()
             return
+        if pieces != 1:
+            raise ValueError("render_layers: frame pieces on a single rank only")
         if self.tiles_multi is None or self.tiles_multi.shape[0] < nlayers:
             self.tiles_multi = torch.zeros((nlayers,) + tuple(self.tiles.shape), dtype=self.tiles.dtype,
                                            device=self.tiles.device)
         self.dev.render_tiles_layers_device(cam, params, nlayers, self.tiles_multi.data_ptr(), stream)
+        self._stats_add()
         for j in range(nlayers):
             self.dist.gather(self.tiles_multi[j], [self.gathered[r] for r in range(L.nranks)] if self.rank == 0
                              else None, dst=0)
@@ -158,19 +190,53 @@ class DistributedFrame:
                 self.dev.blend_tiles_device(_with_layer(params, params.layer + j), self.gathered.data_ptr(),
                                             self.frame.data_ptr(), stream)
 
-    def render_layer(self, cam, params, stream: int = 0):
+    # the device's counters, pass time and trace stats summed over the passes of the last
+    # render_layer(s) call
+    def _stats_begin(self):
+        self._stats = {"counters": {}, "kernel_ms": 0.0, "trace": None, "passes": 0}
+
+    def _stats_add(self):
+        st = self._stats
+        st["passes"] += 1
+        if not hasattr(self.dev, "counters"):  # (a device with the render / blend calls only)
+            return
+        for key, v in self.dev.counters().items():
+            st["counters"][key] = st["counters"].get(key, 0) + v
+        st["kernel_ms"] += self.dev.last_kernel_ms()
+        if hasattr(self.dev, "trace_stats"):
+            ts = self.dev.trace_stats()
+            if st["trace"] is None:
+                st["trace"] = {k: dict(v) for k, v in ts.items()}
+            else:
+                for kind, v in ts.items():
+                    for key, x in v.items():
+                        st["trace"][kind][key] += x
+
+    def last_stats(self):
+        """{"counters", "kernel_ms", "trace", "passes"} of the last render_layer(s) call."""
+        return self._stats
+
+    def _render_one(self, cam, params, stream):
+        self.render_layer(cam, params, stream, _keep_stats=True)
+
+    def render_layer(self, cam, params, stream: int = 0, _keep_stats: bool = False):
         """params: chiaroscuro_amd.render_params(..., layer=L, rank, nranks, tile)."""
+        if not _keep_stats:
+            self._stats_begin()
         L = self.layout
         if (params.rank, params.nranks, params.tile or 32, params.xres, params.yres) != \
                 (self.rank, L.nranks, L.tile, L.xres, L.yres):
             raise ValueError("render_layer: params do not match this frame's partition")
         if L.nranks == 1:
             self.dev.render_device(cam, params, self.frame.data_ptr(), stream)
+            self._stats_add()
             return
         if self.gather == "cabi":
             self.dev.render_dist_device(cam, params, self.frame.data_ptr() if self.rank == 0 else 0, stream)
+            self._stats_add()
             return
         self.dev.render_tiles_device(cam, params, self.tiles.data_ptr(), stream)
+        self._stats_add()
         self.dist.gather(self.tiles, [self.gathered[r] for r in range(L.nranks)] if self.rank == 0 else None, dst=0)
         if self.rank == 0:
             self.dev.blend_tiles_device(params, self.gathered.data_ptr(), self.frame.data_ptr(), stream)

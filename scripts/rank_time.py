@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE", help="cr_set_option (experiments)")
     ap.add_argument("--tile", type=int, default=32, help="tile edge of the split (bench.py: 32)")
-    ap.add_argument("--layers", type=int, default=2, help="layers per pass where they fit (bench.py: 2)")
+    ap.add_argument("--layers", type=int, default=8, help="layers per pass group (bench.py --layers-per-pass)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -49,14 +49,23 @@ def main():
             for rank in range(n):
                 p = ca.render_params(i["xres"], i["yres"], spp, i["k"], i["seed"], rank=rank, nranks=n,
                                      tile=args.tile)
-                nl = dev.layers_per_pass(p, args.layers)
-                tiles = torch.zeros((nl, ca.Device.tiles_for_rank(p, 0), args.tile, args.tile, 3),
-                                    dtype=torch.float32, device="cuda")
-                dev.render_tiles_layers_device(cam, p, nl, tiles.data_ptr())
-                torch.cuda.synchronize()
-                c = dev.counters()
+                if n == 1:  # one GPU: the frame in pieces, as DistributedFrame.plan_layers / bench.py
+                    from chiaroscuro_amd.tiles import DistributedFrame
+                    fr = DistributedFrame(dev, i["xres"], i["yres"], 0, 1, args.tile)
+                    nl, pieces = fr.plan_layers(p, args.layers)
+                    fr.render_layers(cam, p, nl, pieces=pieces)
+                    torch.cuda.synchronize()
+                    st = fr.last_stats()
+                    ms, c = st["kernel_ms"], st["counters"]
+                else:
+                    nl, pieces = dev.layers_per_pass(p, args.layers), 1
+                    tiles = torch.zeros((nl, ca.Device.tiles_for_rank(p, 0), args.tile, args.tile, 3),
+                                        dtype=torch.float32, device="cuda")
+                    dev.render_tiles_layers_device(cam, p, nl, tiles.data_ptr())
+                    torch.cuda.synchronize()
+                    ms, c = dev.last_kernel_ms(), dev.counters()
                 res.setdefault(n, {}).setdefault(rank, []).append(
-                    (dev.last_kernel_ms() / nl, (c["closest"] + c["shadow"]) / nl, nl))
+                    (ms / nl, (c["closest"] + c["shadow"]) / nl, nl, pieces))
     base = None
     for n, ranks in sorted(res.items()):
         ms = {rk: statistics.median(x[0] for x in xs) for rk, xs in ranks.items()}
@@ -68,7 +77,7 @@ def main():
                           "imbalance": round(ms[slow] / (sum(ms.values()) / n), 3),
                           "projected_mray_s": round(rays / ms[slow] / 1e3, 1), "ideal_ms": round(base / n, 2),
                           "projected_speedup": round(base / ms[slow], 2),
-                          "layers_per_pass": ranks[0][0][2],
+                          "layers_per_pass": ranks[0][0][2], "pieces": ranks[0][0][3],
                           "rank_mrays": [round(ranks[rk][0][1] / 1e6, 2) for rk in sorted(ranks)]}), flush=True)
 
 

@@ -30,7 +30,7 @@ def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", str(STEPS), "--warmup", str(WARMUP),
-           "--config", "cornell", "--res", "%dx%d" % RES, "--spp", str(SPP), "--no-cpu-baseline",
+           "--config", "cornell", "--res", "%dx%d" % RES, "--spp", str(SPP), "--no-cpu-baseline", "--layers-per-pass", "2",
            "--save-frame", str(frame)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
@@ -40,7 +40,7 @@ def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
     assert line["config"]["parallelism"] == "tile-split x2"
     # two layers per render pass (DistributedFrame.render_layers: one pass, a gather + blend per
     # layer), then the odd step as a single-layer pass
-    assert line["config"]["layers_per_pass"] == 2
+    assert line["config"]["layers_per_pass"] == 2 and line["config"]["pass_groups"] == [[2, 1], [1, 1]]
     # the oracle's frame and rays over the same layers (warmup layers included in the frame)
     sc = scenes.config_rtc("cornell")
     s = ca.Scene(sc, "xres", str(RES[0]), "yres", str(RES[1]))

@@ -810,3 +810,37 @@ def test_layers_per_pass_limits(ca, cornell):
         dev.set_option("kernel", 2)
         dev.set_option("counters", 1)
         torch.cuda.synchronize()
+
+
+def test_layer_groups_frame_pieces_bitexact(ca, sponza):
+    """bench.py's pass groups on one GPU (DistributedFrame.plan_layers / render_layers):
+    4 layers per pass, the frame cut into the fewest tile-split pieces whose paths fit one
+    chunk (option wf_paths caps it here), each piece blended in place -- equal bit for bit
+    to the oracle's layers 1..4, and the summed counters to the oracle's rays."""
+    import torch
+    from chiaroscuro_amd.tiles import DistributedFrame
+    x, y, s = 96, 54, 3
+    dev = sponza.dev
+    cam = sponza.camera(ca, x, y)
+    dev.set_option("kernel", 2)
+    dev.set_option("counters", 0)
+    dev.set_option("wf_paths", 40000)  # one layer of the frame is 18432 paths: 4 layers need 2 pieces
+    try:
+        fr = DistributedFrame(dev, x, y, 0, 1, 32, device="cuda")
+        p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=1)
+        nl, pieces = fr.plan_layers(p, 4)
+        assert (nl, pieces) == (4, 2)
+        fr.render_layers(cam, p, nl, pieces=pieces)
+        torch.cuda.synchronize()
+        st = fr.last_stats()
+        o, rays = None, 0
+        for layer in range(1, 5):
+            o, oc = sponza.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
+            rays += oc["closest"] + oc["shadow"]
+        assert_bitwise(fr.frame.cpu().numpy(), o, "4 layers, 2 pieces")
+        assert st["passes"] == 2 and st["counters"]["closest"] + st["counters"]["shadow"] == rays
+        assert st["counters"]["pixels"] == 4 * x * y
+    finally:
+        dev.set_option("wf_paths", 256 << 20)
+        dev.set_option("counters", 1)
+        torch.cuda.synchronize()
