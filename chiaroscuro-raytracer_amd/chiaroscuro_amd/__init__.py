@@ -183,7 +183,7 @@ HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "c
                "cr_group_upload_scene", "cr_group_set_option", "cr_group_render", "cr_group_get_counters",
                "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap", "cr_set_accumulator",
                "cr_group_set_accumulator", "cr_layers_per_pass", "cr_render_layers_device",
-               "cr_render_tiles_layers_device")
+               "cr_render_tiles_layers_device", "cr_render_layers")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
                 "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
@@ -238,6 +238,7 @@ def libs():
     _sig(hip, "cr_render_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
     _sig(hip, "cr_render_tiles_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
     _sig(hip, "cr_layers_per_pass", C.c_uint32, [P, C.POINTER(CrRenderParams), C.c_uint32])
+    _sig(hip, "cr_render_layers", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P])
     _sig(hip, "cr_render_layers_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P, P])
     _sig(hip, "cr_render_tiles_layers_device", C.c_int,
          [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P, P])
@@ -504,6 +505,16 @@ class Device:
         out = accum if accum is not None else np.zeros((p.yres, p.xres, 3), np.float32)
         assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == p.yres * p.xres * 3
         self._chk(libs()[0].cr_render(self._c, C.byref(cam), C.byref(p), _ptr(out)), "cr_render")
+        return out
+
+    def render_layers(self, cam: CrCamera, p: CrRenderParams, nlayers: int,
+                      accum: np.ndarray | None = None) -> np.ndarray:
+        """cr_render_layers: layers p.layer .. + nlayers - 1 of the whole frame in pass groups
+        (bit-identical to nlayers render calls); counters sum over the passes."""
+        out = accum if accum is not None else np.zeros((p.yres, p.xres, 3), np.float32)
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == p.yres * p.xres * 3
+        self._chk(libs()[0].cr_render_layers(self._c, C.byref(cam), C.byref(p), nlayers, _ptr(out)),
+                  "cr_render_layers")
         return out
 
     def render_device(self, cam, p, d_frame_ptr: int, stream: int = 0):

@@ -776,6 +776,73 @@ int cr_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float 
     return CR_OK;
 }
 
+// cr_render over nlayers layers in pass groups: up to LAYER_GROUP layers per pass, the frame cut
+// into the fewest tile-split pieces whose paths fit one chunk (DistributedFrame.plan_layers)
+static const uint32_t LAYER_GROUP = 8, MAX_PIECES = 64;
+int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                     float *accum_rgb_out) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!accum_rgb_out || !p || nlayers < 1) return fail(c, CR_E_INVALID, "null output/params or no layers");
+    cr_render_params q = *p;
+    if (q.nranks == 0) q.nranks = 1;
+    if (q.nranks != 1) return fail(c, CR_E_INVALID, "cr_render_layers: the whole frame (nranks 1)");
+    int rc = check_params(c, &q);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t elems = (size_t)q.xres * q.yres * 3;
+    if (elems != c->accum_elems) {
+        if (c->d_accum) hipFree(c->d_accum);
+        c->d_accum = nullptr;
+        c->accum_elems = 0;
+        if (hipMalloc(&c->d_accum, elems * sizeof(float)) != hipSuccess) return fail(c, CR_E_OOM, "accumulator");
+        c->accum_elems = elems;
+        HIPCHK(hipMemset(c->d_accum, 0, elems * sizeof(float)));
+    }
+    const uint32_t tiles = cr_tiles_for_rank(&q, 0);
+    uint64_t sum[sizeof(cr_counters) / sizeof(uint64_t)] = {};
+    float ms = 0.f;
+    cr_trace_stats ts{};
+    for (uint32_t done = 0; done < nlayers;) {
+        // the largest group that fits with at most MAX_PIECES pieces, the fewest pieces for it
+        uint32_t nl = 1, m = 1;
+        for (uint32_t want = std::min(LAYER_GROUP, nlayers - done); want > 1 && nl == 1; want--)
+            for (uint32_t pieces = 1; pieces <= std::min(MAX_PIECES, tiles); pieces++) {
+                cr_render_params t = q;
+                t.rank = 0;
+                t.nranks = pieces;
+                if (cr_layers_per_pass(c, &t, want) == want) {
+                    nl = want;
+                    m = pieces;
+                    break;
+                }
+            }
+        for (uint32_t k = 0; k < m; k++) {
+            cr_render_params t = q;
+            t.layer = q.layer + done;
+            t.rank = k;
+            t.nranks = m;
+            if ((rc = run_render(c, cam, &t, c->d_accum, cr::MODE_BLEND, c->stream, nl))) return rc;
+            const uint64_t *h = (const uint64_t *)&c->last;
+            for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) sum[i] += h[i];
+            ms += c->last_ms;
+            for (int kind = 0; kind < 4; kind++) {
+                ts.launches[kind] += c->last_trace.launches[kind];
+                ts.ms[kind] += c->last_trace.ms[kind];
+                ts.inner[kind] += c->last_trace.inner[kind];
+                ts.leaf[kind] += c->last_trace.leaf[kind];
+                ts.tritest[kind] += c->last_trace.tritest[kind];
+            }
+        }
+        done += nl;
+    }
+    std::memcpy(&c->last, sum, sizeof(cr_counters));
+    c->last_ms = ms;
+    c->last_trace = ts;
+    HIPCHK(hipMemcpy(accum_rgb_out, c->d_accum, elems * sizeof(float), hipMemcpyDeviceToHost));
+    return CR_OK;
+}
+
 int cr_set_accumulator(cr_ctx *c, uint32_t xres, uint32_t yres, const float *rgb) {
     if (!c) return CR_E_INVALID;
     if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);

@@ -39,11 +39,10 @@ int main(int argc, char **argv) {
         chiaro::Model model(scene);
         if (!model.error.empty()) std::fprintf(stderr, "%s\n", model.error.c_str());
         chiaro::RayTracer renderer(model, scene);
-        for (unsigned l = 0; l < layers; l++) {
-            renderer.rayTrace(scene.VP, scene.LA, scene.UP, scene.yview);
-            std::fprintf(stderr, "layer %u: %.3f s, %llu rays\n", renderer.layers(), renderer.lastSeconds(),
-                         (unsigned long long)(renderer.lastCounters().closest + renderer.lastCounters().shadow));
-        }
+        // the layers in pass groups (RayTracer::rayTraceLayers, bit-identical to one rayTrace per layer)
+        renderer.rayTraceLayers(layers, scene.VP, scene.LA, scene.UP, scene.yview);
+        std::fprintf(stderr, "layers 1..%u: %.3f s, %llu rays\n", renderer.layers(), renderer.lastSeconds(),
+                     (unsigned long long)(renderer.lastCounters().closest + renderer.lastCounters().shadow));
         renderer.exportImage(scene.renderPath.c_str());
     } catch (const std::exception &e) {
         std::fprintf(stderr, "chiaroscuro: %s\n", e.what());

@@ -101,7 +101,14 @@ RayTracer::~RayTracer() {
     else cr_destroy(ctx_);
 }
 
-void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) {
+void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) { rayTraceLayers(1, eye, center, up, yview); }
+
+void RayTracer::rayTraceLayers(unsigned n, vec3 eye, vec3 center, vec3 up, float yview) {
+    if (n < 1) return;
+    if (group_ && n > 1) { // the GPU group renders layer by layer
+        for (unsigned i = 0; i < n; i++) rayTraceLayers(1, eye, center, up, yview);
+        return;
+    }
     // rayTracer.cpp:24 -- including the reference's `(lastUp == lastUp)`: a
     // change of `up` alone does not reset the accumulation.
     const bool newLayer = (eye == lastEye) && (center == lastCenter) && (lastUp == lastUp) && (yview == lastYview);
@@ -138,8 +145,10 @@ void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) {
             throw std::runtime_error(std::string("chiaro: render failed: ") + cr_group_last_error(group_));
         cr_group_get_counters(group_, &counters_);
     } else {
-        if (cr_render(ctx_, &cam, &p, pixels.data()) != CR_OK)
+        if ((n == 1 ? cr_render(ctx_, &cam, &p, pixels.data()) : cr_render_layers(ctx_, &cam, &p, n, pixels.data())) !=
+            CR_OK)
             throw std::runtime_error(std::string("chiaro: render failed: ") + cr_last_error(ctx_));
+        layers_ += n - 1; // layers p.layer .. p.layer + n - 1 are in the frame
         cr_get_counters(ctx_, &counters_);
     }
     // rayTracer.cpp:51,66-68 (computed after the render instead of racily inside it)
