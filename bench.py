@@ -245,7 +245,7 @@ def load_backend():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (= rank processes) of one node, default 1")
-    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sponza", help="cornell | cornell_box | sponza | sponza_4k")
     ap.add_argument("--spp", type=int, default=0, help="override samples per step (default: config's)")
@@ -261,7 +261,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-perf-pass", action="store_true",
                     help="skip the untimed performed-work pass (profiling runs: its kernels are not the timed ones)")
-    ap.add_argument("--layers-per-pass", type=int, default=8,
+    ap.add_argument("--layers-per-pass", type=int, default=16,
                     help="progressive layers per render pass group (DistributedFrame.plan_layers; 1 = one per pass)")
     ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")

@@ -778,7 +778,7 @@ int cr_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float 
 
 // cr_render over nlayers layers in pass groups: up to LAYER_GROUP layers per pass, the frame cut
 // into the fewest tile-split pieces whose paths fit one chunk (DistributedFrame.plan_layers)
-static const uint32_t LAYER_GROUP = 8, MAX_PIECES = 64;
+static const uint32_t LAYER_GROUP = 16, MAX_PIECES = 64;
 int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
                      float *accum_rgb_out) {
     if (!c) return CR_E_INVALID;

@@ -7,11 +7,11 @@
 cd $GRAFT_REPO_ROOT
 TAG=${1:?tag}; CFG=${2:?config}; SPP=${3:?spp of the config}
 mkdir -p gpurun_out/profiles
-bash scripts/profile.sh ${TAG}_$CFG --config $CFG --steps 8 --warmup 0 --no-cpu-baseline || exit 1
+bash scripts/profile.sh ${TAG}_$CFG --config $CFG --steps 16 --warmup 0 --no-cpu-baseline || exit 1
 python scripts/prof_summary.py gpurun_out/prof_${TAG}_$CFG ${TAG}_$CFG --config $CFG --spp $SPP > gpurun_out/prof_summary_$CFG.txt || exit 1
 rm -rf gpurun_out/pmc_issue
-bash scripts/pmc_issue.sh --config $CFG --steps 8 --warmup 0 --no-cpu-baseline || exit 1
+bash scripts/pmc_issue.sh --config $CFG --steps 16 --warmup 0 --no-cpu-baseline || exit 1
 python scripts/pmc_issue_summary.py gpurun_out/pmc_issue/a/pmc_counter_collection.csv profiles/pmc_issue_$CFG.json $SPP || exit 1
-timeout -k 10 600 python bench.py --config $CFG --steps 8 --warmup 1 > profiles/${TAG}_bench_$CFG.json 2> gpurun_out/bench_$CFG.log || { echo "bench $CFG failed"; tail -20 gpurun_out/bench_$CFG.log; exit 1; }
+timeout -k 10 600 python bench.py --config $CFG --steps 16 --warmup 1 > profiles/${TAG}_bench_$CFG.json 2> gpurun_out/bench_$CFG.log || { echo "bench $CFG failed"; tail -20 gpurun_out/bench_$CFG.log; exit 1; }
 cat profiles/${TAG}_bench_$CFG.json
 cp -r profiles/. gpurun_out/profiles/

@@ -848,9 +848,9 @@ def test_layer_groups_frame_pieces_bitexact(ca, sponza):
 
 def test_render_layers_c_abi_groups_bitexact(ca, sponza):
     """cr_render_layers (the C-ABI of RayTracer::rayTraceLayers and the CLI's `layers N`):
-    10 layers of the whole frame as pass groups of up to 8 layers, each group in the fewest
-    frame pieces whose paths fit (wf_paths caps the chunk here: 8 layers in 4 pieces, then 2
-    layers in 1), equal to the oracle's layers 1..10; counters summed over the passes."""
+    20 layers of the whole frame as pass groups of up to 16 layers, each group in the fewest
+    frame pieces whose paths fit (wf_paths caps the chunk here: 14 layers in 6 pieces, then 6
+    layers in 3), equal to the oracle's layers 1..20; counters summed over the passes."""
     x, y, s = 96, 54, 2
     dev = sponza.dev
     cam = sponza.camera(ca, x, y)
@@ -858,14 +858,14 @@ def test_render_layers_c_abi_groups_bitexact(ca, sponza):
     dev.set_option("counters", 0)
     dev.set_option("wf_paths", 30000)  # a layer is 12288 paths
     try:
-        g = dev.render_layers(cam, ca.render_params(x, y, s, 6, 77, layer=1), 10)
+        g = dev.render_layers(cam, ca.render_params(x, y, s, 6, 77, layer=1), 20)
         c = dev.counters()
     finally:
         dev.set_option("wf_paths", 256 << 20)
         dev.set_option("counters", 1)
     o, rays = None, 0
-    for layer in range(1, 11):
+    for layer in range(1, 21):
         o, oc = sponza.oracle.render(cam.as_array(), x, y, s, 6, 77, layer=layer, pixels=o)
         rays += oc["closest"] + oc["shadow"]
-    assert_bitwise(g, o, "10 layers in pass groups")
-    assert c["closest"] + c["shadow"] == rays and c["pixels"] == 10 * x * y
+    assert_bitwise(g, o, "20 layers in pass groups")
+    assert c["closest"] + c["shadow"] == rays and c["pixels"] == 20 * x * y
