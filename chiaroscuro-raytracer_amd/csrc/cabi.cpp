@@ -202,7 +202,13 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         if (int r = grow(c, &c->d_gstack, c->gstack_bytes,
                          (wf ? 2 * c->wf_lanes : 1) * cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
             return r;
-        if (int r = grow(c, &c->d_samples, c->samples_bytes, per_sample * chunk)) return r;
+        // large renders reserve the whole sample budget at once: a later pass of another shape (a pass
+        // group's frame piece, cr_render_layers) then reuses the buffer instead of regrowing it
+        {
+            const uint64_t need = per_sample * chunk;
+            if (int r = grow(c, &c->d_samples, c->samples_bytes, need * 4 > c->sample_buf ? std::max<uint64_t>(need, c->sample_buf) : need))
+                return r;
+        }
         if (chunked)
             if (int r = grow(c, &c->d_run, c->run_bytes, per_sample)) return r;
         A.gstack = (uint2 *)c->d_gstack;
@@ -254,9 +260,16 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 16 * (size_t)P +
                                 (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
                                 8192;
-            if (int r = grow(c, &c->d_wf, c->wf_bytes, need)) return r;
+            // a chunk of more than a quarter of the path cap reserves the whole cap (need scaled
+            // linearly), so passes of slightly different sizes do not regrow ~100 GB of buffers
+            size_t need_alloc = need;
+            {
+                const uint64_t pcap = std::min<uint64_t>(c->wf_paths, wf_path_cap(c, p->k) / (uint64_t)lanes);
+                if (P * 4 > pcap && pcap > P) need_alloc = (size_t)((double)need * ((double)pcap / (double)P)) + 4096;
+            }
+            if (int r = grow(c, &c->d_wf, c->wf_bytes, need_alloc)) return r;
             if (lanes == 2)
-                if (int r = grow(c, &c->d_wf2, c->wf2_bytes, need)) return r;
+                if (int r = grow(c, &c->d_wf2, c->wf2_bytes, need_alloc)) return r;
             auto carve = [&](void *base, cr::WfArgs &W, int lane) {
                 char *b = (char *)base;
                 auto take = [&](size_t bytes) {
