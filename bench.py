@@ -336,7 +336,10 @@ def run_rank(args, world, backend):
     def step(layer, n, record):
         """Layers layer .. layer + n - 1 (n <= nl_pass) as one pass group."""
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
+        tp = time.perf_counter()
         n, pieces = fr.plan_layers(p, n)
+        if rank == 0:
+            log("group of %d layers in %d pieces (plan %.1f ms)" % (n, pieces, (time.perf_counter() - tp) * 1e3))
         if n == 1 and pieces == 1:
             fr.render_layer(cam, p, stream)
         else:

@@ -154,9 +154,12 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
 
 // path slots one wavefront chunk may hold: ~45% of the free HBM (the grown buffers included)
 uint64_t wf_path_cap(cr_ctx *c, int k) {
-    size_t freeb = 0, totalb = 0;
-    if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) return ~0ull;
-    return (uint64_t)((freeb + c->wf_bytes + c->wf2_bytes) * 0.45) / cr::wf_bytes_per_path(k);
+    if (!c->wf_mem_budget) {
+        size_t freeb = 0, totalb = 0;
+        if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) return ~0ull;
+        c->wf_mem_budget = freeb + c->wf_bytes + c->wf2_bytes;
+    }
+    return (uint64_t)(c->wf_mem_budget * 0.45) / cr::wf_bytes_per_path(k);
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st,
@@ -267,9 +270,11 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 const uint64_t pcap = std::min<uint64_t>(c->wf_paths, wf_path_cap(c, p->k) / (uint64_t)lanes);
                 if (P * 4 > pcap && pcap > P) need_alloc = (size_t)((double)need * ((double)pcap / (double)P)) + 4096;
             }
+            const size_t had = c->wf_bytes + c->wf2_bytes;
             if (int r = grow(c, &c->d_wf, c->wf_bytes, need_alloc)) return r;
             if (lanes == 2)
                 if (int r = grow(c, &c->d_wf2, c->wf2_bytes, need_alloc)) return r;
+            if (c->wf_bytes + c->wf2_bytes != had) c->wf_mem_budget = 0; // re-query after a growth
             auto carve = [&](void *base, cr::WfArgs &W, int lane) {
                 char *b = (char *)base;
                 auto take = [&](size_t bytes) {

@@ -24,6 +24,9 @@ struct cr_ctx {
     uint32_t *hcnt = nullptr;
     void *d_wf2 = nullptr;
     size_t wf2_bytes = 0;
+    // HBM the path-chunk buffers may take: free + their current size, queried once (hipMemGetInfo can
+    // be slow on a busy node) and again after they grow (wf_path_cap)
+    uint64_t wf_mem_budget = 0;
     float last_ms = 0.f;
     // scene
     bool has_scene = false;
