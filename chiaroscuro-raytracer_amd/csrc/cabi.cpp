@@ -259,16 +259,21 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             // (leaf keys replace the pixel and world keys in every queue: their width alone sets the
             // digit passes)
             if (leaf_keys) key_bits = leaf_bits;
+            // bytes of the buffers of a chunk of Pn paths with kb-bit sort keys
+            auto need_for = [&](uint64_t Pn, int kb) -> size_t {
+                const size_t st = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)Pn, kb, c->wf_sort_lib != 0) : 0;
+                return (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 16 * (size_t)Pn +
+                       (c->wf_sort ? 32 * (size_t)Pn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
+            };
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
-            const size_t need = (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * f4 + 16 * (size_t)P +
-                                (c->wf_sort ? 32 * (size_t)P + sort_tmp : 0) + cr::WF_CNT * sizeof(uint32_t) +
-                                8192;
-            // a chunk of more than a quarter of the path cap reserves the whole cap (need scaled
-            // linearly), so passes of slightly different sizes do not regrow ~100 GB of buffers
+            const size_t need = need_for(P, key_bits);
+            // a chunk of more than a quarter of the path cap reserves the buffers of a whole-cap chunk
+            // with the widest keys, so passes of other sizes (a pass group's frame pieces, the next
+            // layer) reuse them instead of regrowing ~100 GB inside a timed render
             size_t need_alloc = need;
             {
                 const uint64_t pcap = std::min<uint64_t>(c->wf_paths, wf_path_cap(c, p->k) / (uint64_t)lanes);
-                if (P * 4 > pcap && pcap > P) need_alloc = (size_t)((double)need * ((double)pcap / (double)P)) + 4096;
+                if (P * 4 > pcap) need_alloc = std::max(need, need_for(std::max<uint64_t>(P, pcap), 32));
             }
             const size_t had = c->wf_bytes + c->wf2_bytes;
             if (int r = grow(c, &c->d_wf, c->wf_bytes, need_alloc)) return r;

@@ -11,4 +11,5 @@ fi
 for cs in "$@"; do
   bash scripts/gpu_profile_cfg.sh r03 ${cs%%:*} ${cs##*:} > gpurun_out/cfg_${cs%%:*}.log 2>&1 || { echo "config $cs failed"; tail -20 gpurun_out/cfg_${cs%%:*}.log; exit 1; }
   tail -1 gpurun_out/cfg_${cs%%:*}.log | cut -c1-300
+  rm -rf gpurun_out/prof_r03_${cs%%:*} gpurun_out/pmc_issue  # raw CSVs (summaries are in profiles/): stay under the 64 MiB pull
 done
