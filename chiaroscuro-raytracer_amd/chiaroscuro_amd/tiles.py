@@ -144,8 +144,12 @@ class DistributedFrame:
             return 1, 1
         if L.nranks > 1:
             return self.dev.layers_per_pass(params, want), 1
+        # frame pieces only for scenes with real geometry (cr_scene_triangles; cabi.cpp PIECES_MIN_TRIS)
+        max_pieces = min(64, L.ntiles)
+        if hasattr(self.dev, "scene_triangles") and self.dev.scene_triangles() < 1024:
+            max_pieces = 1
         for nl in range(want, 0, -1):
-            for m in range(1, min(64, L.ntiles) + 1):
+            for m in range(1, max_pieces + 1):
                 q = _with_layer(params, params.layer)
                 q.rank, q.nranks = 0, m
                 if self.dev.layers_per_pass(q, nl) == nl:

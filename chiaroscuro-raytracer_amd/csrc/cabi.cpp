@@ -802,6 +802,11 @@ int cr_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float 
 // cr_render over nlayers layers in pass groups: up to LAYER_GROUP layers per pass, the frame cut
 // into the fewest tile-split pieces whose paths fit one chunk (DistributedFrame.plan_layers)
 static const uint32_t LAYER_GROUP = 16, MAX_PIECES = 64;
+// frame pieces pay on scenes with real geometry (sponza stand-in 353 -> 324 ms per layer, 4K 1122 ->
+// 987, nanobox stand-in 1922 -> 2173 Mray/s) and lose on a handful of triangles (cornell_box, 36:
+// 147.6 -> 153.8 ms per layer), whose queues gain no coherence from denser passes
+static const uint32_t PIECES_MIN_TRIS = 1024;
+uint32_t cr_scene_triangles(cr_ctx *c) { return c && c->has_scene ? c->n_tris : 0u; }
 int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
                      float *accum_rgb_out) {
     if (!c) return CR_E_INVALID;
@@ -830,7 +835,8 @@ int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p,
         // the largest group that fits with at most MAX_PIECES pieces, the fewest pieces for it
         uint32_t nl = 1, m = 1;
         for (uint32_t want = std::min(LAYER_GROUP, nlayers - done); want > 1 && nl == 1; want--)
-            for (uint32_t pieces = 1; pieces <= std::min(MAX_PIECES, tiles); pieces++) {
+            for (uint32_t pieces = 1; pieces <= (c->n_tris < PIECES_MIN_TRIS ? 1u : std::min(MAX_PIECES, tiles));
+                 pieces++) {
                 cr_render_params t = q;
                 t.rank = 0;
                 t.nranks = pieces;

@@ -233,6 +233,9 @@ int cr_render_tiles_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_re
  * cr_render calls.  Counters, cr_last_kernel_ms and the trace stats sum over the passes. */
 int cr_render_layers(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
                      float *accum_rgb_out);
+/* Triangles of the uploaded scene (0: none).  Frame pieces are used for scenes of at least 1024
+ * triangles only: on a handful of triangles denser passes gain no coherence. */
+uint32_t cr_scene_triangles(cr_ctx *ctx);
 /* Pixel origin of rank's local tile `local` (slot rank + local * nranks of the frame's
  * row-major tile slots; with nranks > 1 each tile row is rotated by its index, so a
  * rank's tiles spread over every column class). */
