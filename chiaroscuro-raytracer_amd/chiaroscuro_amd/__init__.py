@@ -183,7 +183,7 @@ HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "c
                "cr_group_upload_scene", "cr_group_set_option", "cr_group_render", "cr_group_get_counters",
                "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap", "cr_set_accumulator",
                "cr_group_set_accumulator", "cr_layers_per_pass", "cr_render_layers_device",
-               "cr_render_tiles_layers_device", "cr_render_layers", "cr_scene_triangles")
+               "cr_render_tiles_layers_device", "cr_render_layers", "cr_scene_triangles", "cr_layers_per_group")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
                 "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
@@ -240,6 +240,7 @@ def libs():
     _sig(hip, "cr_layers_per_pass", C.c_uint32, [P, C.POINTER(CrRenderParams), C.c_uint32])
     _sig(hip, "cr_render_layers", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P])
     _sig(hip, "cr_scene_triangles", C.c_uint32, [P])
+    _sig(hip, "cr_layers_per_group", C.c_uint32, [P, C.POINTER(CrRenderParams), C.c_uint32])
     _sig(hip, "cr_render_layers_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P, P])
     _sig(hip, "cr_render_tiles_layers_device", C.c_int,
          [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P, P])
@@ -525,6 +526,10 @@ class Device:
     def render_tiles_device(self, cam, p, d_tiles_ptr: int, stream: int = 0):
         self._chk(libs()[0].cr_render_tiles_device(self._c, C.byref(cam), C.byref(p), C.c_void_p(d_tiles_ptr),
                                                    C.c_void_p(stream)), "cr_render_tiles_device")
+
+    def layers_per_group(self, p, want: int) -> int:
+        """How many of `want` layers one pass group renders for p's share (in pieces)."""
+        return int(libs()[0].cr_layers_per_group(self._c, C.byref(p), want))
 
     def scene_triangles(self) -> int:
         return int(libs()[0].cr_scene_triangles(self._c))

@@ -142,7 +142,9 @@ class DistributedFrame:
         want = max(1, int(want))
         if not hasattr(self.dev, "layers_per_pass") or (L.nranks > 1 and self.gather == "cabi"):
             return 1, 1
-        if L.nranks > 1:
+        if L.nranks > 1:  # (cr_render_tiles_layers_device cuts the rank's tiles into pieces itself)
+            if hasattr(self.dev, "layers_per_group"):
+                return self.dev.layers_per_group(params, want), 1
             return self.dev.layers_per_pass(params, want), 1
         # frame pieces only for scenes with real geometry (cr_scene_triangles; cabi.cpp PIECES_MIN_TRIS)
         max_pieces = min(64, L.ntiles)

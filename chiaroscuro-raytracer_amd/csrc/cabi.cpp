@@ -95,6 +95,8 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.layer = p->layer;
     A.nl = 1;
     A.layer_stride = 0;
+    A.piece_k = 0;
+    A.piece_m = 1;
     A.rank = p->rank;
     A.nranks = p->nranks;
     A.tile = tile_of(p);
@@ -163,7 +165,7 @@ uint64_t wf_path_cap(cr_ctx *c, int k) {
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st,
-               uint32_t nl) {
+               uint32_t nl, uint32_t piece_k, uint32_t piece_m, uint64_t stride) {
     if (!cam || !out) return fail(c, CR_E_INVALID, "null camera/output");
     int rc = check_params(c, p);
     if (rc) return rc;
@@ -177,6 +179,12 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     if (spp_pass >= (1ull << 31)) return fail(c, CR_E_INVALID, "layers x spp too large");
     A.nl = nl;
     A.layer_stride = (uint64_t)cr_tiles_for_rank(p, 0) * A.tile * A.tile * 3;
+    if (piece_m > 1) {
+        if (mode != cr::MODE_TILES || piece_k >= piece_m || !stride) return fail(c, CR_E_INVALID, "bad piece");
+        A.piece_k = piece_k;
+        A.piece_m = piece_m;
+        A.layer_stride = stride;
+    }
     if (c->kernel == 2 && !c->full_counters && !cr::wf_variant_available(A.variant))
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
                                          " is not compiled in (make ALL_VARIANTS=1)");
@@ -799,6 +807,30 @@ int cr_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float 
     return CR_OK;
 }
 
+// the counters, pass time and trace stats of several passes, summed (pass groups)
+struct PassSum {
+    uint64_t ctr[sizeof(cr_counters) / sizeof(uint64_t)] = {};
+    float ms = 0.f;
+    cr_trace_stats ts{};
+    void add(const cr_ctx *c) {
+        const uint64_t *h = (const uint64_t *)&c->last;
+        for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) ctr[i] += h[i];
+        ms += c->last_ms;
+        for (int kind = 0; kind < 4; kind++) {
+            ts.launches[kind] += c->last_trace.launches[kind];
+            ts.ms[kind] += c->last_trace.ms[kind];
+            ts.inner[kind] += c->last_trace.inner[kind];
+            ts.leaf[kind] += c->last_trace.leaf[kind];
+            ts.tritest[kind] += c->last_trace.tritest[kind];
+        }
+    }
+    void store(cr_ctx *c) const {
+        std::memcpy(&c->last, ctr, sizeof(cr_counters));
+        c->last_ms = ms;
+        c->last_trace = ts;
+    }
+};
+
 // cr_render over nlayers layers in pass groups: up to LAYER_GROUP layers per pass, the frame cut
 // into the fewest tile-split pieces whose paths fit one chunk (DistributedFrame.plan_layers)
 static const uint32_t LAYER_GROUP = 16, MAX_PIECES = 64;
@@ -807,6 +839,33 @@ static const uint32_t LAYER_GROUP = 16, MAX_PIECES = 64;
 // 147.6 -> 153.8 ms per layer), whose queues gain no coherence from denser passes
 static const uint32_t PIECES_MIN_TRIS = 1024;
 uint32_t cr_scene_triangles(cr_ctx *c) { return c && c->has_scene ? c->n_tris : 0u; }
+// The largest nl <= want (>= 1) whose paths fit one chunk when p's share is cut into *m pieces (the
+// fewest; scenes of at least PIECES_MIN_TRIS triangles only): for the whole frame (nranks 1) the
+// ranks of an m-way split, for rank r of N the ranks r + kN of an N * m split
+static uint32_t group_plan(cr_ctx *c, const cr_render_params *p, uint32_t want, uint32_t *m_out) {
+    *m_out = 1;
+    const uint32_t N = p->nranks ? p->nranks : 1;
+    const uint32_t share = cr_tiles_for_rank(p, p->rank);
+    const uint32_t maxm = c->n_tris < PIECES_MIN_TRIS ? 1u : std::min(MAX_PIECES, std::max(share, 1u));
+    for (uint32_t nl = std::max(want, 1u); nl > 1; nl--)
+        for (uint32_t m = 1; m <= maxm; m++) {
+            cr_render_params t = *p;
+            t.nranks = N * m;
+            t.rank = N == 1 ? 0 : p->rank; // the largest piece
+            if (cr_layers_per_pass(c, &t, nl) == nl) {
+                *m_out = m;
+                return nl;
+            }
+        }
+    return 1;
+}
+
+uint32_t cr_layers_per_group(cr_ctx *c, const cr_render_params *p, uint32_t want) {
+    if (!c || c->device < 0 || !c->has_scene || !p || want < 1 || check_params(c, p) != CR_OK) return 1;
+    uint32_t m = 1;
+    return group_plan(c, p, want, &m);
+}
+
 int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
                      float *accum_rgb_out) {
     if (!c) return CR_E_INVALID;
@@ -827,47 +886,21 @@ int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p,
         c->accum_elems = elems;
         HIPCHK(hipMemset(c->d_accum, 0, elems * sizeof(float)));
     }
-    const uint32_t tiles = cr_tiles_for_rank(&q, 0);
-    uint64_t sum[sizeof(cr_counters) / sizeof(uint64_t)] = {};
-    float ms = 0.f;
-    cr_trace_stats ts{};
+    PassSum sum;
     for (uint32_t done = 0; done < nlayers;) {
-        // the largest group that fits with at most MAX_PIECES pieces, the fewest pieces for it
-        uint32_t nl = 1, m = 1;
-        for (uint32_t want = std::min(LAYER_GROUP, nlayers - done); want > 1 && nl == 1; want--)
-            for (uint32_t pieces = 1; pieces <= (c->n_tris < PIECES_MIN_TRIS ? 1u : std::min(MAX_PIECES, tiles));
-                 pieces++) {
-                cr_render_params t = q;
-                t.rank = 0;
-                t.nranks = pieces;
-                if (cr_layers_per_pass(c, &t, want) == want) {
-                    nl = want;
-                    m = pieces;
-                    break;
-                }
-            }
+        uint32_t m = 1;
+        const uint32_t nl = group_plan(c, &q, std::min(LAYER_GROUP, nlayers - done), &m);
         for (uint32_t k = 0; k < m; k++) {
             cr_render_params t = q;
             t.layer = q.layer + done;
             t.rank = k;
             t.nranks = m;
             if ((rc = run_render(c, cam, &t, c->d_accum, cr::MODE_BLEND, c->stream, nl))) return rc;
-            const uint64_t *h = (const uint64_t *)&c->last;
-            for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) sum[i] += h[i];
-            ms += c->last_ms;
-            for (int kind = 0; kind < 4; kind++) {
-                ts.launches[kind] += c->last_trace.launches[kind];
-                ts.ms[kind] += c->last_trace.ms[kind];
-                ts.inner[kind] += c->last_trace.inner[kind];
-                ts.leaf[kind] += c->last_trace.leaf[kind];
-                ts.tritest[kind] += c->last_trace.tritest[kind];
-            }
+            sum.add(c);
         }
         done += nl;
     }
-    std::memcpy(&c->last, sum, sizeof(cr_counters));
-    c->last_ms = ms;
-    c->last_trace = ts;
+    sum.store(c);
     HIPCHK(hipMemcpy(accum_rgb_out, c->d_accum, elems * sizeof(float), hipMemcpyDeviceToHost));
     return CR_OK;
 }
@@ -927,7 +960,26 @@ int cr_render_tiles_layers_device(cr_ctx *c, const cr_camera *cam, const cr_rend
                                   float *d_tiles, void *stream) {
     if (!c) return CR_E_INVALID;
     if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
-    return run_render(c, cam, p, d_tiles, cr::MODE_TILES, (hipStream_t)stream, nlayers);
+    if (!p || p->nranks <= 1 || nlayers <= 1 || cr_layers_per_pass(c, p, nlayers) == nlayers)
+        return run_render(c, cam, p, d_tiles, cr::MODE_TILES, (hipStream_t)stream, nlayers);
+    // the rank's tiles in pieces (ranks r + kN of an N * m split: every tile slot keeps its pixels
+    // for any split of more than one rank), each written into the rank's compact buffer
+    uint32_t m = 1;
+    if (group_plan(c, p, nlayers, &m) != nlayers)
+        return fail(c, CR_E_INVALID, "layers per pass: the rank's share does not fit in pieces");
+    const uint64_t stride = (uint64_t)cr_tiles_for_rank(p, 0) * tile_of(p) * tile_of(p) * 3;
+    PassSum sum;
+    for (uint32_t k = 0; k < m; k++) {
+        cr_render_params t = *p;
+        t.rank = p->rank + k * p->nranks;
+        t.nranks = p->nranks * m;
+        if (cr_tiles_for_rank(&t, t.rank) == 0) continue;
+        if (int rc = run_render(c, cam, &t, d_tiles, cr::MODE_TILES, (hipStream_t)stream, nlayers, k, m, stride))
+            return rc;
+        sum.add(c);
+    }
+    sum.store(c);
+    return CR_OK;
 }
 
 int cr_blend_tiles_device(cr_ctx *c, const cr_render_params *p, const float *d_gathered, float *d_frame,

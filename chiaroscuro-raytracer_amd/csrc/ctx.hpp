@@ -140,8 +140,10 @@ int grow(cr_ctx *c, void **buf, size_t &cap, size_t need);
 // into out) or of the whole frame blended into out (MODE_BLEND), on stream st;
 // returns after the pass, counters and trace stats are read back
 // nl > 1 (wavefront kernel): layers p->layer .. p->layer + nl - 1 in one pass (cr_render_layers_device)
+// piece_m > 1 (MODE_TILES): p is piece piece_k of a rank's tiles (rank r + piece_k * N of an
+// N * piece_m split), written into the rank's compact buffer of layer stride `stride` floats
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st,
-               uint32_t nl = 1);
+               uint32_t nl = 1, uint32_t piece_k = 0, uint32_t piece_m = 1, uint64_t stride = 0);
 // group.cpp: the communicator and buffers of the multi-process split (cr_destroy)
 void release_dist(cr_ctx *c);
 } // namespace crx

@@ -121,6 +121,10 @@ struct RenderArgs {
     // layer j's tile means at out + j * layer_stride floats
     uint32_t nl;
     uint64_t layer_stride;
+    // MODE_TILES of one piece of a rank's tiles (cr_render_tiles_layers_device): this launch renders
+    // rank r + piece_k * N of an N * piece_m split, whose local tile j is the rank's local tile
+    // piece_k + j * piece_m (tile slots keep their pixels for any split of more than one rank)
+    uint32_t piece_k, piece_m;
     uint32_t rank, nranks, tile, tiles_x;
     uint32_t n_items;     // my_tiles * tile * tile
     uint32_t stack_depth;

@@ -177,7 +177,12 @@ __device__ __forceinline__ void write_pixel(const RenderArgs &A, uint32_t x, uin
     const uint32_t layer = A.layer + lj;
     if (A.mode == MODE_TILES) {
         const f3 m = muls(temp, inv);
-        float *o = A.out + (size_t)lj * A.layer_stride + 3 * (size_t)item;
+        size_t slot = item;
+        if (A.piece_m > 1) {
+            const uint32_t TT = A.tile * A.tile, lt = item / TT;
+            slot = (size_t)(A.piece_k + lt * A.piece_m) * TT + (item - lt * TT);
+        }
+        float *o = A.out + (size_t)lj * A.layer_stride + 3 * slot;
         o[0] = m.x;
         o[1] = m.y;
         o[2] = m.z;

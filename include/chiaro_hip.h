@@ -219,9 +219,10 @@ uint32_t cr_tiles_for_rank(const cr_render_params *p, uint32_t rank);
  * what a rank's small share of the frame needs when the frame is split over GPUs.
  * cr_layers_per_pass: how many of `want` layers fit one path chunk and one sample buffer (1 when
  * the kernel, lanes or counting build do not allow more); a larger nlayers is refused
- * (CR_E_INVALID).  cr_render_layers_device blends the layers in order into d_frame;
+ * (CR_E_INVALID) by cr_render_layers_device, which blends the layers in order into d_frame;
  * cr_render_tiles_layers_device writes layer j's batch means at
- * d_tiles + j * cr_tiles_for_rank(p, 0) * tile * tile * 3 floats. */
+ * d_tiles + j * cr_tiles_for_rank(p, 0) * tile * tile * 3 floats, and with nranks > 1 takes up to
+ * cr_layers_per_group layers (the rank's tiles in pieces). */
 uint32_t cr_layers_per_pass(cr_ctx *ctx, const cr_render_params *p, uint32_t want);
 int cr_render_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
                             float *d_frame, void *stream);
@@ -233,6 +234,12 @@ int cr_render_tiles_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_re
  * cr_render calls.  Counters, cr_last_kernel_ms and the trace stats sum over the passes. */
 int cr_render_layers(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
                      float *accum_rgb_out);
+/* How many of `want` layers (from p->layer) one pass group can render for p's share of the frame
+ * (the whole frame with nranks 1, else rank p->rank's tiles), cutting the share into up to 64
+ * pieces whose paths fit one chunk each: cr_render_layers plans the same for the frame, and
+ * cr_render_tiles_layers_device renders that many layers of a rank's tiles in pieces (the ranks
+ * r + kN of an N * m split; every tile slot keeps its pixels for any split of more than one rank). */
+uint32_t cr_layers_per_group(cr_ctx *ctx, const cr_render_params *p, uint32_t want);
 /* Triangles of the uploaded scene (0: none).  Frame pieces are used for scenes of at least 1024
  * triangles only: on a handful of triangles denser passes gain no coherence. */
 uint32_t cr_scene_triangles(cr_ctx *ctx);

@@ -58,7 +58,7 @@ def main():
                     st = fr.last_stats()
                     ms, c = st["kernel_ms"], st["counters"]
                 else:
-                    nl, pieces = dev.layers_per_pass(p, args.layers), 1
+                    nl, pieces = dev.layers_per_group(p, args.layers), 1  # (pieces inside the library)
                     tiles = torch.zeros((nl, ca.Device.tiles_for_rank(p, 0), args.tile, args.tile, 3),
                                         dtype=torch.float32, device="cuda")
                     dev.render_tiles_layers_device(cam, p, nl, tiles.data_ptr())

@@ -869,3 +869,39 @@ def test_render_layers_c_abi_groups_bitexact(ca, sponza):
         rays += oc["closest"] + oc["shadow"]
     assert_bitwise(g, o, "20 layers in pass groups")
     assert c["closest"] + c["shadow"] == rays and c["pixels"] == 20 * x * y
+
+
+def test_rank_pieces_tiles_layers_bitexact(ca, sponza):
+    """cr_render_tiles_layers_device with more layers than one chunk holds for a rank's tiles:
+    the rank's share is cut into pieces (ranks r + kN of an N * m split, each written into the
+    rank's compact buffer); every layer's tile means equal render_tiles_device of that layer
+    alone, for both ranks of a 2-way split (tile 16, ragged edges)."""
+    import torch
+    x, y, s, tile, nr, nl = 96, 54, 3, 16, 2, 6
+    dev = sponza.dev
+    cam = sponza.camera(ca, x, y)
+    dev.set_option("kernel", 2)
+    dev.set_option("counters", 0)
+    dev.set_option("wf_paths", 20000)  # a rank's 12 tiles x 6 layers are 55296 paths: 3 pieces
+    try:
+        for r in range(nr):
+            q = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=4, rank=r, nranks=nr, tile=tile)
+            assert dev.layers_per_pass(q, nl) < nl and dev.layers_per_group(q, nl) == nl
+            mt = ca.Device.tiles_for_rank(q, 0)
+            allt = torch.full((nl, mt, tile, tile, 3), -1.0, dtype=torch.float32, device="cuda")
+            dev.render_tiles_layers_device(cam, q, nl, allt.data_ptr())
+            c = dev.counters()
+            rays = 0
+            for j in range(nl):
+                one = torch.full((mt, tile, tile, 3), -1.0, dtype=torch.float32, device="cuda")
+                dev.render_tiles_device(cam, ca.render_params(x, y, s, 6, 0xC41A05C0, layer=4 + j, rank=r, nranks=nr,
+                                                              tile=tile), one.data_ptr())
+                torch.cuda.synchronize()
+                oc = dev.counters()
+                rays += oc["closest"] + oc["shadow"]
+                assert_bitwise(allt[j].cpu().numpy(), one.cpu().numpy(), "rank %d layer %d, pieces" % (r, 4 + j))
+            assert c["closest"] + c["shadow"] == rays
+    finally:
+        dev.set_option("wf_paths", 256 << 20)
+        dev.set_option("counters", 1)
+        torch.cuda.synchronize()
