@@ -261,7 +261,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-perf-pass", action="store_true",
                     help="skip the untimed performed-work pass (profiling runs: its kernels are not the timed ones)")
-    ap.add_argument("--layers-per-pass", type=int, default=16,
+    ap.add_argument("--layers-per-pass", type=int, default=32,
                     help="progressive layers per render pass group (DistributedFrame.plan_layers; 1 = one per pass)")
     ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")

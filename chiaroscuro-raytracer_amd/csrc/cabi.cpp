@@ -833,7 +833,7 @@ struct PassSum {
 
 // cr_render over nlayers layers in pass groups: up to LAYER_GROUP layers per pass, the frame cut
 // into the fewest tile-split pieces whose paths fit one chunk (DistributedFrame.plan_layers)
-static const uint32_t LAYER_GROUP = 16, MAX_PIECES = 64;
+static const uint32_t LAYER_GROUP = 32, MAX_PIECES = 64;
 // frame pieces pay on scenes with real geometry (sponza stand-in 353 -> 324 ms per layer, 4K 1122 ->
 // 987, nanobox stand-in 1922 -> 2173 Mray/s) and lose on a handful of triangles (cornell_box, 36:
 // 147.6 -> 153.8 ms per layer), whose queues gain no coherence from denser passes

@@ -229,7 +229,7 @@ int cr_render_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_p
 int cr_render_tiles_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
                                   float *d_tiles, void *stream);
 /* cr_render of layers p->layer .. + nlayers - 1 of the whole frame (p->nranks 1) in pass groups:
- * up to 16 layers per pass, the frame cut into the fewest tile-split pieces (the ranks of a
+ * up to 32 layers per pass, the frame cut into the fewest tile-split pieces (the ranks of a
  * pieces-way split, each blended in place) whose paths fit one chunk; bit-identical to nlayers
  * cr_render calls.  Counters, cr_last_kernel_ms and the trace stats sum over the passes. */
 int cr_render_layers(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,

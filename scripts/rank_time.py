@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE", help="cr_set_option (experiments)")
     ap.add_argument("--tile", type=int, default=32, help="tile edge of the split (bench.py: 32)")
-    ap.add_argument("--layers", type=int, default=16, help="layers per pass group (bench.py --layers-per-pass)")
+    ap.add_argument("--layers", type=int, default=32, help="layers per pass group (bench.py --layers-per-pass)")
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
