@@ -74,18 +74,24 @@ def cpu_threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(pair_tris, textures, info, leaf, cam, xres, yres, spp, k, seed, budget_s):
+def oracle_scene(model, leaf):
+    """The oracle's scene (oracle/liboracle.so, test infrastructure) over the same triangle
+    soup: the CPU baseline's timed restatement and the checker of the timed frame."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle as po
+
+    t0 = time.time()
+    osc = po.OracleScene(model.triangles(), leaf_size=leaf, textures=model.textures(), build_threads=cpu_threads())
+    log("oracle: kd build %.1fs" % (time.time() - t0))
+    return osc
+
+
+def cpu_baseline(osc, cam, xres, yres, spp, k, seed, budget_s):
     """Oracle restatement on a row sample of the same frame: OpenMP over the sampled
     rows with the reference's static schedule (src/rayTracer.cpp:55), with all
     threads of this process's CPU share and with 1 thread, on the SAME sample (every
     ystep-th row x sample_spp), so the two legs and their ratio are comparable."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import pyoracle as po
-
     threads = cpu_threads()
-    t0 = time.time()
-    osc = po.OracleScene(pair_tris, leaf_size=leaf, textures=textures, build_threads=threads)
-    log("cpu_baseline: oracle kd build %.1fs" % (time.time() - t0))
     # calibrate with 1 thread on every 16th row at 1 spp, then size the sample so the
     # 1-thread leg takes ~0.7 of the budget (the all-thread leg then takes ~1/threads of it)
     step = min(16, yres)
@@ -118,6 +124,44 @@ def cpu_baseline(pair_tris, textures, info, leaf, cam, xres, yres, spp, k, seed,
             "sample": "oracle/liboracle.so (OpenMP over rows, static schedule as src/rayTracer.cpp:55) on the "
                       "same frame / seed, the same sample for both legs: %s; %d threads %.2f s (median of 3), "
                       "1 thread %.1f s" % (sample, threads, dtn, dt1)}
+
+
+def parity_rows(yres, nrows):
+    """nrows rows spread evenly over the frame, the first and the last included."""
+    if nrows <= 1:
+        return [yres // 2]
+    return sorted({int(round(i * (yres - 1) / (nrows - 1))) for i in range(nrows)})
+
+
+def frame_parity(osc, frame_rows, rows, cam, xres, yres, spp, k, seed, nlayers):
+    """The timed frame against the oracle, bit for bit, on whole rows at the full spp.
+
+    frame_rows [len(rows)][xres][3]: those rows of the accumulated frame after layers
+    1..nlayers (warmup and timed groups, rendered by the lean default trace build in its
+    pass groups / frame pieces / tile split).  The oracle renders every layer's batch mean of
+    the same pixels (or_render_pixels: sendRay per sample in sample order, x 1/spp) and blends
+    them in layer order exactly as src/rayTracer.cpp:64 does, in fp32:
+        pixels = (pixels * (L - 1) + mean) / L."""
+    import numpy as np
+    px = np.tile(np.arange(xres, dtype=np.uint32), len(rows))
+    py = np.repeat(np.asarray(rows, np.uint32), xres)
+    acc = np.zeros((len(px), 3), np.float32)
+    t0 = time.time()
+    rays = 0
+    for L in range(1, nlayers + 1):
+        mean, c = osc.render_pixels(cam, xres, yres, spp, k, seed, px, py, layer=L, threads=cpu_threads())
+        acc = (acc * np.float32(L - 1) + mean) / np.float32(L)
+        rays += c["closest"] + c["shadow"]
+    g = np.ascontiguousarray(frame_rows, np.float32).reshape(-1, 3)
+    diff = g.view(np.uint32) != acc.view(np.uint32)
+    ad = np.abs(g.astype(np.float64) - acc.astype(np.float64))
+    rel = ad / np.maximum(np.abs(acc.astype(np.float64)), 1e-30)
+    rmse = float(np.sqrt(np.mean(ad ** 2)) / max(float(np.mean(np.abs(acc))), 1e-30))
+    return {"rows": [int(r) for r in rows], "layers": nlayers, "spp": spp, "values": int(diff.size),
+            "differing": int(diff.sum()), "max_rel": float(rel[diff].max()) if diff.any() else 0.0,
+            "rel_rmse": rmse, "oracle_rays": int(rays), "oracle_s": round(time.time() - t0, 2),
+            "what": "rows of the timed frame (layers 1..%d blended) vs oracle/liboracle.so at the same seed, "
+                    "bit for bit (uint32 compare of every fp32 value)" % nlayers}
 
 
 def issue_roofline(dom, iss, views, issue, pass_view, kind):
@@ -265,6 +309,9 @@ def main():
                     help="progressive layers per render pass group (DistributedFrame.plan_layers; 1 = one per pass)")
     ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")
+    ap.add_argument("--parity-rows", type=int, default=8,
+                    help="rank 0 checks this many rows of the timed frame (every layer, full spp) bit for bit "
+                         "against the oracle after the timed region (0: skip)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
@@ -386,6 +433,11 @@ def run_rank(args, world, backend):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timed_build = dev.last_trace_build() if hasattr(dev, "last_trace_build") else None
+    nlayers_done = layer - 1  # the frame holds layers 1 .. nlayers_done (warmup and timed groups)
+    # rows of the timed frame for the parity check (rank 0; the oracle runs after the collectives)
+    prows = parity_rows(yres, args.parity_rows) if args.parity_rows > 0 else []
+    frame_rows = fr.frame[prows].cpu().numpy() if (prows and fr.frame is not None) else None
     if args.save_frame and fr.frame is not None:
         import numpy as np
         np.save(args.save_frame, fr.frame.cpu().numpy())
@@ -449,10 +501,17 @@ def run_rank(args, world, backend):
         kernel_name = {0: "persistent megakernel", 1: "thread per pixel", 2: "wavefront"}[
             args.kernel if args.kernel >= 0 else 2]
         cpu = None
+        parity = None
+        osc = None
+        if frame_rows is not None or (not args.no_cpu_baseline and world == 1):
+            osc = oracle_scene(model, info["leaf_size"])
+        if frame_rows is not None:
+            parity = frame_parity(osc, frame_rows, prows, cam.as_array(), xres, yres, spp, k, seed, nlayers_done)
+            parity["trace_build"] = timed_build
+            log("parity: %d of %d values differ over rows %s x %d layers (oracle %.1fs)" % (
+                parity["differing"], parity["values"], parity["rows"], nlayers_done, parity["oracle_s"]))
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(model.triangles(), model.textures(), info, info["leaf_size"], cam.as_array(), xres,
-                               yres, spp, k, seed,
-                               args.cpu_budget)
+            cpu = cpu_baseline(osc, cam.as_array(), xres, yres, spp, k, seed, args.cpu_budget)
         # the pass: its measured fabric (HBM) bytes over its time is north_star's "rocprof HBM GB/s";
         # the SURVEY §8d bytes of the reference algorithm's work over the same time are a
         # reference-equivalent rate (the culls skip most of that work), not a performed one
@@ -565,10 +624,11 @@ def run_rank(args, world, backend):
                        "parallelism": "tile-split x%d" % world, "gather": args.gather if world > 1 else None,
                        "rays": int(rays_all),
                        "rank_render_ms": rank_render_ms, "layers_per_pass": nl_pass,
-                       "pass_groups": [list(g) for g in groups],
+                       "pass_groups": [list(g) for g in groups], "trace_build": timed_build,
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         if backend.name != "gpu":
             out["backend"] = backend.name

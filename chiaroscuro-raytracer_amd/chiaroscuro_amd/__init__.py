@@ -176,7 +176,7 @@ _host = None
 # Every symbol declared in include/chiaro_hip.h and include/chiaroscuro.h.
 HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "cr_render", "cr_render_device",
                "cr_render_tiles_device", "cr_blend_tiles_device", "cr_tiles_for_rank", "cr_tile_origin", "cr_intersect",
-               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize", "cr_get_diag", "cr_get_perf", "cr_trace_build_available",
+               "cr_intersect_shadow", "cr_get_counters", "cr_last_kernel_ms", "cr_get_trace_stats", "cr_set_option", "cr_synchronize", "cr_get_diag", "cr_get_perf", "cr_trace_build_available", "cr_last_trace_build",
                "cr_tonemap_setup", "cr_tonemap_device", "cr_tonemap",
                "cr_comm_unique_id", "cr_comm_init", "cr_comm_destroy", "cr_render_dist_device",
                "cr_device_count", "cr_group_create", "cr_group_destroy", "cr_group_last_error", "cr_group_size", "cr_group_ok",
@@ -257,6 +257,7 @@ def libs():
     _sig(hip, "cr_get_diag", C.c_int, [P, C.POINTER(C.c_uint64), C.c_int])
     _sig(hip, "cr_get_perf", C.c_int, [P, C.POINTER(C.c_uint64), C.c_int])
     _sig(hip, "cr_trace_build_available", C.c_int, [C.c_int])
+    _sig(hip, "cr_last_trace_build", C.c_int, [P])
     _sig(hip, "cr_synchronize", C.c_int, [P])
     _sig(hip, "cr_tonemap_setup", None, [C.c_float] * 5 + [C.POINTER(CrTonemapParams)])
     _sig(hip, "cr_tonemap_device", C.c_int, [P, C.POINTER(CrTonemapParams), C.c_uint32, C.c_uint32, P, P, P])
@@ -629,6 +630,10 @@ class Device:
 
     def set_option(self, key: str, value: int):
         self._chk(libs()[0].cr_set_option(self._c, key.encode(), int(value)), "cr_set_option")
+
+    def last_trace_build(self) -> int:
+        """cr_last_trace_build: the trace build of the last render (-1 counting build, -2 not wavefront)."""
+        return int(libs()[0].cr_last_trace_build(self._c))
 
     @staticmethod
     def trace_builds(upto: int = 64) -> list:

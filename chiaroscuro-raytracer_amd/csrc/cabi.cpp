@@ -191,6 +191,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     if (c->perf_counters && (c->kernel != 2 || c->full_counters || !cr::wf_perf_available(A.variant)))
         return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18 and 26 only, "
                                      "without the counting build");
+    c->last_build = c->kernel == 2 ? (c->full_counters ? -1 : A.variant) : -2;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     if (c->kernel == 0 || c->kernel == 2) {
         const bool wf = c->kernel == 2;
@@ -1135,6 +1136,7 @@ int cr_get_trace_stats(cr_ctx *c, cr_trace_stats *out) {
 }
 
 int cr_trace_build_available(int build) { return cr::wf_variant_available(build) ? 1 : 0; }
+int cr_last_trace_build(cr_ctx *c) { return c ? c->last_build : -2; }
 
 int cr_get_diag(cr_ctx *c, uint64_t *out, int n) {
     if (!c || !out || n < 0) return CR_E_INVALID;

@@ -28,6 +28,7 @@ struct cr_ctx {
     // be slow on a busy node) and again after they grow (wf_path_cap)
     uint64_t wf_mem_budget = 0;
     float last_ms = 0.f;
+    int last_build = -2; // cr_last_trace_build
     // scene
     bool has_scene = false;
     cr::DevScene S{};

@@ -297,6 +297,10 @@ int cr_get_perf(cr_ctx *ctx, uint64_t *out, int n);
  * the default compile holds 0, 15, 18 and 26 (the default); `make ALL_VARIANTS=1` every
  * measured build.  A render with a missing build returns CR_E_INVALID. */
 int cr_trace_build_available(int build);
+/* The wavefront trace build the last render on ctx ran (its "variant": the scene-size default 43 / 44
+ * unless set), -1 when it was the counting build ("counters" 1), -2 when it was not a wavefront render
+ * (or none has run).  Lets a caller name the kernels a result came from (bench.py, smoke()). */
+int cr_last_trace_build(cr_ctx *ctx);
 int cr_synchronize(cr_ctx *ctx);
 
 /* ---------------------------------------------------------- multi-GPU --

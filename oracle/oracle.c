@@ -794,7 +794,8 @@ void or_render_pixels(or_scene *s, const float cam[12], uint32_t xres, uint32_t 
 #pragma omp parallel num_threads(nth)
     {
         ctr_t ct; memset(&ct, 0, sizeof ct);
-#pragma omp for schedule(static)
+        /* (a checker, not the timed baseline: dynamic chunks balance pixels of uneven cost) */
+#pragma omp for schedule(dynamic, 16)
         for (int64_t i = 0; i < (int64_t)n; i++) {
             v3 temp = V3(0.f, 0.f, 0.f);
             for (uint32_t smp = 0; smp < spp; smp++) {

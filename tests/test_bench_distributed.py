@@ -56,6 +56,34 @@ def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
     assert line["config"]["rays"] == rays
     got = np.load(frame)
     assert got.shape == ref.shape and (got.view(np.uint32) == ref.view(np.uint32)).all() and got.mean() > 0
+    # the bench's own parity check of the timed frame: every row it sampled, every layer, bit for bit
+    par = line["parity"]
+    assert par["differing"] == 0 and par["layers"] == WARMUP + STEPS and par["spp"] == SPP
+    assert par["values"] == len(par["rows"]) * RES[0] * 3 and par["rows"][0] == 0 and par["rows"][-1] == RES[1] - 1
     # value: the rays of all ranks over the slowest rank's wall time (ms_per_step is that / steps)
     want = rays / (line["ms_per_step"] * STEPS / 1e3) / 1e6
     assert abs(line["value"] - want) <= 1e-3 * want + 2e-3
+
+
+def test_frame_parity_detects_one_flipped_bit(ca, po, scenes):
+    """bench.frame_parity compares the frame's rows with the oracle's layer blend bit for bit:
+    the oracle's own frame passes, and one flipped mantissa bit is reported."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    xres, yres, spp, layers = 24, 20, 2, 3
+    s = ca.Scene(scenes.config_rtc("cornell"), "xres", str(xres), "yres", str(yres))
+    i = s.info
+    m = ca.Model(s)
+    osc = bench.oracle_scene(m, i["leaf_size"])
+    cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], xres, yres).as_array()
+    ref = None
+    for L in range(1, layers + 1):
+        ref, _ = osc.render(cam, xres, yres, spp, i["k"], i["seed"], layer=L, pixels=ref)
+    rows = bench.parity_rows(yres, 4)
+    assert rows == [0, 6, 13, 19]
+    ok = bench.frame_parity(osc, ref[rows], rows, cam, xres, yres, spp, i["k"], i["seed"], layers)
+    assert ok["differing"] == 0 and ok["values"] == 4 * xres * 3 and ok["max_rel"] == 0.0
+    bad = ref[rows].copy()
+    bad.view(np.uint32)[2, 5, 1] ^= 1
+    r = bench.frame_parity(osc, bad, rows, cam, xres, yres, spp, i["k"], i["seed"], layers)
+    assert r["differing"] == 1 and r["max_rel"] > 0.0
