@@ -385,6 +385,10 @@ def run_rank(args, world, backend):
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
         tp = time.perf_counter()
         n, pieces = fr.plan_layers(p, n)
+        if dist:  # every rank runs the same group (its per-layer gathers pair up): the smallest plan
+            t = torch.tensor([n], dtype=torch.int64, device=backend.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            n = int(t.item())
         if rank == 0:
             log("group of %d layers in %d pieces (plan %.1f ms)" % (n, pieces, (time.perf_counter() - tp) * 1e3))
         if n == 1 and pieces == 1:

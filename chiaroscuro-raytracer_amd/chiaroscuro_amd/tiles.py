@@ -105,7 +105,9 @@ class DistributedFrame:
         """Continue from a checkpoint: rank 0 loads the frame, every rank gets the
         layer count (the next layer to render is that + 1).  `expect` is the
         Checkpoint of this run (layers ignored): another frame, sampling or scene is
-        refused, as RayTracer.resume refuses it."""
+        refused, as RayTracer.resume refuses it, and so is another camera -- eye, center
+        or yview (src/rayTracer.cpp:23-33 restarts the accumulation when they change;
+        `up` is not compared, as the reference's `lastUp == lastUp` never compares it)."""
         import torch
         layers = torch.zeros(1, dtype=torch.int64)
         err = ""
@@ -115,6 +117,9 @@ class DistributedFrame:
             keys = ("xres", "yres", "samples", "k", "seed", "scene")
             if any(getattr(h, k) != getattr(expect, k) for k in keys) or list(h.background) != list(expect.background):
                 err = "resume: the checkpoint is of another frame / sampling / scene"
+            elif (list(h.eye) != list(expect.eye) or list(h.center) != list(expect.center)
+                  or h.yview != expect.yview):
+                err = "resume: the checkpoint is of another camera (eye / center / yview)"
             else:
                 self.frame.copy_(torch.from_numpy(px).to(self.frame.device))
                 layers[0] = h.layers

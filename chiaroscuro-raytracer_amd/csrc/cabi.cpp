@@ -154,7 +154,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
 }
 
-// path slots one wavefront chunk may hold: ~45% of the free HBM (the grown buffers included)
+// path slots one wavefront chunk may hold: ~45% of the HBM that was free (plus the chunk buffers then
+// held) when the ctx first asked.  Queried once and kept: the plan of a pass group (cr_layers_per_group,
+// cr_layers_per_pass) must not change as this ctx's own buffers grow, or ranks that asked at different
+// moments would plan different groups and their per-layer gathers would not pair up
 uint64_t wf_path_cap(cr_ctx *c, int k) {
     if (!c->wf_mem_budget) {
         size_t freeb = 0, totalb = 0;
@@ -284,11 +287,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 const uint64_t pcap = std::min<uint64_t>(c->wf_paths, wf_path_cap(c, p->k) / (uint64_t)lanes);
                 if (P * 4 > pcap) need_alloc = std::max(need, need_for(std::max<uint64_t>(P, pcap), 32));
             }
-            const size_t had = c->wf_bytes + c->wf2_bytes;
             if (int r = grow(c, &c->d_wf, c->wf_bytes, need_alloc)) return r;
             if (lanes == 2)
                 if (int r = grow(c, &c->d_wf2, c->wf2_bytes, need_alloc)) return r;
-            if (c->wf_bytes + c->wf2_bytes != had) c->wf_mem_budget = 0; // re-query after a growth
             auto carve = [&](void *base, cr::WfArgs &W, int lane) {
                 char *b = (char *)base;
                 auto take = [&](size_t bytes) {

@@ -24,8 +24,7 @@ struct cr_ctx {
     uint32_t *hcnt = nullptr;
     void *d_wf2 = nullptr;
     size_t wf2_bytes = 0;
-    // HBM the path-chunk buffers may take: free + their current size, queried once (hipMemGetInfo can
-    // be slow on a busy node) and again after they grow (wf_path_cap)
+    // HBM the path-chunk buffers may take: free + their size at the first query, kept (wf_path_cap)
     uint64_t wf_mem_budget = 0;
     float last_ms = 0.f;
     int last_build = -2; // cr_last_trace_build

@@ -3,12 +3,16 @@
 
 #include "kdtree.hpp"
 
+#include <cerrno>
 #include <cstring>
 #include <fstream>
 #include <stdexcept>
 #include <vector>
 
 #include <zlib.h>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 namespace chiaro {
 
@@ -65,15 +69,38 @@ void checkpoint_write(const std::string &path, const chiaro_checkpoint &h, const
     put(b, h.scene);
     put(b, crc_of(pixels, n));
     // written next to the target and renamed over it: a crash leaves the old checkpoint whole
+    // (closed and flushed to the disk before the rename; a failed write removes the partial file)
     const std::string tmp = path + ".tmp";
-    {
-        std::ofstream o(tmp, std::ios::binary | std::ios::trunc);
-        if (!o) throw std::runtime_error("checkpoint: cannot write " + tmp);
-        o.write((const char *)b.data(), (std::streamsize)b.size());
-        o.write((const char *)pixels, (std::streamsize)(n * sizeof(float)));
-        if (!o) throw std::runtime_error("checkpoint: write failed: " + tmp);
+    const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) throw std::runtime_error("checkpoint: cannot write " + tmp);
+    auto write_all = [&](const void *data, size_t bytes) {
+        const char *q = (const char *)data;
+        while (bytes) {
+            const ssize_t w = ::write(fd, q, bytes);
+            if (w < 0 && errno == EINTR) continue;
+            if (w <= 0) return false;
+            q += w;
+            bytes -= (size_t)w;
+        }
+        return true;
+    };
+    const bool ok = write_all(b.data(), b.size()) && write_all(pixels, n * sizeof(float)) && ::fsync(fd) == 0;
+    if (::close(fd) != 0 || !ok) {
+        ::unlink(tmp.c_str());
+        throw std::runtime_error("checkpoint: write failed: " + tmp);
     }
-    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("checkpoint: cannot rename to " + path);
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) {
+        ::unlink(tmp.c_str());
+        throw std::runtime_error("checkpoint: cannot rename to " + path);
+    }
+    // the rename itself made durable: fsync the directory that holds the checkpoint
+    const size_t slash = path.find_last_of('/');
+    const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : path.substr(0, slash));
+    const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    if (dfd >= 0) {
+        ::fsync(dfd);
+        ::close(dfd);
+    }
 }
 
 void checkpoint_read(const std::string &path, chiaro_checkpoint &h, float *pixels) {

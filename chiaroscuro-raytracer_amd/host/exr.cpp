@@ -598,17 +598,23 @@ bool exr_decode_half(const unsigned char *f, size_t n, int &W, int &H, std::vect
                 k += 16;
             }
         } else if (name == "compression") {
+            if (size < 1) return err = "bad compression attribute", false;
             comp = f[at];
         } else if (name == "dataWindow") {
+            if (size < 16) return err = "bad dataWindow attribute", false;
             for (int i = 0; i < 4; i++) dw[i] = (int)rd32(at + 4 * i);
         } else if (name == "lineOrder") {
+            if (size < 1) return err = "bad lineOrder attribute", false;
             line_order = f[at];
         }
         at += size;
     }
-    W = dw[2] - dw[0] + 1;
-    H = dw[3] - dw[1] + 1;
-    if (W <= 0 || H <= 0) return err = "empty data window", false;
+    // (64-bit arithmetic: the window's corners are untrusted int32s)
+    const int64_t W64 = (int64_t)dw[2] - dw[0] + 1, H64 = (int64_t)dw[3] - dw[1] + 1;
+    if (W64 <= 0 || H64 <= 0) return err = "empty data window", false;
+    if (W64 > (1 << 16) || H64 > (1 << 16) || W64 * H64 > (int64_t)1 << 28) return err = "data window too large", false;
+    W = (int)W64;
+    H = (int)H64;
     if (comp != 0 && comp != 4) return err = "compression " + std::to_string(comp) + " not supported", false;
     (void)line_order; // chunks carry their own y
     int idx[3] = {-1, -1, -1};

@@ -140,14 +140,21 @@ void RayTracer::rayTraceLayers(unsigned n, vec3 eye, vec3 center, vec3 up, float
     p.rank = 0;
     p.nranks = 1;
     p.tile = 32;
+    // a failed render leaves the device accumulator holding an unknown number of this call's layers
+    // (cr_render_layers blends group after group): the next rayTrace then starts over at layer 1,
+    // whose blend weight (L - 1 = 0) discards whatever the accumulator holds
     if (group_) {
-        if (cr_group_render(group_, &cam, &p, pixels.data()) != CR_OK)
+        if (cr_group_render(group_, &cam, &p, pixels.data()) != CR_OK) {
+            layers_ = 0;
             throw std::runtime_error(std::string("chiaro: render failed: ") + cr_group_last_error(group_));
+        }
         cr_group_get_counters(group_, &counters_);
     } else {
         if ((n == 1 ? cr_render(ctx_, &cam, &p, pixels.data()) : cr_render_layers(ctx_, &cam, &p, n, pixels.data())) !=
-            CR_OK)
+            CR_OK) {
+            layers_ = 0;
             throw std::runtime_error(std::string("chiaro: render failed: ") + cr_last_error(ctx_));
+        }
         layers_ += n - 1; // layers p.layer .. p.layer + n - 1 are in the frame
         cr_get_counters(ctx_, &counters_);
     }

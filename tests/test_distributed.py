@@ -132,9 +132,51 @@ def _worker(rank, world, port, q):
                 ok = ok and bool((frame.view(np.uint32) == ref.view(np.uint32)).all()) and float(frame.mean()) > 0
             else:
                 ok = ok and fr.frame is None and fr.gathered is None
-        want = [("tiles", rank, L) for L in range(1, LAYERS + 1)]
+        # checkpoint / resume (DistributedFrame.save / resume): rank 0 writes the frame, a new frame
+        # resumes it on every rank, continues one layer equal to the oracle's; another camera or
+        # another sampling is refused on every rank
+        kd = ca.KDTree(m, sc)
+        hdr = ca.Checkpoint()
+        hdr.xres, hdr.yres, hdr.samples, hdr.k, hdr.seed, hdr.layers = XRES, YRES, SPP, info["k"], info["seed"], LAYERS
+        for name, v in (("eye", info["VP"]), ("center", info["LA"]), ("up", info["UP"]),
+                        ("background", info["background"])):
+            getattr(hdr, name)[:] = [float(x) for x in v]
+        hdr.yview = info["yview"]
+        hdr.scene = kd.fingerprint()
+        chk = Path(os.environ["CHIARO_TEST_TMP"]) / "frame.chk"
+        fr.save(chk, hdr)
+        dist.barrier()
+        fr2 = DistributedFrame(dev, XRES, YRES, rank, world, TILE, dist, device="cpu")
+        resumed = fr2.resume(chk, hdr)  # (collective: called on every rank, whatever `ok` says)
+        ok = ok and resumed == LAYERS
+        p = ca.render_params(XRES, YRES, SPP, info["k"], info["seed"], layer=LAYERS + 1, rank=rank, nranks=world,
+                             tile=TILE, background=info["background"])
+        fr2.render_layer(cam, p)
         if rank == 0:
-            want = [c for L in range(1, LAYERS + 1) for c in (("tiles", 0, L), ("blend", 0, L))]
+            ref, _ = osc.render(cam.as_array(), XRES, YRES, SPP, info["k"], info["seed"], layer=LAYERS + 1,
+                                bg=info["background"], pixels=ref, threads=1)
+            ok = ok and bool((fr2.frame.numpy().view(np.uint32) == ref.view(np.uint32)).all())
+        for field, val in (("eye", [0.0, 1.0, 3.0]), ("center", [0.0, 0.5, 0.0]), ("yview", 0.5), ("samples", 3)):
+            bad = ca.Checkpoint.from_buffer_copy(hdr)
+            if isinstance(val, list):
+                getattr(bad, field)[:] = val
+            else:
+                setattr(bad, field, val)
+            fr3 = DistributedFrame(dev, XRES, YRES, rank, world, TILE, dist, device="cpu")
+            try:
+                fr3.resume(chk, bad)
+                ok = False
+            except ValueError as e:
+                want_msg = "camera" if field != "samples" else "sampling"
+                ok = ok and (want_msg in str(e) if rank == 0 else "rank 0 refused" in str(e))
+        # `up` alone is not compared (the reference's lastUp quirk)
+        up = ca.Checkpoint.from_buffer_copy(hdr)
+        up.up[:] = [1.0, 0.0, 0.0]
+        resumed = DistributedFrame(dev, XRES, YRES, rank, world, TILE, dist, device="cpu").resume(chk, up)
+        ok = ok and resumed == LAYERS
+        want = [("tiles", rank, L) for L in range(1, LAYERS + 2)]
+        if rank == 0:
+            want = [c for L in range(1, LAYERS + 2) for c in (("tiles", 0, L), ("blend", 0, L))]
         ok = ok and dev.calls == want
         # a partition that disagrees with the process group is refused
         try:
@@ -170,8 +212,9 @@ def test_tile_layout_matches_cabi(ca):
     assert cols == set(range(8))
 
 
-def test_gloo_tile_gather_matches_single_process():
+def test_gloo_tile_gather_matches_single_process(tmp_path, monkeypatch):
     import torch.multiprocessing as mp
+    monkeypatch.setenv("CHIARO_TEST_TMP", str(tmp_path))
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

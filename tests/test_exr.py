@@ -100,3 +100,25 @@ def test_reference_renders_reencode_identically(ca, tmp_path):
         px = ca.exr_read_half(f)
         ca.exr_write_half(tmp_path / "x.exr", px)
         assert (tmp_path / "x.exr").read_bytes() == f.read_bytes(), f.name
+
+
+def test_malformed_headers_refused(ca, tmp_path):
+    """A dataWindow / compression attribute shorter than its type, or a window too large for
+    int arithmetic, is refused instead of read past the header (exr_decode_half)."""
+    px = np.arange(4 * 6 * 3, dtype=np.uint16).reshape(4, 6, 3)
+    ca.exr_write_half(tmp_path / "ok.exr", px)
+    good = (tmp_path / "ok.exr").read_bytes()
+    assert np.array_equal(ca.exr_read_half(tmp_path / "ok.exr"), px)
+    for name, typ in ((b"dataWindow", b"box2i"), (b"compression", b"compression")):
+        at = good.index(name + b"\0" + typ + b"\0") + len(name) + len(typ) + 2
+        raw = bytearray(good)
+        raw[at:at + 4] = (0).to_bytes(4, "little")  # declared size 0
+        (tmp_path / "bad.exr").write_bytes(bytes(raw))
+        with pytest.raises(RuntimeError):
+            ca.exr_read_half(tmp_path / "bad.exr")
+    at = good.index(b"dataWindow\0box2i\0") + len(b"dataWindow\0box2i\0") + 4
+    raw = bytearray(good)
+    raw[at:at + 16] = b"".join(v.to_bytes(4, "little", signed=True) for v in (-(2 ** 31), 0, 2 ** 31 - 1, 3))
+    (tmp_path / "huge.exr").write_bytes(bytes(raw))
+    with pytest.raises(RuntimeError):
+        ca.exr_read_half(tmp_path / "huge.exr")
