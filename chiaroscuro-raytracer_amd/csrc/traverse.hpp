@@ -84,17 +84,6 @@ __device__ __forceinline__ void pc_load(Pc *pc, bool scalar, uint32_t bytes) {
     if (!scalar) pc->vb += bytes;
     else if (wave_leader()) pc->sb += bytes;
 }
-// Per-wave LDS of the dealt shadow-leaf tests (trav_round's DEAL): owner lane per start position, the
-// start positions' mask, the accepted tests' mask (bit = worker rank).
-struct DealLds {
-    unsigned long long smask, rmask;
-    uint8_t tab[64];
-};
-__device__ __forceinline__ void wave_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
 // Call with the whole wave converged: the lane sums go to ctrs[0 .. PERF_N).
 __device__ __forceinline__ void pc_flush(unsigned long long *ctrs, const Pc &pc) {
     const unsigned long long v[PERF_N] = {pc.q,     pc.steps,   pc.leaves, pc.masks,  pc.tests,  pc.vb,
@@ -249,29 +238,6 @@ __device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_R
 }
 template <bool SC, int FORM = 0>
 __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
-    if (FORM == 3 && !(SC && wave_uniform(node))) {
-        // the packed record of a divergent leaf in two halves, one group each (12 instead of 24
-        // VGPRs at the peak): group 0 = float4 0..2, group 1 = 3..5, masks in the low bytes
-        const uint32_t all = count >= 32 ? 0xffffffffu : ((1u << count) - 1u);
-        if (!lc_unit(d.x, d.y, d.z) || count > (uint32_t)LC_MAXREFS_P) return all;
-        const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
-        const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
-        const float4 *p = (const float4 *)((const char *)S.lcullp + node * (uint32_t)(16 * LC_RECP));
-        const float4 a0 = p[0], a1 = p[1], a2 = p[2];
-        const uint32_t m0 = lc_lowbyte(a0.w) | lc_lowbyte(a1.w) << 8, m1lo = lc_lowbyte(a2.w);
-        uint32_t keep = 0u;
-        if (m0 && !lc_group_skip_fixed(ov, dv, inv, tmax, LcFloat4{a0.x, a0.y, a0.z, a0.w},
-                                       LcFloat4{a1.x, a1.y, a1.z, a1.w}, LcFloat4{a2.x, a2.y, a2.z, a2.w}))
-            keep = m0;
-        asm volatile("" ::: "memory"); // the second half's loads after the first half's test
-        const float4 a3 = p[3], a4 = p[4], a5 = p[5];
-        const uint32_t m1 = m1lo | lc_lowbyte(a3.w) << 8;
-        keep |= lc_lowbyte(a4.w) | lc_lowbyte(a5.w) << 8;
-        if (m1 && !lc_group_skip_fixed(ov, dv, inv, tmax, LcFloat4{a3.x, a3.y, a3.z, a3.w},
-                                       LcFloat4{a4.x, a4.y, a4.z, a4.w}, LcFloat4{a5.x, a5.y, a5.z, a5.w}))
-            keep |= m1;
-        return keep & all;
-    }
     LcFloat4 rec[LC_REC];
     constexpr int NR = FORM >= 2 ? LC_RECP : LC_REC;
     const float4 *recs = FORM >= 2 ? S.lcullp : (FORM == 1 ? S.lcullf : S.lcull);
@@ -343,14 +309,13 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // LC (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a leaf's tests run only
 // for the references its cull record (leafcull.hpp) cannot exclude for this ray and segment.
 template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0, bool REV = false, bool DEAL = false>
+          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0>
 __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
-                                               Prof *pf = nullptr, Pc *pc = nullptr, const float *rcp_lds = nullptr,
-                                               DealLds *deal = nullptr) {
+                                               Prof *pf = nullptr, Pc *pc = nullptr) {
     uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
     if (pf) pt0 = prof_now();
     if (pc && wave_leader()) pc->waves++;
@@ -367,8 +332,6 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
     static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
-    static_assert(!REV || (BF && !FULL), "far-first order: lean BF builds (shadow queries only)");
-    static_assert(!DEAL || (LC && !FULL), "dealt leaf tests: lean leaf-cull builds (shadow queries only)");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -387,11 +350,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         const uint32_t a = nd.y & 3u;
         const float split = __uint_as_float(nd.x);
         const float oa = comp(o, a), da = comp(d, a);
-        // rcp_lds (RL builds): the ray's RN(1/d) per axis in LDS [axis][thread], set at query start --
-        // the exact short division without three more VGPRs
-        const float tsplit = rcp_lds ? div_by_rcp(split - oa, da, rcp_lds[a * bdim + tid])
-                             : FD    ? div_by_rcp(split - oa, da, comp(T.r, a))
-                                     : split_distance(split, oa, da);
+        const float tsplit = FD ? div_by_rcp(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
         const uint32_t below = (oa < split) || (oa == split && da <= 0);
         const uint32_t child = nd.y >> 2;
         uint32_t k;
@@ -399,21 +358,16 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             const bool near_only = (tsplit >= T.tmax) | (tsplit < 0);
             const bool far_only = !near_only & (tsplit <= T.tmin);
             const bool push = !near_only & !far_only;
-            // REV (shadow queries): a node crossed in both children is entered far side first, the
-            // near child pushed with its interval start (the query's answer does not depend on
-            // the order of the leaves, each tested over its own interval)
-            k = (far_only | (REV & push)) ? below : 1u - below;
+            k = far_only ? below : 1u - below;
             if (push) {
                 const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
                 if (pc && T.nl == R) pc->vb += 8;
                 if (T.nl == R) gstack_at(gstk, T.sp - R, gstride, gid) = ring[slot]; // spill the oldest
-                ring[slot] = REV ? make_uint2(child + 1u - below, __float_as_uint(T.tmin))
-                                 : make_uint2(child + below, __float_as_uint(T.tmax));
+                ring[slot] = make_uint2(child + below, __float_as_uint(T.tmax));
             }
             T.nl = push && T.nl < R ? T.nl + 1 : T.nl;
             T.sp += push ? 1u : 0u;
-            if (REV) T.tmin = push ? tsplit : T.tmin;
-            else T.tmax = push ? tsplit : T.tmax;
+            T.tmax = push ? tsplit : T.tmax;
         } else if (tsplit >= T.tmax || tsplit < 0) {
             k = 1u - below;
         } else if (tsplit <= T.tmin) {
@@ -450,17 +404,11 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             if (pc) pc->vb += 8;
         }
         T.node = e.x;
-        if (REV) { // the far subtree ended with its nearest leaf, whose interval starts at the split
-            T.tmax = T.tmin;
-            T.tmin = __uint_as_float(e.y);
-        } else {
-            T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
-            T.tmax = __uint_as_float(e.y);
-        }
+        T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
+        T.tmax = __uint_as_float(e.y);
     };
     // LC 2: a leaf whose references are all excluded is passed like an empty leaf -- the lane
     // pops and descends to its next leaf in the same round, so the round's tests run on every lane
-    uint32_t passes = 0; // LC 6 / 7: empty leaves passed in this round
     for (;;) {
     culled = false;
     if (FAT) { // two levels per dependent load: a node's record carries its children's
@@ -539,15 +487,11 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             pc->masks++;
             pc_load(pc, SC && wave_uniform(T.node), 16u * (LC >= 4 ? LC_RECP : LC_REC));
         }
-        lmask = count >= lc_min ? leaf_mask<SC, LC == 5 ? 3 : (LC == 4 || LC >= 6 ? 2 : (LC == 3 ? 1 : 0))>(S, T.node, count, o, d, T.tmax)
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 4 ? 2 : (LC == 3 ? 1 : 0)>(S, T.node, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }
-    // LC 6 / 7 (packed records): at most 1 / 3 such passes per round, so the lanes with tests do not
-    // wait on the longest chain of empty leaves
-    if ((LC == 2 || LC >= 6) && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp &&
-        (LC == 2 || passes < (LC == 6 ? 1u : 3u))) {
-        passes++;
+    if (LC == 2 && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp) {
         pop_entry();
         continue;
     }
@@ -764,69 +708,6 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             const float s1 = s0 + T.tmax * dot(mk(pl.x, pl.y, pl.z), d);
             if (!((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f)))
                 if (!test(lrec(first + j))) break;
-        }
-    } else if (DEAL && count <= (uint32_t)LC_MAXREFS) {
-        // DEAL (shadow queries): the divergent leaf's tests -- the set bits of every lane's mask --
-        // dealt out over the lanes of this branch, one test per lane and chunk, instead of each lane
-        // walking its own bits (the loop would run as often as the largest mask; measured lane
-        // efficiency 0.22).  A shadow leaf's answer is "some test accepts", whatever the order, so
-        // an owner is occluded when any of its workers' tests accepted (rank-space mask in LDS).
-        const uint32_t lane = tid & 63u;
-        const uint64_t act = __ballot(1), lbelow = lane ? (~0ull >> (64 - lane)) : 0ull;
-        const uint32_t A = (uint32_t)__popcll(act), rank = (uint32_t)__popcll(act & lbelow);
-        const uint32_t cnt = (uint32_t)__builtin_popcount(lmask);
-        uint32_t pre = 0, total = 0; // exclusive prefix of the counts over the branch's lanes (5-bit counts)
-#pragma unroll
-        for (int b = 0; b < 5; b++) {
-            const uint64_t m = __ballot((cnt >> b) & 1u);
-            pre += (uint32_t)__popcll(m & lbelow) << b;
-            total += (uint32_t)__popcll(m) << b;
-        }
-        DealLds &dl = deal[tid >> 6];
-        for (uint32_t base = 0; base < total; base += A) { // wave-uniform
-            const int sp0 = (int)pre - (int)base;
-            const bool ov = cnt && sp0 < (int)A && sp0 + (int)cnt > 0; // my tests meet this chunk
-            const uint32_t sp = ov ? (uint32_t)max(sp0, 0) : 0u;
-            if (rank == 0) {
-                dl.smask = 0ull;
-                dl.rmask = 0ull;
-            }
-            wave_fence();
-            if (ov) {
-                dl.tab[sp] = (uint8_t)lane;
-                atomicOr(&dl.smask, 1ull << sp);
-            }
-            wave_fence();
-            // my test: chunk position = rank; its owner starts at the highest start position <= rank
-            const uint64_t sm = dl.smask;
-            const uint64_t upto = rank >= 63u ? ~0ull : ((2ull << rank) - 1ull);
-            const uint32_t spos = 63u - (uint32_t)__clzll(sm & upto);
-            const int owner = (int)dl.tab[spos];
-            const uint32_t pre_o = (uint32_t)__shfl((int)pre, owner, 64);
-            const uint32_t mask_o = (uint32_t)__shfl((int)lmask, owner, 64);
-            const uint32_t first_o = (uint32_t)__shfl((int)first, owner, 64);
-            const uint32_t excl_o = (uint32_t)__shfl((int)exclude, owner, 64);
-            const f3 oo = mk(__shfl(o.x, owner, 64), __shfl(o.y, owner, 64), __shfl(o.z, owner, 64));
-            const f3 dd = mk(__shfl(d.x, owner, 64), __shfl(d.y, owner, 64), __shfl(d.z, owner, 64));
-            const float tmax_o = __shfl(T.tmax, owner, 64);
-            bool acc = false;
-            if (base + rank < total) {
-                uint32_t mm = mask_o;
-                for (uint32_t k = base + rank - pre_o; k; k--) mm &= mm - 1u; // the owner's k-th reference
-                const TriRec r = lrec(first_o + (uint32_t)__builtin_ctz(mm));
-                if (pc) pc->tests++;
-                float ux, uy, tt;
-                acc = rec_id(r) != excl_o && tri_test_wave(oo, dd, r, tmax_o, ux, uy, tt);
-            }
-            if (acc) atomicOr(&dl.rmask, 1ull << rank);
-            wave_fence();
-            if (ov) {
-                const uint32_t r1 = min((uint32_t)(sp0 + (int)cnt), A);
-                const uint32_t w = r1 - sp;
-                const uint64_t range = (w >= 64u ? ~0ull : ((1ull << w) - 1ull)) << sp;
-                occluded = occluded | ((dl.rmask & range) != 0ull);
-            }
-            wave_fence();
         }
     } else if (LC && count <= (uint32_t)LC_MAXREFS) { // the mask's references, pipelined one ahead
         uint32_t m = lmask;

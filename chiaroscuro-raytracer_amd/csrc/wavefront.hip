@@ -202,19 +202,13 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
 template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
           bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0,
-          bool PROF = false, bool PC = false, bool RL = false, bool REV = false, bool DEAL = false>
+          bool PROF = false, bool PC = false>
 __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
-    static_assert(!DEAL || SHADOW, "dealt leaf tests: shadow queries only");
-    __shared__ DealLds deal_lds[DEAL ? 4 : 1];
-    static_assert(!REV || SHADOW, "far-first order: shadow queries only");
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
     // TILE: the top of the tree (fat records of nodes 0..TILE-1) copied into LDS after the stack ring
     uint4 *tile = (uint4 *)(ring_lds + R * blockDim.x);
-    // RL: the query's RN(1/d) per axis, [axis][thread] after the stack ring (no TILE in RL builds)
-    float *rl = (float *)(ring_lds + R * blockDim.x);
-    static_assert(!RL || !TILE, "RL: no LDS node tile");
     if (TILE) {
         const uint32_t nt = 2u * min((uint32_t)TILE, S.n_nodes);
         for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) tile[i] = S.fat[i];
@@ -289,11 +283,6 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                             W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
                         } else if (iss = true, trav_begin(S, o, d, SHADOW, r1.w, T)) {
                             state = busy_st;
-                            if (RL) {
-                                rl[threadIdx.x] = T.r.x;
-                                rl[blockDim.x + threadIdx.x] = T.r.y;
-                                rl[2 * blockDim.x + threadIdx.x] = T.r.z;
-                            }
                             if (FULL) diag_begin(&dg);
                         } else if (SHADOW) {
                             if (PC) pc.vb += 4;
@@ -317,10 +306,9 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC, REV, DEAL>(A.lc_debug, A.lc_min, 
+            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC>(A.lc_debug, A.lc_min,
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
-                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr, RL ? rl : nullptr,
-                DEAL ? deal_lds : nullptr);
+                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr);
             if (r != busy_st) {
                 if (PC) pc.vb += SHADOW ? 4u : 16u;
                 if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
@@ -1049,9 +1037,6 @@ struct WfVariant {
     int cull; // the camera trace reads the cull boxes (1: references and leaves, 2: also subtrees)
     int packet; // the camera trace is a packet trace (needs a near child common to all camera rays)
     int lc;     // the tail kernel's leaf cull form (trav_round's LC; 0: none)
-    int rl;     // the secondary and shadow traces keep RN(1/d) in LDS (12 B per thread after the ring)
-    int closest_waves; // the secondary closest trace's waves per SIMD when not waves_per_simd (0: the same)
-    int shadow_waves;  // the shadow trace's (0: the same)
 };
 #define CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, PL)                                                     \
     {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
@@ -1128,67 +1113,19 @@ static const WfVariant kWf[] = {
     // the tail kernel culls the same way
     {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
-    // 27: 26 whose secondary and shadow traces divide exactly by the ray's RN(1/d) kept in LDS
-    //     (round 3: 377.4 vs 366.1 ms per pass, shadow 54.7 vs 53.1 ms per launch)
-    CR_WF_OPT({wf_trace_packet<8, 2>,
-     wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, false, true>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, false, true>, 8, 8, 0, 2,
-     1, 4, 1}),
-    // 28: 26 whose shadow trace enters both-crossed nodes far side first (toward the light;
-    //     exact for any-hit queries): 570.9 ms, shadow 104.7 ms -- occluders lie near the origins
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, false, false, true>, 8, 8,
-     0, 2, 1, 4}),
-    // 29: 26 with the exact short division by RN(1/d) kept in VGPRs (FD) in the secondary and shadow
-    //     traces: 390.8 ms, shadow 58.8 ms
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}),
-    // 30: 26 whose secondary closest trace runs at 7 waves / SIMD (72 VGPRs: no spills): 373.0 ms
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 7, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 7}),
-    // 31: 26 whose secondary closest trace does not cull leaves (build 18's): 371.0 ms
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}),
-    // 32: 26 whose shadow trace deals a divergent leaf's tests out over the lanes of the round (the
-    //     leaf-cull loop runs 6.0 iterations per divergent round at lane efficiency 0.22, cr_get_perf):
-    //     bit-exact, but 368.9 / 369.2 vs 362.1 / 362.4 ms (shadow 54.4 vs 52.6 ms: 11 lane shuffles and
-    //     LDS traffic per dealt test, 14 VGPR spills)
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, false, false, false, true>,
-     8, 8, 0, 2, 1, 4}),
-    // 33: 29 (the exact short division from RN(1/d) in VGPRs) with a divergent leaf's cull record
-    //     loaded and tested one group at a time (the record's peak register use halved; the leaf loop's
-    //     one-ahead record pipeline is the other peak): 378.4 vs 362.4 ms, shadow 55.3 vs 52.5 ms
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 5>,
-     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 5>, 8, 8, 0, 2, 1, 4}),
-    // 34: 26 with the cull record loaded one group at a time (no FD): 375.7 ms, shadow 55.0 ms
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 5>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 5>, 8, 8, 0, 2, 1, 4}),
-    // 35: 26 whose shadow trace runs at 7 waves / SIMD (68 VGPRs, no spills) with the exact short
-    //     division (FD): 369.9 vs 363.7 ms (shadow 53.3 vs 52.5 ms); the division saves 2.5% of the
-    //     7-wave trace, the eighth wave is worth more
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 7, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 0, 7}),
-    // 36: 26 whose shadow trace runs at 7 waves / SIMD (no FD): 375.1 ms (shadow 54.6 ms)
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 7, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4, 0, 0, 7}),
-    // 37 / 38: 26 whose shadow-trace lanes pass up to 1 / 3 leaves with every reference excluded (or
-    //     none) and descend to the next in the same round (build 20 passed any number: 2x slower):
-    //     bit-exact; 364.0 / 380.7 vs 363.4 ms per pass (shadow 53.0 / 57.4 vs 52.8 ms)
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>, 8, 8, 0, 2, 1, 4}),
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 7>, 8, 8, 0, 2, 1, 4}),
-    // 39: 37 whose secondary closest trace passes up to 1 such leaf too: 363.5 ms (neutral)
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 6>, 8, 8, 0, 2, 1, 4}),
+    // 27-39: measured on top of 26 in round 3 and rejected (DESIGN.md §3.7 keeps their numbers): the
+    //     exact short division by RN(1/d) kept in LDS (27) or in VGPRs (29), far-side-first shadow
+    //     traversal (28), the secondary closest trace at 7 waves (30) or without the leaf cull (31), dealt
+    //     shadow-leaf tests (32), cull records loaded one group at a time (33, 34), the shadow trace at 7
+    //     waves (35, 36), lanes passing up to 1 / 3 fully culled leaves per round (37-39)
+    CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE,
+    CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE,
     // 40: 26 whose camera packet divides by the rays' RN(1/d) kept in VGPRs (FD; the packet's
     //     spills are outside its loops): camera trace 41.0 -> 37.7 ms, 363.1 -> 360.0 ms per pass
     {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
-    // 41: 40 with packets of 64 rays (one per lane: no spills): camera 49.6 ms
-    CR_WF_OPT({wf_trace_packet<8, 1, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4}),
+    // 41: 40 with packets of 64 rays (one per lane: no spills): camera 49.6 ms (rejected)
+    CR_WF_NONE,
     // 42: 18 with 40's camera packet (the default below LEAF_CULL_MIN_TRIS triangles)
     {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
      wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0},
@@ -1199,9 +1136,8 @@ static const WfVariant kWf[] = {
      wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
     {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
      wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0},
-    // 45: 43 with FD in the secondary closest trace too (3 loop-invariant lane values spilled)
-    CR_WF_OPT({wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4})};
+    // 45: 43 with FD in the secondary closest trace too (3 loop-invariant lane values spilled; rejected)
+    CR_WF_NONE};
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {
     wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
@@ -1391,14 +1327,11 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
                                            : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
-    const uint32_t cblocks =
-        (!A.full_counters && v.closest_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.closest_waves : blocks;
-    const uint32_t sblocks =
-        (!A.full_counters && v.shadow_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.shadow_waves : blocks;
+    const uint32_t cblocks = blocks, sblocks = blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds =
-        (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4) + (v.rl ? 3 * (size_t)blk * 4 : 0);
+        (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
     int err = 0;
     // the rest of the chunk from closest queue g on, in one launch
@@ -1426,9 +1359,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         Wc.gstack = gstack;
         const int kind = g == 1 ? TK_CAMERA : TK_CLOSEST;
         if ((err = trace_event(te, s, kind, true))) return;
-        // (the camera trace does not use the RL area: without it, 8 packet blocks fit a CU's LDS)
         hipLaunchKernelGGL(g == 1 ? camera_kernel(v, A) : v.closest, dim3(g == 1 ? blocks : cblocks), dim3(blk),
-                           g == 1 ? lds - (v.rl ? 3 * (size_t)blk * 4 : 0) : lds, s, A, Wc, g);
+                           lds, s, A, Wc, g);
         err = trace_event(te, s, kind, false);
     };
     hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
@@ -1490,15 +1422,12 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
                                            : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
-    const uint32_t cblocks =
-        (!A.full_counters && v.closest_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.closest_waves : blocks;
-    const uint32_t sblocks =
-        (!A.full_counters && v.shadow_waves) ? (uint32_t)(num_cus > 0 ? num_cus : 256) * v.shadow_waves : blocks;
+    const uint32_t cblocks = blocks, sblocks = blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     for (int i = 0; i < nl; i++)
         if (L[i].W.gstride < blk * blocks || L[i].W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds =
-        (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4) + (v.rl ? 3 * (size_t)blk * 4 : 0);
+        (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8;
     int err = 0;
     struct Run {
@@ -1529,9 +1458,8 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         Wc.gstack = gstack;
         const int kind = g == 1 ? TK_CAMERA : TK_CLOSEST;
         if ((err = trace_event(te, s, kind, true))) return;
-        // (the camera trace does not use the RL area: without it, 8 packet blocks fit a CU's LDS)
         hipLaunchKernelGGL(g == 1 ? camera_kernel(v, A) : v.closest, dim3(g == 1 ? blocks : cblocks), dim3(blk),
-                           g == 1 ? lds - (v.rl ? 3 * (size_t)blk * 4 : 0) : lds, s, A, Wc, g);
+                           lds, s, A, Wc, g);
         err = trace_event(te, s, kind, false);
     };
     auto shade = [&](WfLane &ln, Run &r) { // wf_shade(g), then the queue lengths to the host, async

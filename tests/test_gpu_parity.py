@@ -729,10 +729,19 @@ def test_default_build_by_scene_size(ca, sponza, nanobox):
         try:
             pair.dev.render(pair.camera(ca, 64, 36), ca.render_params(64, 36, 2, 6, 0xC41A05C0, layer=1), None)
             perf = pair.dev.perf()
+            builds = [pair.dev.last_trace_build()]
+            pair.dev.set_option("perf_counters", 0)
+            pair.dev.render(pair.camera(ca, 16, 8), ca.render_params(16, 8, 1, 6, 0xC41A05C0, layer=1), None)
+            builds.append(pair.dev.last_trace_build())
         finally:
             pair.dev.set_option("perf_counters", 0)
             pair.dev.set_option("counters", 1)
+        pair.dev.render(pair.camera(ca, 16, 8), ca.render_params(16, 8, 1, 6, 0xC41A05C0, layer=1), None)
+        builds.append(pair.dev.last_trace_build())
         masks[name] = perf["shadow"]["masks"] + perf["closest"]["masks"] + perf["tail"]["masks"]
+        # cr_last_trace_build names it: perf and lean renders the scene-size default, counting -1
+        want = 43 if name == "sponza" else 44
+        assert builds == [want, want, -1], (name, builds)
     assert masks["sponza"] > 0 and masks["nanobox"] == 0, masks
 
 
