@@ -274,7 +274,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             // bytes of the buffers of a chunk of Pn paths with kb-bit sort keys
             auto need_for = [&](uint64_t Pn, int kb) -> size_t {
                 const size_t st = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)Pn, kb, c->wf_sort_lib != 0) : 0;
-                return (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 16 * (size_t)Pn +
+                return (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 20 * (size_t)Pn +
                        (c->wf_sort ? 32 * (size_t)Pn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
             };
             const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
@@ -308,6 +308,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.occ = (uint32_t *)take(4 * (size_t)P);
                 W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
                 W.cxy = (float2 *)take(8 * (size_t)P);
+                W.ended = (uint32_t *)take(4 * (size_t)P);
+                W.fold = c->wf_fold;
                 W.sort = c->wf_sort && nkeys <= (1ull << 32);
                 W.key_bits = key_bits;
                 W.key_bits_pixel = key_bits_pixel;
@@ -1203,6 +1205,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_xcd") && v >= 0 && v <= 7) c->wf_xcd = (uint32_t)v;
     else if (!std::strcmp(key, "wf_leaf_keys") && (v == 0 || v == 1)) c->wf_leaf_keys = (int)v;
     else if (!std::strcmp(key, "wf_resolve_paths") && v >= 0 && v <= 64) c->wf_resolve_paths = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_fold") && v >= 0 && v <= 2) c->wf_fold = (int)v;
     else if (!std::strcmp(key, "wf_leaf_shift") && v >= 0 && v <= 24) c->wf_leaf_shift = (uint32_t)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;

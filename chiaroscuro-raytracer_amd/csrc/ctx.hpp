@@ -113,6 +113,12 @@ struct cr_ctx {
     uint32_t wf_leaf_shift = 1; // ... its node index >> this (a leaf and its sibling share a key region)
     // sweep (1080p x 128 spp, 2 rounds): 0 / 1 / 2 / 4 / 8 / 16 / 64 -> 399.2 / 394.6 / 394.8 / 394.8 / 393.8 / 393.6 / 394.5 ms
     uint32_t wf_resolve_paths = 16; // wf_resolve in path order for queues of at least P / this rays (0: never)
+    // WfArgs::fold: 0 wf_resolve's path-order sweep per generation; 1 / 2 lists instead of the sweep
+    // (round 4, bit-exact, slower: 1080p x 128 spp in pass groups, two interleaved rounds, ms per layer:
+    // sweep 322.9 / 323.4, fold 1 (continuing paths resolved in the next wf_shade) 324.5 / 324.6;
+    // sweep 322.5 / 322.9, fold 2 (resolved beside the closest trace from its queue) 325.6 / 325.3 --
+    // the sweep runs beside the closest trace of g + 1, off the critical path, and reads in path order)
+    int wf_fold = 0;
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

@@ -180,10 +180,11 @@ int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t s
 // work items [w0, w0 + P) advance one bounce per generation through separate
 // kernels (camera, closest trace, shade, shadow trace, bounce) that exchange
 // rays through queues in HBM.
-// counters: closest count [g], shadow count [WF_G+g], work [2*WF_G+g], [3*WF_G+g]; g <= K + 1 <= 65;
+// counters: closest count [g], shadow count [WF_G+g], work [2*WF_G+g], [3*WF_G+g], ended paths [4*WF_G+g];
+// g <= K + 1 <= 65;
 // then the per-XCD work counters of the partitioned queues (WfArgs::xcd), WF_XSTRIDE apart
 // (one 64-B line each): closest [WF_XBASE + (g*8 + x)*WF_XSTRIDE], shadow after WF_G*8 of those
-enum : uint32_t { WF_G = 66, WF_XCDS = 8, WF_XSTRIDE = 16, WF_XBASE = 4 * WF_G,
+enum : uint32_t { WF_G = 66, WF_XCDS = 8, WF_XSTRIDE = 16, WF_XBASE = 5 * WF_G,
                   WF_CNT = WF_XBASE + 2 * WF_G * WF_XCDS * WF_XSTRIDE };
 enum { WF_STATE = 6 };            // path-state float4 slots per path (wavefront.hip PS)
 struct WfArgs {
@@ -243,10 +244,16 @@ struct WfArgs {
     uint32_t dir_res_s; // leaf keys: direction bins per axis of the SHADOW queues' keys
     int key_bits_s;     // significant bits of the shadow queues' keys
     int tail_waves;     // waves per SIMD of the lean tail launch (4, 5, 6)
+    // fold = 1 (option "wf_fold", the default): no sweep over the paths per generation -- wf_shade(g)
+    // lists the paths whose hit at g ends them (ended, count at cnt[4 WF_G + g]), wf_fold(g) folds
+    // those after the shadow trace, and the paths that continue have their bounce g resolved where
+    // they are read next (wf_shade(g + 1), or wf_tail at pickup).  0: wf_resolve (round 3)
+    int fold;
+    uint32_t *ended;    // [P] paths that ended at the generation being folded
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position
-inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8; }
+inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4; }
 // Second stream and fork / join events of a render (shadow trace g beside closest trace g + 1).
 struct WfStreams {
     hipStream_t side;

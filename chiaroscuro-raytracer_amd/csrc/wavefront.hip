@@ -67,6 +67,7 @@ __device__ __forceinline__ uint32_t *cnt_closest(const WfArgs &W, uint32_t g) { 
 __device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + WF_G + g; }
 __device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 2 * WF_G + g; }
 __device__ __forceinline__ uint32_t *work_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 3 * WF_G + g; }
+__device__ __forceinline__ uint32_t *cnt_ended(const WfArgs &W, uint32_t g) { return W.cnt + 4 * WF_G + g; }
 
 // Queue sort key (raysort.hip): 8x8-pixel sub-tile of the path's pixel, then an
 // 8x8 octahedral direction bin.  Any deterministic key is exact -- it only
@@ -475,6 +476,19 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
     return nee;
 }
 
+// The pending NEE term of bounce gp of a path that continues (W.fold): D = direct + (visible ? contrib :
+// 0) (rayTracer.cpp:96-99, the reference's single add), written back over dw[2(gp-1)] -- where the
+// path is read next (wf_shade(gp + 1), wf_tail at pickup), before anything folds or overwrites PS3.
+// The shadow result occ[slot] is generation gp's: the next shadow trace has not run yet.
+__device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32_t gp) {
+    float4 &dk = W.dw[(size_t)(2 * (gp - 1)) * W.P + p];
+    const float4 d4 = dk;
+    const uint32_t slot = __float_as_uint(d4.w);
+    f3 direct = ld3(d4);
+    if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(PS(W, 3, p)));
+    dk = pk(direct, 0u);
+}
+
 // ----------------------------------------------------------------- shade --
 // Every closest ray of generation g: misses finish their path with the
 // background; hits run shade_next and append their NEE ray to shadow queue g and
@@ -499,6 +513,8 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
         }
         const uint32_t p = __float_as_uint(r0.w);
         const bool hit = in && h.w != 0u;
+        // (fold: bounce g - 1 of every path read here, hit or miss, before it is folded or shaded on)
+        if (W.fold == 1 && g >= 2 && in && p != NO_PATH) resolve_prev(W, p, g - 1);
         bool textured = false, nee = false, cont = false;
         ShadowRay sh = {mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, 0u};
         f3 org = mk(0.f, 0.f, 0.f), wi = mk(0.f, 0.f, 0.f);
@@ -519,6 +535,11 @@ __global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t
                                                                                  : sort_key(A, W, p, sh.d);
                 if (W.sort_lib) W.perm[0][0][j] = j; // (raysort.hip takes the identity itself)
             }
+        }
+        if (W.fold) { // (uniform: every thread of the block calls block_append)
+            const bool ends = hit && !cont;
+            const uint32_t je = block_append(cnt_ended(W, g), ends, app);
+            if (ends) W.ended[je] = p;
         }
         const uint32_t jc = block_append(cnt_closest(W, g + 1), cont, app);
         if (cont) {
@@ -576,6 +597,27 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
         // then no longer names generation g)
         if (W.ended_only && (__float_as_uint(s3.w) >> 1 != g || !(__float_as_uint(s3.w) & 1u))) continue;
         resolve_path(A, W, p, g, s3);
+    }
+}
+
+// W.fold: after the shadow trace of generation g, the paths that ended at g (wf_shade's list, in
+// the order it met them -- path order for every queue of a chunk): their last bounce's NEE term,
+// then the back-to-front fold into samples[w].  No pass over the other paths.
+__global__ void __launch_bounds__(256) wf_fold(RenderArgs A, WfArgs W, uint32_t g) {
+    const uint32_t n = *cnt_ended(W, g);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t p = W.ended[i];
+        const float4 s3 = PS(W, 3, p);
+        // (overlapped tail: only the ended paths are here, which the tail never takes)
+        resolve_path(A, W, p, g, s3);
+    }
+    // fold 2: the paths that go on -- closest queue g + 1 -- have their bounce g resolved here too (beside
+    // the closest trace of g + 1, off the critical path), unless an overlapped tail resolves them itself
+    if (W.fold == 2 && !W.ended_only && g < (uint32_t)A.K) {
+        const uint32_t nc = *cnt_closest(W, g + 1);
+        const float4 *rays = W.ray[(g + 1) & 1];
+        for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nc; j += gridDim.x * blockDim.x)
+            resolve_prev(W, __float_as_uint(rays[2 * (size_t)j].w), g);
     }
 }
 
@@ -648,6 +690,8 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                         nshadow++;
                         state = trav_begin(S, o, d, true, s1.w, T) ? ST_SHADOW : ST_VISIBLE;
                     } else if (p != NO_PATH) {
+                        // (fold: the path's bounce g0 - 1 is still pending; overlapped tails resolve it above)
+                        if (W.fold == 1 && g0 >= 2) resolve_prev(W, p, g0 - 1);
                         start_closest(); // (a dead camera ray of a partial tile: no query)
                     }
                 }
@@ -1403,7 +1447,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, st, TK_SHADOW, true))) break;
         hipLaunchKernelGGL(v.shadow, dim3(sblocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, TK_SHADOW, false))) break;
-        hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        hipLaunchKernelGGL(W.fold ? wf_fold : wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
         W.ended_only = 0u;
         if (next || overlap)
             if ((err = (int)hipEventRecord(ss.join, ss.side)) || (err = (int)hipStreamWaitEvent(st, ss.join, 0)))
@@ -1514,7 +1558,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_SHADOW, true))) return true;
         hipLaunchKernelGGL(v.shadow, dim3(sblocks), dim3(blk), lds, ln.st, A, Ws, g);
         if ((err = trace_event(te, ln.st, TK_SHADOW, false))) return true;
-        hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, g);
+        hipLaunchKernelGGL(r.W.fold ? wf_fold : wf_resolve, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, g);
         if (next) {
             if ((err = (int)hipEventRecord(ln.join, ln.side)) || (err = (int)hipStreamWaitEvent(ln.st, ln.join, 0)))
                 return true;

@@ -1,14 +1,20 @@
 #!/bin/bash
-# Interleaved A/B timing of bench.py argument sets (default sponza config, no CPU leg).
-#   bash scripts/gpu_ab.sh ROUNDS "args A" "args B" ...
+# A/B of bench options, interleaved rounds: bash scripts/gpu_ab.sh "pytest -k expr" "optsA" "optsB" [rounds]
+# (each opts string is passed to bench.py as-is, e.g. "--opt wf_fold=0"; "" = the defaults)
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/ab
-R=$1; shift
-for r in $(seq 1 $R); do
-  i=0
-  for a in "$@"; do
-    i=$((i+1))
-    timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 --warmup 1 $a > gpurun_out/ab/$i.$r.json 2>gpurun_out/ab/$i.$r.log || { echo "failed: $a"; tail -5 gpurun_out/ab/$i.$r.log; exit 1; }
-    python -c "import json,sys;d=json.load(open('gpurun_out/ab/$i.$r.json'));r=d['roofline'];o=r.get('other_traces',{});print('%-40s %8.2f ms  %s %7.2f  camera %7.2f' % (sys.argv[1], d['ms_per_step'], r['kernel'][9:15], r['avg_launch_ms'], o.get('camera',{}).get('avg_launch_ms',r['avg_launch_ms'])))" "$a"
+mkdir -p gpurun_out
+K=$1; A=$2; B=$3; N=${4:-2}
+if [ -n "$K" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "$K" > gpurun_out/pytest_ab.txt 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_ab.txt
+  [ $rc -eq 0 ] || exit $rc
+fi
+for r in $(seq $N); do
+  for tag in A B; do
+    if [ $tag = A ]; then O=$A; else O=$B; fi
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --parity-rows 0 --steps 20 --warmup 5 $O > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err || { tail -5 gpurun_out/ab_$tag.err; exit 1; }
+    python -c "
+import json; d=json.load(open('gpurun_out/ab_$tag.json')); r=d['roofline']
+print('$tag', '$O', d['value'], d['ms_per_step'], r.get('avg_launch_ms'), {k: (v or {}).get('avg_launch_ms') for k, v in r.get('other_traces', {}).items()})"
   done
 done

@@ -67,14 +67,18 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir, leaf):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("resolve_paths", [0, 1, 4, 64])
-def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, resolve_paths):
-    """wf_resolve in queue order (0) or, for queues of at least P / resolve_paths rays, in
-    path order by the PS3 bounce mark (default 16; 64: nearly every generation): the same bits and counters over progressive
-    layers 1..3 on the same buffers (a mark left by an earlier layer or chunk must not
-    resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks."""
+@pytest.mark.parametrize("fold,resolve_paths", [(1, 16), (2, 16), (0, 0), (0, 1), (0, 4), (0, 64)])
+def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_paths):
+    """The NEE term of a bounce and the fold of an ended path: by default (wf_fold 1) wf_shade lists
+    the paths a hit ends, wf_fold folds them after the shadow trace, and a path that goes on has its
+    bounce resolved where it is read next (wf_shade of the next generation, wf_tail at pickup); wf_fold 0
+    is round 3's wf_resolve sweep, in queue order (0) or, for queues of at least P / resolve_paths
+    rays, in path order by the PS3 bounce mark (64: nearly every generation).  The same bits and
+    counters over progressive layers 1..3 on the same buffers (a mark left by an earlier layer or chunk
+    must not resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_fold", fold)
         pair.dev.set_option("wf_resolve_paths", resolve_paths)
         pair.dev.set_option("wf_sort_min", 0)
         cam = pair.camera(ca, x, y)
@@ -90,6 +94,7 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, resolve_paths):
                     assert_bitwise(g, o, "resolve_paths %d wf_paths %d layer %d" % (resolve_paths, paths, layer))
                     assert {k: gc[k] for k in ORACLE_KEYS} == oc
         finally:
+            pair.dev.set_option("wf_fold", 1)
             pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_paths", 256 << 20)
@@ -290,8 +295,8 @@ def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
 
 
 @pytest.mark.parametrize("tail_min", [1 << 30, 12000, 3000])
-@pytest.mark.parametrize("overlap", [1, 0])
-def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap):
+@pytest.mark.parametrize("overlap,fold", [(1, 1), (0, 1), (1, 2), (0, 2), (1, 0), (0, 0)])
+def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap, fold):
     """wf_tail (the last generations of a chunk in one launch, per-path bodies
     shared with wf_shade / wf_bounce): from generation 1 (every queue is below
     1 << 30) and from later generations, counting and lean builds; after the last shadow trace
@@ -302,6 +307,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_tail_min", tail_min)
         pair.dev.set_option("wf_tail_overlap", overlap)
+        pair.dev.set_option("wf_fold", fold)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
             pair.dev.set_option("counters", 0)
@@ -311,6 +317,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_tail_min", 0)
             pair.dev.set_option("wf_tail_overlap", 0)
+            pair.dev.set_option("wf_fold", 1)
         assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
         assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
