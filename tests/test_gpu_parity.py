@@ -69,11 +69,12 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir, leaf):
 
 @pytest.mark.parametrize("fold,resolve_paths", [(1, 16), (2, 16), (0, 0), (0, 1), (0, 4), (0, 64)])
 def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_paths):
-    """The NEE term of a bounce and the fold of an ended path: by default (wf_fold 1) wf_shade lists
-    the paths a hit ends, wf_fold folds them after the shadow trace, and a path that goes on has its
-    bounce resolved where it is read next (wf_shade of the next generation, wf_tail at pickup); wf_fold 0
-    is round 3's wf_resolve sweep, in queue order (0) or, for queues of at least P / resolve_paths
-    rays, in path order by the PS3 bounce mark (64: nearly every generation).  The same bits and
+    """The NEE term of a bounce and the fold of an ended path: by default (wf_fold 0) wf_resolve's
+    sweep after each shadow trace, in queue order (resolve_paths 0) or, for queues of at least
+    P / resolve_paths rays, in path order by the PS3 bounce mark (default 16; 64: nearly every
+    generation); wf_fold 1 / 2: wf_shade lists the paths a hit ends, wf_fold folds them after the shadow
+    trace, and a path that goes on has its bounce resolved where it is read next (1: wf_shade of the next
+    generation, wf_tail at pickup) or beside the next closest trace from its queue (2).  The same bits and
     counters over progressive layers 1..3 on the same buffers (a mark left by an earlier layer or chunk
     must not resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
@@ -94,7 +95,7 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
                     assert_bitwise(g, o, "resolve_paths %d wf_paths %d layer %d" % (resolve_paths, paths, layer))
                     assert {k: gc[k] for k in ORACLE_KEYS} == oc
         finally:
-            pair.dev.set_option("wf_fold", 1)
+            pair.dev.set_option("wf_fold", 0)
             pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_paths", 256 << 20)
@@ -317,7 +318,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_tail_min", 0)
             pair.dev.set_option("wf_tail_overlap", 0)
-            pair.dev.set_option("wf_fold", 1)
+            pair.dev.set_option("wf_fold", 0)
         assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
         assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
