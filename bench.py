@@ -373,22 +373,14 @@ def run_rank(args, world, backend):
     # work); bit-identical to one layer per pass (tests/test_gpu_parity.py)
     dev.set_option("counters", 0)  # (the timed, lean build: the counting build renders one layer per pass)
     p1 = ca.render_params(xres, yres, spp, k, seed, layer=1, rank=rank, nranks=world, tile=tile)
-    nl_pass, _ = fr.plan_layers(p1, args.layers_per_pass)
-    if dist:  # every rank must run the same passes (the gathers pair up)
-        t = torch.tensor([nl_pass], dtype=torch.int64, device=backend.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        nl_pass = int(t.item())
+    nl_pass, _ = fr.plan_layers(p1, args.layers_per_pass)  # (every rank the same: plan_layers agrees)
     groups = []
 
     def step(layer, n, record):
         """Layers layer .. layer + n - 1 (n <= nl_pass) as one pass group."""
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
         tp = time.perf_counter()
-        n, pieces = fr.plan_layers(p, n)
-        if dist:  # every rank runs the same group (its per-layer gathers pair up): the smallest plan
-            t = torch.tensor([n], dtype=torch.int64, device=backend.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            n = int(t.item())
+        n, pieces = fr.plan_layers(p, n)  # (with several ranks: agreed by an all-reduce MIN)
         if rank == 0:
             log("group of %d layers in %d pieces (plan %.1f ms)" % (n, pieces, (time.perf_counter() - tp) * 1e3))
         if n == 1 and pieces == 1:

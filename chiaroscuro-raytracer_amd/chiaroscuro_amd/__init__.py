@@ -183,13 +183,15 @@ HIP_SYMBOLS = ("cr_create", "cr_destroy", "cr_last_error", "cr_upload_scene", "c
                "cr_group_upload_scene", "cr_group_set_option", "cr_group_render", "cr_group_get_counters",
                "cr_group_rank_ms", "cr_group_ctx", "cr_group_tonemap", "cr_set_accumulator",
                "cr_group_set_accumulator", "cr_layers_per_pass", "cr_render_layers_device",
-               "cr_render_tiles_layers_device", "cr_render_layers", "cr_scene_triangles", "cr_layers_per_group")
+               "cr_render_tiles_layers_device", "cr_render_layers", "cr_scene_triangles", "cr_layers_per_group",
+               "cr_blend_tiles_layers_device", "cr_render_dist_layers_device", "cr_group_render_layers")
 HOST_SYMBOLS = ("chiaro_last_error", "chiaro_scene_create", "chiaro_scene_info_get", "chiaro_scene_destroy",
                 "chiaro_model_create", "chiaro_model_load", "chiaro_model_num_meshes", "chiaro_model_num_triangles",
                 "chiaro_model_num_textures", "chiaro_model_triangles", "chiaro_model_texture",
                 "chiaro_model_destroy", "chiaro_kdtree_create", "chiaro_kdtree_num_nodes", "chiaro_kdtree_num_refs",
                 "chiaro_kdtree_export", "chiaro_kdtree_describe", "chiaro_kdtree_destroy",
-                "chiaro_raytracer_create", "chiaro_raytracer_raytrace", "chiaro_raytracer_pixels",
+                "chiaro_raytracer_create", "chiaro_raytracer_raytrace", "chiaro_raytracer_raytrace_layers",
+                "chiaro_raytracer_pixels",
                 "chiaro_raytracer_data", "chiaro_raytracer_maxval", "chiaro_raytracer_layers",
                 "chiaro_raytracer_counters", "chiaro_raytracer_normalize", "chiaro_raytracer_export",
                 "chiaro_raytracer_ctx", "chiaro_raytracer_destroy", "chiaro_camera",
@@ -245,6 +247,7 @@ def libs():
     _sig(hip, "cr_render_tiles_layers_device", C.c_int,
          [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32, P, P])
     _sig(hip, "cr_blend_tiles_device", C.c_int, [P, C.POINTER(CrRenderParams), P, P, P])
+    _sig(hip, "cr_blend_tiles_layers_device", C.c_int, [P, C.POINTER(CrRenderParams), C.c_uint32, P, P, P])
     _sig(hip, "cr_tiles_for_rank", C.c_uint32, [C.POINTER(CrRenderParams), C.c_uint32])
     _sig(hip, "cr_tile_origin", C.c_int, [C.POINTER(CrRenderParams), C.c_uint32, C.c_uint32,
                                           C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)])
@@ -268,6 +271,8 @@ def libs():
     _sig(hip, "cr_comm_init", C.c_int, [P, C.c_int, C.c_int, C.POINTER(C.c_uint8)])
     _sig(hip, "cr_comm_destroy", C.c_int, [P])
     _sig(hip, "cr_render_dist_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), P, P])
+    _sig(hip, "cr_render_dist_layers_device", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams),
+                                                         C.c_uint32, P, P])
     _sig(hip, "cr_device_count", C.c_int, [])
     _sig(hip, "cr_group_create", P, [C.c_int, C.POINTER(C.c_int)])
     _sig(hip, "cr_group_destroy", None, [P])
@@ -277,6 +282,8 @@ def libs():
     _sig(hip, "cr_group_upload_scene", C.c_int, [P, C.POINTER(CrSceneDesc)])
     _sig(hip, "cr_group_set_option", C.c_int, [P, C.c_char_p, C.c_int64])
     _sig(hip, "cr_group_render", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), FP])
+    _sig(hip, "cr_group_render_layers", C.c_int, [P, C.POINTER(CrCamera), C.POINTER(CrRenderParams), C.c_uint32,
+                                                   FP])
     _sig(hip, "cr_group_get_counters", C.c_int, [P, C.POINTER(CrCounters)])
     _sig(hip, "cr_group_rank_ms", C.c_int, [P, FP])
     _sig(hip, "cr_group_ctx", P, [P, C.c_int])
@@ -306,6 +313,7 @@ def libs():
     _sig(host, "chiaro_kdtree_destroy", None, [P])
     _sig(host, "chiaro_raytracer_create", P, [P, P, C.c_int])
     _sig(host, "chiaro_raytracer_raytrace", C.c_int, [P, FP, FP, FP, C.c_float])
+    _sig(host, "chiaro_raytracer_raytrace_layers", C.c_int, [P, C.c_uint32, FP, FP, FP, C.c_float])
     _sig(host, "chiaro_raytracer_pixels", FP, [P])
     _sig(host, "chiaro_raytracer_data", C.POINTER(C.c_uint8), [P])
     _sig(host, "chiaro_raytracer_maxval", C.c_float, [P])
@@ -553,6 +561,13 @@ class Device:
                                                           C.c_void_p(d_tiles_ptr), C.c_void_p(stream)),
                   "cr_render_tiles_layers_device")
 
+    def blend_tiles_layers_device(self, p, nlayers: int, d_gathered_ptr: int, d_frame_ptr: int, stream: int = 0):
+        """cr_blend_tiles_layers_device: gathered [nranks][nlayers][max_tiles][T][T][3], layers p.layer ..
+        + nlayers - 1 blended in order in one launch."""
+        self._chk(libs()[0].cr_blend_tiles_layers_device(self._c, C.byref(p), int(nlayers), C.c_void_p(d_gathered_ptr),
+                                                         C.c_void_p(d_frame_ptr), C.c_void_p(stream)),
+                  "cr_blend_tiles_layers_device")
+
     def blend_tiles_device(self, p, d_gathered_ptr: int, d_frame_ptr: int, stream: int = 0):
         self._chk(libs()[0].cr_blend_tiles_device(self._c, C.byref(p), C.c_void_p(d_gathered_ptr),
                                                   C.c_void_p(d_frame_ptr), C.c_void_p(stream)),
@@ -667,6 +682,13 @@ class Device:
         self._chk(libs()[0].cr_render_dist_device(self._c, C.byref(cam), C.byref(p), C.c_void_p(d_frame_ptr),
                                                   C.c_void_p(stream)), "cr_render_dist_device")
 
+    def render_dist_layers_device(self, cam, p, nlayers: int, d_frame_ptr: int, stream: int = 0):
+        """cr_render_dist_layers_device: my tiles of nlayers layers in one pass group, one RCCL gather of
+        the group's buffers to rank 0, one blend of its layers there (every rank the same nlayers)."""
+        self._chk(libs()[0].cr_render_dist_layers_device(self._c, C.byref(cam), C.byref(p), int(nlayers),
+                                                         C.c_void_p(d_frame_ptr), C.c_void_p(stream)),
+                  "cr_render_dist_layers_device")
+
     def synchronize(self):
         self._chk(libs()[0].cr_synchronize(self._c), "cr_synchronize")
 
@@ -710,6 +732,13 @@ class Group:
         self._chk(libs()[0].cr_group_render(self._g, C.byref(cam), C.byref(p), _ptr(out)), "cr_group_render")
         return out
 
+    def render_layers(self, cam: CrCamera, p: CrRenderParams, nlayers: int) -> np.ndarray:
+        """cr_group_render_layers: layers p.layer .. + nlayers - 1 in pass groups across the group."""
+        out = np.zeros((p.yres, p.xres, 3), np.float32)
+        self._chk(libs()[0].cr_group_render_layers(self._g, C.byref(cam), C.byref(p), int(nlayers), _ptr(out)),
+                  "cr_group_render_layers")
+        return out
+
     def counters(self) -> dict:
         c = CrCounters()
         libs()[0].cr_group_get_counters(self._g, C.byref(c))
@@ -748,6 +777,12 @@ class RayTracer:
             raise RuntimeError("rayTrace: " + _host_err())
 
     ray_trace = rayTrace
+
+    def rayTraceLayers(self, n, eye, center, up=(0.0, 1.0, 0.0), yview=1.0):
+        """n rayTrace calls with the same view in pass groups (bit-identical)."""
+        rc = libs()[1].chiaro_raytracer_raytrace_layers(self._h, int(n), _fa(eye), _fa(center), _fa(up), float(yview))
+        if rc:
+            raise RuntimeError("rayTraceLayers: " + _host_err())
 
     @property
     def pixels(self) -> np.ndarray:

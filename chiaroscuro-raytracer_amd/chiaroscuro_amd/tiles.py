@@ -76,7 +76,7 @@ class DistributedFrame:
             raise ValueError("DistributedFrame: nranks %d / rank %d disagree with the process group" % (nranks, rank))
         if gather not in ("torch", "cabi"):
             raise ValueError("DistributedFrame: gather must be 'torch' or 'cabi'")
-        self.dev, self.dist, self.rank, self.gather = dev, dist, rank, gather
+        self.dev, self.dist, self.rank, self.gather, self.device = dev, dist, rank, gather, device
         self.layout = TileLayout(xres, yres, nranks, tile)
         L = self.layout
         f32 = dict(dtype=torch.float32, device=device)
@@ -85,6 +85,7 @@ class DistributedFrame:
         self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), **f32) if split else None
         self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), **f32) if split and rank == 0 else None
         self.tiles_multi = None  # [nlayers][max_tiles][tile][tile][3] of render_layers
+        self.gathered_multi = None  # root: [nranks][nlayers][max_tiles][tile][tile][3] of render_layers
         self._stats_begin()
         if nranks > 1 and gather == "cabi":
             uid = [dev.comm_unique_id() if rank == 0 else None]
@@ -142,15 +143,21 @@ class DistributedFrame:
         small, so on ONE rank the frame is cut into `pieces` (the ranks of a pieces-way
         tile split, each rendered as its own pass of all the layers) -- the smallest
         number whose paths fit one chunk (Device.layers_per_pass).  With several ranks
-        a rank's share is its tiles (pieces = 1) and `layers` what fits it."""
+        a rank's share is its tiles (pieces = 1, the rank's tiles cut into pieces by the
+        device itself) and `layers` what fits every rank: the ranks agree on the
+        smallest plan (an all-reduce MIN -- collective: every rank calls plan_layers), so
+        their per-group gathers pair up."""
         L = self.layout
         want = max(1, int(want))
-        if not hasattr(self.dev, "layers_per_pass") or (L.nranks > 1 and self.gather == "cabi"):
+        if not hasattr(self.dev, "layers_per_pass"):
             return 1, 1
         if L.nranks > 1:  # (cr_render_tiles_layers_device cuts the rank's tiles into pieces itself)
-            if hasattr(self.dev, "layers_per_group"):
-                return self.dev.layers_per_group(params, want), 1
-            return self.dev.layers_per_pass(params, want), 1
+            n = self.dev.layers_per_group(params, want) if hasattr(self.dev, "layers_per_group") \
+                else self.dev.layers_per_pass(params, want)
+            import torch
+            t = torch.tensor([n], dtype=torch.int64, device=self.device)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+            return int(t.item()), 1
         # frame pieces only for scenes with real geometry (cr_scene_triangles; cabi.cpp PIECES_MIN_TRIS)
         max_pieces = min(64, L.ntiles)
         if hasattr(self.dev, "scene_triangles") and self.dev.scene_triangles() < 1024:
@@ -164,18 +171,18 @@ class DistributedFrame:
         return 1, 1
 
     def render_layers(self, cam, params, nlayers: int, stream: int = 0, pieces: int = 1):
-        """Layers params.layer .. + nlayers - 1 as ONE render pass of my tiles (of each of
-        `pieces` frame pieces on a single rank) -- cr_render_layers_device /
-        cr_render_tiles_layers_device, bit-identical to nlayers render_layer calls --
-        then per layer the gather and blend.  (nlayers, pieces) from plan_layers; the
-        library's own gather ("cabi") renders layer by layer.  last_stats() sums the
+        """Layers params.layer .. + nlayers - 1 as ONE render pass group of my tiles (of each
+        of `pieces` frame pieces on a single rank) -- cr_render_layers_device /
+        cr_render_tiles_layers_device, bit-identical to nlayers render_layer calls -- then
+        ONE gather of the group's tile buffers and one blend of its layers at rank 0
+        (cr_blend_tiles_layers_device; the library's own gather: cr_render_dist_layers_device
+        does all of it).  (nlayers, pieces) from plan_layers.  last_stats() sums the
         passes' counters."""
         import torch
         L = self.layout
         self._stats_begin()
-        if nlayers == 1 and pieces == 1 or (L.nranks > 1 and self.gather == "cabi"):
-            for j in range(nlayers):
-                self._render_one(cam, _with_layer(params, params.layer + j), stream)
+        if nlayers == 1 and pieces == 1:
+            self._render_one(cam, params, stream)
             return
         if (params.rank, params.nranks, params.tile or 32, params.xres, params.yres) != \
                 (self.rank, L.nranks, L.tile, L.xres, L.yres):
@@ -189,17 +196,32 @@ class DistributedFrame:
             return
         if pieces != 1:
             raise ValueError("render_layers: frame pieces on a single rank only")
+        if self.gather == "cabi":
+            self.dev.render_dist_layers_device(cam, params, nlayers, self.frame.data_ptr() if self.rank == 0 else 0,
+                                               stream)
+            self._stats_add()
+            return
         if self.tiles_multi is None or self.tiles_multi.shape[0] < nlayers:
             self.tiles_multi = torch.zeros((nlayers,) + tuple(self.tiles.shape), dtype=self.tiles.dtype,
                                            device=self.tiles.device)
-        self.dev.render_tiles_layers_device(cam, params, nlayers, self.tiles_multi.data_ptr(), stream)
+        mine = self.tiles_multi[:nlayers]  # [nlayers][max_tiles][T][T][3], contiguous
+        self.dev.render_tiles_layers_device(cam, params, nlayers, mine.data_ptr(), stream)
         self._stats_add()
-        for j in range(nlayers):
-            self.dist.gather(self.tiles_multi[j], [self.gathered[r] for r in range(L.nranks)] if self.rank == 0
-                             else None, dst=0)
-            if self.rank == 0:
-                self.dev.blend_tiles_device(_with_layer(params, params.layer + j), self.gathered.data_ptr(),
-                                            self.frame.data_ptr(), stream)
+        if not hasattr(self.dev, "blend_tiles_layers_device"):  # (a device with the one-layer blend only)
+            for j in range(nlayers):
+                self.dist.gather(mine[j], [self.gathered[r] for r in range(L.nranks)] if self.rank == 0 else None,
+                                 dst=0)
+                if self.rank == 0:
+                    self.dev.blend_tiles_device(_with_layer(params, params.layer + j), self.gathered.data_ptr(),
+                                                self.frame.data_ptr(), stream)
+            return
+        # one gather of the whole group: rank r's nlayers buffers land at the root's [r], then one blend
+        if self.rank == 0 and (self.gathered_multi is None or self.gathered_multi.shape[1] != nlayers):
+            self.gathered_multi = torch.zeros((L.nranks,) + tuple(mine.shape), dtype=mine.dtype, device=mine.device)
+        self.dist.gather(mine, [self.gathered_multi[r] for r in range(L.nranks)] if self.rank == 0 else None, dst=0)
+        if self.rank == 0:
+            self.dev.blend_tiles_layers_device(params, nlayers, self.gathered_multi.data_ptr(), self.frame.data_ptr(),
+                                               stream)
 
     # the device's counters, pass time and trace stats summed over the passes of the last
     # render_layer(s) call

@@ -811,29 +811,6 @@ int cr_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float 
     return CR_OK;
 }
 
-// the counters, pass time and trace stats of several passes, summed (pass groups)
-struct PassSum {
-    uint64_t ctr[sizeof(cr_counters) / sizeof(uint64_t)] = {};
-    float ms = 0.f;
-    cr_trace_stats ts{};
-    void add(const cr_ctx *c) {
-        const uint64_t *h = (const uint64_t *)&c->last;
-        for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) ctr[i] += h[i];
-        ms += c->last_ms;
-        for (int kind = 0; kind < 4; kind++) {
-            ts.launches[kind] += c->last_trace.launches[kind];
-            ts.ms[kind] += c->last_trace.ms[kind];
-            ts.inner[kind] += c->last_trace.inner[kind];
-            ts.leaf[kind] += c->last_trace.leaf[kind];
-            ts.tritest[kind] += c->last_trace.tritest[kind];
-        }
-    }
-    void store(cr_ctx *c) const {
-        std::memcpy(&c->last, ctr, sizeof(cr_counters));
-        c->last_ms = ms;
-        c->last_trace = ts;
-    }
-};
 
 // cr_render over nlayers layers in pass groups: up to LAYER_GROUP layers per pass, the frame cut
 // into the fewest tile-split pieces whose paths fit one chunk (DistributedFrame.plan_layers)
@@ -846,7 +823,8 @@ uint32_t cr_scene_triangles(cr_ctx *c) { return c && c->has_scene ? c->n_tris : 
 // The largest nl <= want (>= 1) whose paths fit one chunk when p's share is cut into *m pieces (the
 // fewest; scenes of at least PIECES_MIN_TRIS triangles only): for the whole frame (nranks 1) the
 // ranks of an m-way split, for rank r of N the ranks r + kN of an N * m split
-static uint32_t group_plan(cr_ctx *c, const cr_render_params *p, uint32_t want, uint32_t *m_out) {
+} // extern "C"
+uint32_t crx::group_layers(cr_ctx *c, const cr_render_params *p, uint32_t want, uint32_t *m_out) {
     *m_out = 1;
     const uint32_t N = p->nranks ? p->nranks : 1;
     const uint32_t share = cr_tiles_for_rank(p, p->rank);
@@ -863,11 +841,12 @@ static uint32_t group_plan(cr_ctx *c, const cr_render_params *p, uint32_t want, 
         }
     return 1;
 }
+extern "C" {
 
 uint32_t cr_layers_per_group(cr_ctx *c, const cr_render_params *p, uint32_t want) {
     if (!c || c->device < 0 || !c->has_scene || !p || want < 1 || check_params(c, p) != CR_OK) return 1;
     uint32_t m = 1;
-    return group_plan(c, p, want, &m);
+    return group_layers(c, p, want, &m);
 }
 
 int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
@@ -890,10 +869,10 @@ int cr_render_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *p,
         c->accum_elems = elems;
         HIPCHK(hipMemset(c->d_accum, 0, elems * sizeof(float)));
     }
-    PassSum sum;
+    PassTotals sum;
     for (uint32_t done = 0; done < nlayers;) {
         uint32_t m = 1;
-        const uint32_t nl = group_plan(c, &q, std::min(LAYER_GROUP, nlayers - done), &m);
+        const uint32_t nl = group_layers(c, &q, std::min(LAYER_GROUP, nlayers - done), &m);
         for (uint32_t k = 0; k < m; k++) {
             cr_render_params t = q;
             t.layer = q.layer + done;
@@ -969,10 +948,10 @@ int cr_render_tiles_layers_device(cr_ctx *c, const cr_camera *cam, const cr_rend
     // the rank's tiles in pieces (ranks r + kN of an N * m split: every tile slot keeps its pixels
     // for any split of more than one rank), each written into the rank's compact buffer
     uint32_t m = 1;
-    if (group_plan(c, p, nlayers, &m) != nlayers)
+    if (group_layers(c, p, nlayers, &m) != nlayers)
         return fail(c, CR_E_INVALID, "layers per pass: the rank's share does not fit in pieces");
     const uint64_t stride = (uint64_t)cr_tiles_for_rank(p, 0) * tile_of(p) * tile_of(p) * 3;
-    PassSum sum;
+    PassTotals sum;
     for (uint32_t k = 0; k < m; k++) {
         cr_render_params t = *p;
         t.rank = p->rank + k * p->nranks;
@@ -988,9 +967,15 @@ int cr_render_tiles_layers_device(cr_ctx *c, const cr_camera *cam, const cr_rend
 
 int cr_blend_tiles_device(cr_ctx *c, const cr_render_params *p, const float *d_gathered, float *d_frame,
                           void *stream) {
+    return cr_blend_tiles_layers_device(c, p, 1, d_gathered, d_frame, stream);
+}
+
+int cr_blend_tiles_layers_device(cr_ctx *c, const cr_render_params *p, uint32_t nlayers, const float *d_gathered,
+                                 float *d_frame, void *stream) {
     if (!c) return CR_E_INVALID;
     if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
-    if (!p || !d_gathered || !d_frame || p->nranks < 1 || p->layer < 1) return fail(c, CR_E_INVALID, "bad blend args");
+    if (!p || !d_gathered || !d_frame || p->nranks < 1 || p->layer < 1 || nlayers < 1)
+        return fail(c, CR_E_INVALID, "bad blend args");
     HIPCHK(hipSetDevice(c->device));
     cr::BlendArgs B{};
     B.gathered = d_gathered;
@@ -1002,6 +987,7 @@ int cr_blend_tiles_device(cr_ctx *c, const cr_render_params *p, const float *d_g
     B.nranks = p->nranks;
     B.max_tiles = cr_tiles_for_rank(p, 0);
     B.layer = p->layer;
+    B.nl = nlayers;
     int e = cr::launch_blend(B, (hipStream_t)stream);
     if (e) return hip_fail(c, (hipError_t)e, "blend kernel launch");
     return CR_OK;

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -152,4 +153,30 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                uint32_t nl = 1, uint32_t piece_k = 0, uint32_t piece_m = 1, uint64_t stride = 0);
 // group.cpp: the communicator and buffers of the multi-process split (cr_destroy)
 void release_dist(cr_ctx *c);
+// The largest nl <= want (>= 1) whose paths fit one chunk when p's share (the frame for nranks 1, else rank
+// p->rank's tiles) is cut into *m_out pieces, the fewest (cabi.cpp; cr_layers_per_group)
+uint32_t group_layers(cr_ctx *c, const cr_render_params *p, uint32_t want, uint32_t *m_out);
+// the counters, pass time and trace stats of several passes, summed (pass groups)
+struct PassTotals {
+    uint64_t ctr[sizeof(cr_counters) / sizeof(uint64_t)] = {};
+    float ms = 0.f;
+    cr_trace_stats ts{};
+    void add(const cr_ctx *c) {
+        const uint64_t *h = (const uint64_t *)&c->last;
+        for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) ctr[i] += h[i];
+        ms += c->last_ms;
+        for (int kind = 0; kind < 4; kind++) {
+            ts.launches[kind] += c->last_trace.launches[kind];
+            ts.ms[kind] += c->last_trace.ms[kind];
+            ts.inner[kind] += c->last_trace.inner[kind];
+            ts.leaf[kind] += c->last_trace.leaf[kind];
+            ts.tritest[kind] += c->last_trace.tritest[kind];
+        }
+    }
+    void store(cr_ctx *c) const {
+        std::memcpy(&c->last, ctr, sizeof(cr_counters));
+        c->last_ms = ms;
+        c->last_trace = ts;
+    }
+};
 } // namespace crx

@@ -90,7 +90,30 @@ static cr::BlendArgs blend_args(const cr_render_params *p, const float *gathered
     B.nranks = p->nranks;
     B.max_tiles = cr_tiles_for_rank(p, 0);
     B.layer = p->layer;
+    B.nl = 1;
     return B;
+}
+
+// Layers q->layer .. + nlayers - 1 of the whole frame (nranks 1) blended into d_frame on st, in the
+// pieces cr_layers_per_group plans (cr_render_layers' scheme on a device frame); counters summed.
+static int frame_layers(cr_ctx *c, const cr_camera *cam, const cr_render_params *q, uint32_t nlayers, float *d_frame,
+                        hipStream_t st) {
+    cr_render_params f = *q;
+    f.rank = 0;
+    f.nranks = 1;
+    uint32_t m = 1;
+    if (nlayers > 1 && group_layers(c, &f, nlayers, &m) != nlayers)
+        return fail(c, CR_E_INVALID, "layers per pass: the frame does not fit in pieces");
+    PassTotals sum;
+    for (uint32_t k = 0; k < m; k++) {
+        cr_render_params t = f;
+        t.rank = k;
+        t.nranks = m;
+        if (int rc = run_render(c, cam, &t, d_frame, cr::MODE_BLEND, st, nlayers)) return rc;
+        sum.add(c);
+    }
+    sum.store(c);
+    return CR_OK;
 }
 
 } // namespace crx
@@ -200,6 +223,56 @@ int cr_render_dist_device(cr_ctx *c, const cr_camera *cam, const cr_render_param
     if (root) {
         const int e = cr::launch_blend(blend_args(&q, c->d_gathered, d_frame), st);
         if (e) return hip_fail(c, (hipError_t)e, "blend kernel launch");
+    }
+    return wait_comm(c, c->comm, st, "tile gather");
+}
+
+int cr_render_dist_layers_device(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                                 float *d_frame, void *stream) {
+    if (!c) return CR_E_INVALID;
+    if (c->device < 0) return fail(c, CR_E_HIP, c->err.empty() ? "no device" : c->err);
+    if (!p || !cam || nlayers < 1) return fail(c, CR_E_INVALID, "null camera/params or no layers");
+    if (!c->comm) return fail(c, CR_E_INVALID, "no communicator (cr_comm_init)");
+    if (nlayers == 1) return cr_render_dist_device(c, cam, p, d_frame, stream);
+    cr_render_params q = *p;
+    q.rank = (uint32_t)c->comm_rank;
+    q.nranks = (uint32_t)c->comm_nranks;
+    const bool root = c->comm_rank == 0;
+    if (root && !d_frame) return fail(c, CR_E_INVALID, "root needs a frame");
+    if (int rc = check_params(c, &q)) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (q.nranks == 1) return frame_layers(c, cam, &q, nlayers, d_frame, st);
+    // every rank's nlayers compact buffers in one piece: [nlayers][slot], the root's in its slot 0 of
+    // [nranks][nlayers][slot]; ONE grouped send / receive of the whole group, one blend of its layers
+    const size_t slot = slot_elems(&q), span = slot * nlayers;
+    float *mine;
+    if (root) {
+        if (int r = grow(c, (void **)&c->d_gathered, c->gathered_bytes, span * q.nranks * sizeof(float))) return r;
+        mine = c->d_gathered;
+    } else {
+        if (int r = grow(c, (void **)&c->d_tiles, c->tiles_bytes, span * sizeof(float))) return r;
+        mine = c->d_tiles;
+    }
+    if (int rc = cr_render_tiles_layers_device(c, cam, &q, nlayers, mine, st)) return rc;
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) {
+        if (root) {
+            for (uint32_t k = 1; k < q.nranks && (r == ncclSuccess || r == ncclInProgress); k++)
+                r = ncclRecv(c->d_gathered + k * span, span, ncclFloat32, (int)k, c->comm, st);
+        } else {
+            r = ncclSend(mine, span, ncclFloat32, 0, c->comm, st);
+        }
+        if (r == ncclInProgress) r = ncclSuccess;
+        ncclResult_t e = ncclGroupEnd();
+        if (e == ncclInProgress) e = nccl_settle(c->comm);
+        if (r == ncclSuccess) r = e;
+    }
+    if (r != ncclSuccess) return nccl_fail(c, r, "tile gather");
+    if (root) {
+        cr::BlendArgs B = blend_args(&q, c->d_gathered, d_frame);
+        B.nl = nlayers;
+        if (const int e = cr::launch_blend(B, st)) return hip_fail(c, (hipError_t)e, "blend kernel launch");
     }
     return wait_comm(c, c->comm, st, "tile gather");
 }
@@ -335,17 +408,88 @@ int cr_group_set_option(cr_group *g, const char *key, int64_t value) {
     return CR_OK;
 }
 
-int cr_group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out) {
+// One pass group of the whole group: layers q->layer .. + nl - 1 (q->nranks = the group size), every
+// rank its tiles of all nl layers (one pass, in pieces when they do not fit one chunk), the gather of
+// the nl compact buffers per rank into the root's [nranks][nl][slot], one blend of the nl layers into
+// the root's frame; counters and rank times added to sum / ms.
+static int group_pass(cr_group *g, const cr_camera *cam, const cr_render_params *q, uint32_t nl, PassTotals *sum,
+                      std::vector<float> &ms) {
+    const uint32_t n = (uint32_t)g->ctx.size();
+    hipStream_t st0 = g->ctx[0]->stream;
+    if (n == 1) {
+        if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
+        cr_render_params f = *q;
+        if (int rc = nl == 1 ? run_render(g->ctx[0], cam, &f, g->frame, cr::MODE_BLEND, st0)
+                             : frame_layers(g->ctx[0], cam, &f, nl, g->frame, st0))
+            return gctx_fail(g, 0, rc);
+        sum[0].add(g->ctx[0]);
+        ms[0] += g->ctx[0]->last_ms;
+        return CR_OK;
+    }
+    const size_t slot = slot_elems(q), span = slot * nl;
+    if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
+    if (int rc = grow(g->ctx[0], (void **)&g->gathered, g->gathered_bytes, span * n * sizeof(float)))
+        return gctx_fail(g, 0, rc);
+    int rc = for_ranks(g, [&](size_t r) -> int {
+        cr_ctx *c = g->ctx[r];
+        if (hipSetDevice(g->devices[r]) != hipSuccess) return fail(c, CR_E_HIP, "hipSetDevice");
+        float *mine = g->gathered;
+        if (r > 0) {
+            if (int e = grow(c, (void **)&g->tiles[r], g->tiles_bytes[r], span * sizeof(float))) return e;
+            mine = g->tiles[r];
+        }
+        cr_render_params qr = *q;
+        qr.rank = (uint32_t)r;
+        const int e = nl == 1 ? run_render(c, cam, &qr, mine, cr::MODE_TILES, c->stream)
+                              : cr_render_tiles_layers_device(c, cam, &qr, nl, mine, c->stream);
+        if (!e) {
+            sum[r].add(c);
+            ms[r] += c->last_ms;
+        }
+        return e;
+    });
+    if (rc) return rc;
+    if (g->comm.empty()) { // a device listed twice: device-to-device copies into the root's slots
+        for (uint32_t r = 1; r < n; r++)
+            if (hipMemcpyPeerAsync(g->gathered + r * span, g->devices[0], g->tiles[r], g->devices[r],
+                                   span * sizeof(float), st0) != hipSuccess)
+                return gfail(g, CR_E_HIP, "tile copy");
+    } else {
+        ncclResult_t r = ncclGroupStart();
+        for (uint32_t k = 1; k < n && r == ncclSuccess; k++) {
+            r = ncclSend(g->tiles[k], span, ncclFloat32, 0, g->comm[k], g->ctx[k]->stream);
+            if (r == ncclSuccess) r = ncclRecv(g->gathered + k * span, span, ncclFloat32, (int)k, g->comm[0], st0);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r == ncclSuccess) r = e;
+        if (r != ncclSuccess) return gfail(g, CR_E_COMM, std::string("tile gather: ") + ncclGetErrorString(r));
+    }
+    if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
+    cr::BlendArgs B = blend_args(q, g->gathered, g->frame);
+    B.nl = nl;
+    const int e = cr::launch_blend(B, st0);
+    if (e) return gfail(g, CR_E_HIP, std::string("blend kernel launch: ") + hipGetErrorString((hipError_t)e));
+    for (uint32_t k = 0; k < n; k++) {
+        hipSetDevice(g->devices[k]);
+        if (int w = wait_comm(g->ctx[k], g->comm.empty() ? nullptr : g->comm[k], g->ctx[k]->stream, "tile gather"))
+            return gctx_fail(g, k, w);
+    }
+    hipSetDevice(g->devices[0]);
+    return CR_OK;
+}
+
+// cr_group_render(_layers): layers p->layer .. + nlayers - 1, pass groups of up to `group` layers
+static int group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                        uint32_t group, float *accum_rgb_out) {
     if (!g) return CR_E_INVALID;
     if (!group_ok(g)) return gfail(g, CR_E_HIP, g->err.empty() ? "group not initialised" : g->err);
-    if (!cam || !p || !accum_rgb_out) return gfail(g, CR_E_INVALID, "null camera/params/output");
+    if (!cam || !p || !accum_rgb_out || nlayers < 1) return gfail(g, CR_E_INVALID, "null camera/params/output");
     const uint32_t n = (uint32_t)g->ctx.size();
     cr_render_params q = *p;
     q.rank = 0;
     q.nranks = n;
     if (int rc = check_params(g->ctx[0], &q)) return gctx_fail(g, 0, rc);
     const size_t elems = (size_t)q.xres * q.yres * 3;
-    hipStream_t st0 = g->ctx[0]->stream;
     if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
     if (elems != g->frame_elems) {
         if (g->frame) hipFree(g->frame);
@@ -355,64 +499,43 @@ int cr_group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p
         g->frame_elems = elems;
         if (hipMemset(g->frame, 0, elems * sizeof(float)) != hipSuccess) return gfail(g, CR_E_HIP, "frame");
     }
-    if (n == 1) {
-        if (int rc = run_render(g->ctx[0], cam, &q, g->frame, cr::MODE_BLEND, st0)) return gctx_fail(g, 0, rc);
-    } else {
-        const size_t slot = slot_elems(&q);
-        if (int rc = grow(g->ctx[0], (void **)&g->gathered, g->gathered_bytes, slot * n * sizeof(float)))
-            return gctx_fail(g, 0, rc);
-        int rc = for_ranks(g, [&](size_t r) -> int {
-            cr_ctx *c = g->ctx[r];
-            if (hipSetDevice(g->devices[r]) != hipSuccess) return fail(c, CR_E_HIP, "hipSetDevice");
-            float *mine = g->gathered;
-            if (r > 0) {
-                if (int e = grow(c, (void **)&g->tiles[r], g->tiles_bytes[r], slot * sizeof(float))) return e;
-                mine = g->tiles[r];
-            }
-            cr_render_params qr = q;
-            qr.rank = (uint32_t)r;
-            return run_render(c, cam, &qr, mine, cr::MODE_TILES, c->stream);
-        });
-        if (rc) return rc;
-        if (g->comm.empty()) { // a device listed twice: device-to-device copies into the root's slots
-            for (uint32_t r = 1; r < n; r++)
-                if (hipMemcpyPeerAsync(g->gathered + r * slot, g->devices[0], g->tiles[r], g->devices[r],
-                                       slot * sizeof(float), st0) != hipSuccess)
-                    return gfail(g, CR_E_HIP, "tile copy");
-        } else {
-            ncclResult_t r = ncclGroupStart();
-            for (uint32_t k = 1; k < n && r == ncclSuccess; k++) {
-                r = ncclSend(g->tiles[k], slot, ncclFloat32, 0, g->comm[k], g->ctx[k]->stream);
-                if (r == ncclSuccess)
-                    r = ncclRecv(g->gathered + k * slot, slot, ncclFloat32, (int)k, g->comm[0], st0);
-            }
-            const ncclResult_t e = ncclGroupEnd();
-            if (r == ncclSuccess) r = e;
-            if (r != ncclSuccess) return gfail(g, CR_E_COMM, std::string("tile gather: ") + ncclGetErrorString(r));
+    std::vector<PassTotals> sum(n);
+    std::vector<float> ms(n, 0.f);
+    for (uint32_t done = 0; done < nlayers;) {
+        cr_render_params t = q;
+        t.layer = q.layer + done;
+        // the group's size: what every rank's share fits (each rank's tiles in up to 64 pieces)
+        uint32_t nl = std::min(group, nlayers - done);
+        for (uint32_t r = 0; r < n && nl > 1; r++) {
+            cr_render_params tr = t;
+            tr.rank = r;
+            if (n == 1) tr.nranks = 1;
+            uint32_t m = 1;
+            nl = std::min(nl, group_layers(g->ctx[r], &tr, nl, &m));
         }
-        if (hipSetDevice(g->devices[0]) != hipSuccess) return gfail(g, CR_E_HIP, "hipSetDevice");
-        const int e = cr::launch_blend(blend_args(&q, g->gathered, g->frame), st0);
-        if (e) return gfail(g, CR_E_HIP, std::string("blend kernel launch: ") + hipGetErrorString((hipError_t)e));
-        for (uint32_t k = 0; k < n; k++) {
-            hipSetDevice(g->devices[k]);
-            if (int w = wait_comm(g->ctx[k], g->comm.empty() ? nullptr : g->comm[k], g->ctx[k]->stream,
-                                  "tile gather"))
-                return gctx_fail(g, k, w);
-        }
-        hipSetDevice(g->devices[0]);
+        if (int rc = group_pass(g, cam, &t, nl, sum.data(), ms)) return rc;
+        done += nl;
     }
     if (hipMemcpy(accum_rgb_out, g->frame, elems * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
         return gfail(g, CR_E_HIP, "frame copy");
-    // counters summed over ranks; each rank's pass time
-    cr_counters sum{};
-    uint64_t *s = (uint64_t *)&sum;
+    // counters summed over ranks (and groups); each rank's pass time
+    cr_counters tot{};
+    uint64_t *s = (uint64_t *)&tot;
     for (uint32_t k = 0; k < n; k++) {
-        const uint64_t *v = (const uint64_t *)&g->ctx[k]->last;
-        for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) s[i] += v[i];
-        g->rank_ms[k] = g->ctx[k]->last_ms;
+        for (size_t i = 0; i < sizeof(cr_counters) / sizeof(uint64_t); i++) s[i] += sum[k].ctr[i];
+        g->rank_ms[k] = ms[k];
     }
-    g->last = sum;
+    g->last = tot;
     return CR_OK;
+}
+
+int cr_group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out) {
+    return group_render(g, cam, p, 1, 1, accum_rgb_out);
+}
+
+int cr_group_render_layers(cr_group *g, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                           float *accum_rgb_out) {
+    return group_render(g, cam, p, nlayers, 32, accum_rgb_out);
 }
 
 int cr_group_set_accumulator(cr_group *g, uint32_t xres, uint32_t yres, const float *rgb) {

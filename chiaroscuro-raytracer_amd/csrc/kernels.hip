@@ -227,12 +227,18 @@ __global__ void __launch_bounds__(256) blend_tiles_kernel(BlendArgs B) {
     const uint32_t T = B.tile;
     const uint32_t s = tile_slot(x / T, y / T, B.tiles_x, B.nranks);
     const uint32_t r = s % B.nranks, lt = s / B.nranks;
-    const size_t src = ((size_t)r * B.max_tiles + lt) * T * T + (y % T) * T + (x % T);
-    const f3 m = mk(B.gathered[3 * src], B.gathered[3 * src + 1], B.gathered[3 * src + 2]);
+    const size_t layer_elems = (size_t)B.max_tiles * T * T; // one rank's buffer of one layer, in pixels
+    const size_t src = ((size_t)r * B.nl * B.max_tiles + lt) * T * T + (y % T) * T + (x % T);
     float *o = B.frame + 3 * (size_t)i;
-    const f3 old = (B.layer > 1) ? mk(o[0], o[1], o[2]) : mk(0.f, 0.f, 0.f);
-    // rayTracer.cpp:64 with mean = temp * invSamples already applied by the rank
-    const f3 nw = divs(add(muls(old, (float)(B.layer - 1)), m), (float)B.layer);
+    f3 nw = (B.layer > 1) ? mk(o[0], o[1], o[2]) : mk(0.f, 0.f, 0.f);
+    // rayTracer.cpp:64 per layer, in layer order (mean = temp * invSamples already applied by the
+    // rank); the running value stays in registers, bit-identical to one blend launch per layer
+    for (uint32_t j = 0; j < B.nl; j++) {
+        const size_t q = 3 * (src + j * layer_elems);
+        const f3 m = mk(B.gathered[q], B.gathered[q + 1], B.gathered[q + 2]);
+        const uint32_t L = B.layer + j;
+        nw = divs(add(muls(nw, (float)(L - 1)), m), (float)L);
+    }
     o[0] = nw.x;
     o[1] = nw.y;
     o[2] = nw.z;

@@ -315,10 +315,12 @@ struct QueryArgs {
     unsigned long long *counters;
 };
 
+// gathered: [nranks][nl][max_tiles][T][T][3] -- every rank's compact tile buffers of layers
+// layer .. layer + nl - 1, blended into the frame in layer order by one launch
 struct BlendArgs {
     const float *gathered;
     float *frame;
-    uint32_t xres, yres, tile, tiles_x, nranks, max_tiles, layer;
+    uint32_t xres, yres, tile, tiles_x, nranks, max_tiles, layer, nl;
 };
 
 // RayTracer::normalizeImage's per-pixel transform (src/rayTracer.cpp:207-221)

@@ -267,6 +267,18 @@ int chiaro_raytracer_raytrace(chiaro_raytracer *r, const float eye[3], const flo
         CR_E_HIP);
 }
 
+int chiaro_raytracer_raytrace_layers(chiaro_raytracer *r, uint32_t n, const float eye[3], const float center[3],
+                                     const float up[3], float yview) {
+    if (!r || n < 1) return CR_E_INVALID;
+    return guard(
+        [&]() -> int {
+            r->r->rayTraceLayers(n, vec3(eye[0], eye[1], eye[2]), vec3(center[0], center[1], center[2]),
+                                 vec3(up[0], up[1], up[2]), yview);
+            return CR_OK;
+        },
+        CR_E_HIP);
+}
+
 const float *chiaro_raytracer_pixels(const chiaro_raytracer *r) { return r ? r->r->pixelData() : nullptr; }
 const uint8_t *chiaro_raytracer_data(chiaro_raytracer *r) { return r ? r->r->getData() : nullptr; }
 float chiaro_raytracer_maxval(const chiaro_raytracer *r) { return r ? r->r->maxVal : 0.f; }

@@ -105,10 +105,6 @@ void RayTracer::rayTrace(vec3 eye, vec3 center, vec3 up, float yview) { rayTrace
 
 void RayTracer::rayTraceLayers(unsigned n, vec3 eye, vec3 center, vec3 up, float yview) {
     if (n < 1) return;
-    if (group_ && n > 1) { // the GPU group renders layer by layer
-        for (unsigned i = 0; i < n; i++) rayTraceLayers(1, eye, center, up, yview);
-        return;
-    }
     // rayTracer.cpp:24 -- including the reference's `(lastUp == lastUp)`: a
     // change of `up` alone does not reset the accumulation.
     const bool newLayer = (eye == lastEye) && (center == lastCenter) && (lastUp == lastUp) && (yview == lastYview);
@@ -144,10 +140,12 @@ void RayTracer::rayTraceLayers(unsigned n, vec3 eye, vec3 center, vec3 up, float
     // (cr_render_layers blends group after group): the next rayTrace then starts over at layer 1,
     // whose blend weight (L - 1 = 0) discards whatever the accumulator holds
     if (group_) {
-        if (cr_group_render(group_, &cam, &p, pixels.data()) != CR_OK) {
+        if ((n == 1 ? cr_group_render(group_, &cam, &p, pixels.data())
+                    : cr_group_render_layers(group_, &cam, &p, n, pixels.data())) != CR_OK) {
             layers_ = 0;
             throw std::runtime_error(std::string("chiaro: render failed: ") + cr_group_last_error(group_));
         }
+        layers_ += n - 1; // layers p.layer .. p.layer + n - 1 are in the frame
         cr_group_get_counters(group_, &counters_);
     } else {
         if ((n == 1 ? cr_render(ctx_, &cam, &p, pixels.data()) : cr_render_layers(ctx_, &cam, &p, n, pixels.data())) !=

@@ -33,7 +33,8 @@ class RayTracer {
     /* Fill pixels with rays shot on screen centered between eye and center. */
     void rayTrace(vec3 eye, vec3 center, vec3 up = vec3(0.f, 1.f, 0.f), float yview = 1.f);
     /* This build: n calls of rayTrace with the same view, rendered as pass groups
-     * (cr_render_layers: several layers per pass, bit-identical; one GPU, else layer by layer). */
+     * (cr_render_layers / cr_group_render_layers with the `gpus` key: several layers per pass group,
+     * bit-identical). */
     void rayTraceLayers(unsigned n, vec3 eye, vec3 center, vec3 up = vec3(0.f, 1.f, 0.f), float yview = 1.f);
     /* Get RGB (24 bits per pixel) image location. */
     uint8_t *getData();

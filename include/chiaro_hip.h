@@ -209,6 +209,12 @@ int cr_render_tiles_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_pa
  * layer p->layer into d_frame [yres][xres][3]. */
 int cr_blend_tiles_device(cr_ctx *ctx, const cr_render_params *p, const float *d_gathered, float *d_frame,
                           void *stream);
+/* The same for layers p->layer .. + nlayers - 1 in ONE launch: d_gathered =
+ * [nranks][nlayers][max_tiles][tile][tile][3] (rank r's nlayers compact buffers, as
+ * cr_render_tiles_layers_device writes them, at slot r); each pixel blended layer after layer
+ * in order, bit-identical to nlayers cr_blend_tiles_device calls. */
+int cr_blend_tiles_layers_device(cr_ctx *ctx, const cr_render_params *p, uint32_t nlayers, const float *d_gathered,
+                                 float *d_frame, void *stream);
 uint32_t cr_tiles_for_rank(const cr_render_params *p, uint32_t rank);
 
 /* Several progressive layers in ONE render pass (wavefront kernel): layers p->layer ..
@@ -323,6 +329,14 @@ int cr_comm_destroy(cr_ctx *ctx);
  * Returns when the layer is complete on this rank's stream. */
 int cr_render_dist_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, float *d_frame,
                           void *stream);
+/* Pass groups over the communicator: layers p->layer .. + nlayers - 1 of this rank's tiles in one
+ * render pass group (cr_render_tiles_layers_device: the rank's tiles in pieces when they do not fit
+ * one chunk), ONE grouped send / receive of all nlayers compact buffers to rank 0 and one blend of
+ * the layers there (cr_blend_tiles_layers_device); bit-identical to nlayers cr_render_dist_device
+ * calls.  nlayers must fit: at most min over the ranks of cr_layers_per_group -- every rank must
+ * pass the same nlayers (the caller agrees on it, e.g. an all-reduce MIN). */
+int cr_render_dist_layers_device(cr_ctx *ctx, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                                 float *d_frame, void *stream);
 
 /* One process driving N GPUs: a ctx per device (devices NULL -> 0..ngpus-1), the
  * passes on one host thread per GPU, grouped RCCL send / receive to rank 0.  A
@@ -345,6 +359,13 @@ int cr_group_set_option(cr_group *g, const char *key, int64_t value); /* on ever
  * ignored, p->tile used), blended into the root's accumulator, copied to
  * accum_rgb_out [yres][xres][3] (host). */
 int cr_group_render(cr_group *g, const cr_camera *cam, const cr_render_params *p, float *accum_rgb_out);
+/* cr_group_render of layers p->layer .. + nlayers - 1 in pass groups (cr_render_layers across the
+ * group): per group of up to 32 layers -- as many as every rank's tiles fit (min over the ranks of
+ * cr_layers_per_group) -- each rank renders its tiles of all of them in one pass group, one gather
+ * of the group's buffers and one blend of its layers at the root; bit-identical to nlayers
+ * cr_group_render calls.  Counters and cr_group_rank_ms sum over the groups. */
+int cr_group_render_layers(cr_group *g, const cr_camera *cam, const cr_render_params *p, uint32_t nlayers,
+                           float *accum_rgb_out);
 int cr_group_get_counters(cr_group *g, cr_counters *out); /* summed over the ranks */
 int cr_group_rank_ms(cr_group *g, float *ms_out);          /* [ngpus] each rank's last pass (HIP events) */
 /* rank's ctx (rank 0: the root, which also answers cr_intersect*), NULL if out of range */

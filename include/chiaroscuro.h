@@ -77,6 +77,10 @@ void chiaro_kdtree_destroy(chiaro_kdtree *k);
 chiaro_raytracer *chiaro_raytracer_create(chiaro_model *m, chiaro_scene *s, int device);
 int chiaro_raytracer_raytrace(chiaro_raytracer *r, const float eye[3], const float center[3], const float up[3],
                               float yview);
+/* n rayTrace calls with the same view (RayTracer::rayTraceLayers), rendered in pass groups -- on one
+ * GPU (cr_render_layers) or across the `gpus` group (cr_group_render_layers); bit-identical. */
+int chiaro_raytracer_raytrace_layers(chiaro_raytracer *r, uint32_t n, const float eye[3], const float center[3],
+                                     const float up[3], float yview);
 const float *chiaro_raytracer_pixels(const chiaro_raytracer *r);
 const uint8_t *chiaro_raytracer_data(chiaro_raytracer *r);
 float chiaro_raytracer_maxval(const chiaro_raytracer *r);

@@ -78,6 +78,16 @@ class OracleDevice:
         g = _view(gathered_ptr, (p.nranks, lay.max_tiles, lay.tile, lay.tile, 3))
         blend_tiles_reference(g, lay, _view(frame_ptr, (p.yres, p.xres, 3)), p.layer)
 
+    def blend_tiles_layers_device(self, p, n, gathered_ptr, frame_ptr, stream=0):
+        """gathered [nranks][n][max_tiles][T][T][3]: layers p.layer .. + n - 1 in order."""
+        from chiaroscuro_amd.tiles import TileLayout, _with_layer
+        from test_distributed import blend_tiles_reference
+        lay = TileLayout(p.xres, p.yres, p.nranks, p.tile)
+        g = _view(gathered_ptr, (p.nranks, n, lay.max_tiles, lay.tile, lay.tile, 3))
+        for j in range(n):
+            blend_tiles_reference(np.ascontiguousarray(g[:, j]), lay, _view(frame_ptr, (p.yres, p.xres, 3)),
+                                  p.layer + j)
+
     def render_device(self, cam, p, frame_ptr, stream=0):
         ys, xs = np.mgrid[0:p.yres, 0:p.xres]
         mean = self._means(cam, p, xs.ravel(), ys.ravel()).reshape(p.yres, p.xres, 3)

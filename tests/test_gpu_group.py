@@ -131,3 +131,93 @@ def test_missing_peers_fail_cleanly(ca):
         ca.Group([0, 1])
     with pytest.raises(RuntimeError, match="device 99"):
         ca.Group([0, 99])
+
+
+@pytest.mark.parametrize("devices,size,nl,paths", [([0], (96, 54, 2), 3, 1 << 28), ([0], (96, 54, 2), 3, 12000),
+                                                   ([0, 0, 0, 0], (310, 180, 2), 4, 1 << 28),
+                                                   ([0, 0, 0, 0], (310, 180, 2), 4, 20000),
+                                                   ([0] * 8, (310, 180, 2), 4, 20000)])
+def test_group_render_pass_groups_bitexact(ca, sponza, devices, size, nl, paths):
+    """cr_group_render_layers: each rank renders its tiles of a whole group of layers in one pass
+    group (in pieces when `wf_paths` makes its share too large for one chunk), ONE gather of the
+    group's buffers and one blend of its layers at the root -- bit-identical to the oracle's layer
+    after layer, counters summed over ranks, passes and layers; then a single layer on top."""
+    x, y, s = size
+    g = ca.Group(devices)
+    g.upload(sponza.kd.describe())
+    g.set_option("counters", 0)
+    g.set_option("wf_paths", paths)
+    cam = sponza.camera(ca, x, y)
+    img = g.render_layers(cam, ca.render_params(x, y, s, 6, SEED, layer=1), nl)
+    gc = g.counters()
+    o, rays = None, 0
+    for layer in range(1, nl + 1):
+        o, oc = sponza.oracle.render(cam.as_array(), x, y, s, 6, SEED, layer=layer, pixels=o)
+        rays += oc["closest"] + oc["shadow"]
+    assert_bitwise(img, o, "group %d ranks, %d layers, wf_paths %d" % (len(devices), nl, paths))
+    assert gc["closest"] + gc["shadow"] == rays and gc["pixels"] == x * y * nl
+    img = g.render(cam, ca.render_params(x, y, s, 6, SEED, layer=nl + 1))
+    o, _ = sponza.oracle.render(cam.as_array(), x, y, s, 6, SEED, layer=nl + 1, pixels=o)
+    assert_bitwise(img, o, "group %d ranks, layer %d after the group" % (len(devices), nl + 1))
+    assert all(t > 0 for t in g.rank_ms())
+    g.close()
+
+
+def test_comm_one_rank_render_dist_layers(ca, sponza):
+    """cr_render_dist_layers_device on a one-rank communicator: the frame's layers in pass groups
+    (frame pieces by wf_paths), then one layer, bit-exact; blend of several layers in one launch
+    (cr_blend_tiles_layers_device) equal to layer-by-layer blends."""
+    import torch
+    x, y, s, nl = 96, 54, 2, 3
+    d = ca.Device(0)
+    d.upload(sponza.kd.describe())
+    d.set_option("counters", 0)
+    d.set_option("wf_paths", 9000)
+    d.comm_init(1, 0, ca.Device.comm_unique_id())
+    cam = sponza.camera(ca, x, y)
+    frame = torch.zeros((y, x, 3), dtype=torch.float32, device="cuda")
+    d.render_dist_layers_device(cam, ca.render_params(x, y, s, 6, SEED, layer=1), nl, frame.data_ptr())
+    torch.cuda.synchronize()
+    o = None
+    for layer in range(1, nl + 1):
+        o, _ = sponza.oracle.render(cam.as_array(), x, y, s, 6, SEED, layer=layer, pixels=o)
+    assert_bitwise(frame.cpu().numpy(), o, "cr_render_dist_layers_device %d layers" % nl)
+    d.comm_destroy()
+    # the multi-layer blend: gathered [nranks][nl][tiles] of a 3-rank split, one launch vs nl launches
+    p = ca.render_params(x, y, s, 6, SEED, layer=2, nranks=3, tile=16)
+    nt = ca.Device.tiles_for_rank(p, 0)
+    gathered = torch.rand((3, nl, nt, 16, 16, 3), dtype=torch.float32, device="cuda")
+    base = torch.rand((y, x, 3), dtype=torch.float32, device="cuda")
+    a, b = base.clone(), base.clone()
+    d.blend_tiles_layers_device(p, nl, gathered.data_ptr(), a.data_ptr())
+    for j in range(nl):
+        q = ca.render_params(x, y, s, 6, SEED, layer=2 + j, nranks=3, tile=16)
+        one = gathered[:, j].contiguous()
+        d.blend_tiles_device(q, one.data_ptr(), b.data_ptr())
+    torch.cuda.synchronize()
+    assert_bitwise(a.cpu().numpy(), b.cpu().numpy(), "multi-layer blend")
+    d.close()
+
+
+def test_raytracer_gpus_key_pass_groups(ca, po, scenes):
+    """RayTracer::rayTraceLayers with the `gpus` key renders through cr_group_render_layers: the
+    layers of a pass group split over 3 ranks equal the one-GPU layers and the oracle's."""
+    rtc = scenes.config_rtc("sponza")
+    out = []
+    for gpus in ("1", "3"):
+        sc = ca.Scene(rtc, "xres", "80", "yres", "45", "samples", "2", "gpus", gpus)
+        i = sc.info
+        rt = ca.RayTracer(ca.Model(sc), sc)
+        rt.rayTraceLayers(3, i["VP"], i["LA"], i["UP"], i["yview"])
+        assert rt.layers == 3
+        rt.rayTrace(i["VP"], i["LA"], i["UP"], i["yview"])
+        assert rt.layers == 4
+        out.append(rt.pixels)
+    assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32)) and out[0].any()
+    m = ca.Model(sc)
+    osc = po.OracleScene(m.triangles(), leaf_size=i["leaf_size"], textures=m.textures())
+    cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], 80, 45).as_array()
+    o = None
+    for L in range(1, 5):
+        o, _ = osc.render(cam, 80, 45, 2, i["k"], i["seed"], layer=L, pixels=o)
+    assert np.array_equal(out[1].view(np.uint32), o.view(np.uint32))

@@ -1,8 +1,8 @@
 """Pass-group planning on the CPU (DistributedFrame.plan_layers): with a stand-in
 device whose chunk holds `cap` paths, one rank cuts the frame into the fewest tile-split pieces
 whose paths fit, scenes below 1024 triangles are never cut, several ranks take what fits their
-share (the library pieces a rank's tiles itself), and the library's own gather renders layer by
-layer.  No GPU: the GPU tests render the plans (tests/test_gpu_parity.py)."""
+share (the library pieces a rank's tiles itself) -- the smallest plan over the ranks, agreed by an
+all-reduce MIN -- with either gather (torch.distributed or the library's own).  No GPU: the GPU tests render the plans (tests/test_gpu_parity.py)."""
 import pytest
 
 
@@ -38,10 +38,14 @@ def params(ca, layer=1, rank=0, nranks=1, spp=128):
     return ca.render_params(1920, 1080, spp, 6, 1, layer=layer, rank=rank, nranks=nranks, tile=32)
 
 
-def frame(dev, nranks=1, rank=0, gather="torch"):
+def frame(dev, nranks=1, rank=0, gather="torch", others=()):
+    """others: the plans (layers) the other ranks bring to plan_layers' all-reduce MIN."""
     from chiaroscuro_amd.tiles import DistributedFrame
 
-    class Dist:  # a process group of nranks (plan_layers never calls it)
+    class Dist:  # a process group of nranks
+        class ReduceOp:
+            MIN = "min"
+
         def get_world_size(self):
             return nranks
 
@@ -50,6 +54,11 @@ def frame(dev, nranks=1, rank=0, gather="torch"):
 
         def broadcast_object_list(self, lst, src=0):
             pass
+
+        def all_reduce(self, t, op=None):
+            assert op == "min"
+            for v in others:
+                t[0] = min(int(t[0]), v)
 
     return DistributedFrame(dev, 1920, 1080, rank, nranks, 32, Dist() if nranks > 1 else None, device="cpu",
                             gather=gather)
@@ -88,4 +97,8 @@ def test_ranks_take_what_fits(ca, nranks):
     fr = frame(dev, nranks=nranks, rank=nranks - 1)
     nl, m = fr.plan_layers(params(ca, rank=nranks - 1, nranks=nranks), 16)
     assert m == 1 and nl == min(16, nranks)
-    assert frame(dev, nranks=nranks, gather="cabi").plan_layers(params(ca, nranks=nranks), 16) == (1, 1)
+    # the library's own gather plans the same groups (cr_render_dist_layers_device)
+    assert frame(dev, nranks=nranks, gather="cabi").plan_layers(params(ca, nranks=nranks), 16) == (nl, 1)
+    # a rank whose share fits fewer layers: every rank takes the smallest plan
+    fr = frame(dev, nranks=nranks, rank=0, others=(nl - 1,) if nl > 1 else ())
+    assert fr.plan_layers(params(ca, rank=0, nranks=nranks), 16) == (max(nl - 1, 1), 1)
