@@ -309,6 +309,8 @@ def main():
                     help="progressive layers per render pass group (DistributedFrame.plan_layers; 1 = one per pass)")
     ap.add_argument("--res", default="", help="WxH override of the config's frame (tests, experiments)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")
+    ap.add_argument("--single-layer-steps", type=int, default=2,
+                    help="after the timed steps: this many one-layer passes (+1 warmup), reported as single_layer_ms")
     ap.add_argument("--parity-rows", type=int, default=8,
                     help="rank 0 checks this many rows of the timed frame (every layer, full spp) bit for bit "
                          "against the oracle after the timed region (0: skip)")
@@ -437,6 +439,25 @@ def run_rank(args, world, backend):
     if args.save_frame and fr.frame is not None:
         import numpy as np
         np.save(args.save_frame, fr.frame.cpu().numpy())
+    # the reference's unit of work, untimed by the line's value: one rayTrace call = ONE layer per
+    # render pass (main.cpp:16, the preview's R key) -- a warmup pass, then --single-layer-steps passes
+    # of the next layers (the frame's rows above are already taken), each bracketed like the steps
+    single_ms = None
+    if args.single_layer_steps > 0:
+        times = []
+        for j in range(args.single_layer_steps + 1):
+            p = ca.render_params(xres, yres, spp, k, seed, layer=layer + j, rank=rank, nranks=world, tile=tile)
+            if dist:
+                dist.barrier()
+            backend.synchronize()
+            ts = time.perf_counter()
+            fr.render_layer(cam, p, stream)
+            backend.synchronize()
+            if dist:
+                dist.barrier()
+            if j:
+                times.append((time.perf_counter() - ts) * 1e3)
+        single_ms = sum(times) / len(times)
     # per rank: wall time, device time of its render passes (HIP events), rays
     mine = torch.tensor([elapsed, totals["kernel_ms"] / max(totals["launches"], 1), totals["rays"]],
                         dtype=torch.float64, device=backend.device)
@@ -611,6 +632,9 @@ def run_rank(args, world, backend):
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            # the same layer as ONE render pass (the reference's unit of work: one rayTrace call), wall
+            # time per pass after the timed region; value and ms_per_step time the pass groups
+            "single_layer_ms": round(single_ms, 3) if single_ms is not None else None,
             "higher_is_better": True,
             "scaling": "strong",  # one fixed frame, tile-split over the ranks
             "vs_baseline": None,

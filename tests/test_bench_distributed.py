@@ -56,6 +56,7 @@ def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
     assert line["config"]["rays"] == rays
     got = np.load(frame)
     assert got.shape == ref.shape and (got.view(np.uint32) == ref.view(np.uint32)).all() and got.mean() > 0
+    assert line["single_layer_ms"] > 0  # one-layer passes after the timed groups (not in value)
     # the bench's own parity check of the timed frame: every row it sampled, every layer, bit for bit
     par = line["parity"]
     assert par["differing"] == 0 and par["layers"] == WARMUP + STEPS and par["spp"] == SPP
