@@ -77,6 +77,11 @@ int grow(cr_ctx *c, void **buf, size_t &cap, size_t need) {
 
 // scenes with fewer triangles default to trace build 18 instead of 26 (fill_args)
 const uint32_t LEAF_CULL_MIN_TRIS = 65536;
+// scenes with fewer triangles trace their queues in append order (wf_sort -1, the default): on a
+// handful of triangles the whole scene stays in cache whatever the order, and the sort plus the
+// trace's reads through the permutation cost more than coherence gains (round 4, cornell_box 1024^2 x
+// 500 spp, two interleaved rounds: sorted 9050 / 8894, unsorted 11140 / 11130 Mray/s)
+const uint32_t SORT_MIN_TRIS = 1024;
 
 void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_render_params *p, float *out, int mode) {
     A.S = c->S;
@@ -245,6 +250,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 P = std::max<uint64_t>(std::min<uint64_t>(P, cap), std::min<uint64_t>(P, 1u << 20));
             }
             const size_t f4 = 16 * (size_t)P;
+            // queue sorting: by default for scenes of at least SORT_MIN_TRIS triangles only (wf_sort -1)
+            const int sort = c->wf_sort >= 0 ? c->wf_sort : (c->n_tris >= SORT_MIN_TRIS ? 1 : 0);
             // queue-sort keys: (pixel sub-tile, octahedral direction bin)
             const uint32_t T = A.tile, sub = (T + (1u << c->wf_sort_tile) - 1) >> c->wf_sort_tile;
             const uint64_t nkeys = (uint64_t)(A.n_items / (T * T)) * sub * sub * c->wf_dir_res * c->wf_dir_res;
@@ -273,11 +280,11 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             if (leaf_keys) key_bits = leaf_bits;
             // bytes of the buffers of a chunk of Pn paths with kb-bit sort keys
             auto need_for = [&](uint64_t Pn, int kb) -> size_t {
-                const size_t st = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)Pn, kb, c->wf_sort_lib != 0) : 0;
+                const size_t st = sort ? cr::wf_sort_tmp_bytes((uint32_t)Pn, kb, c->wf_sort_lib != 0) : 0;
                 return (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 20 * (size_t)Pn +
-                       (c->wf_sort ? 32 * (size_t)Pn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
+                       (sort ? 32 * (size_t)Pn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
             };
-            const size_t sort_tmp = c->wf_sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
+            const size_t sort_tmp = sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
             const size_t need = need_for(P, key_bits);
             // a chunk of more than a quarter of the path cap reserves the buffers of a whole-cap chunk
             // with the widest keys, so passes of other sizes (a pass group's frame pieces, the next
@@ -310,7 +317,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cxy = (float2 *)take(8 * (size_t)P);
                 W.ended = (uint32_t *)take(4 * (size_t)P);
                 W.fold = c->wf_fold;
-                W.sort = c->wf_sort && nkeys <= (1ull << 32);
+                W.sort = sort && nkeys <= (1ull << 32);
                 W.key_bits = key_bits;
                 W.key_bits_pixel = key_bits_pixel;
                 W.sort_lib = c->wf_sort_lib;
@@ -330,7 +337,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.sort_g1 = c->wf_sort_g1;
                 W.cam_lean = c->wf_cam_lean;
                 W.tail_waves = c->wf_tail_waves;
-                if (c->wf_sort) {
+                if (sort) {
                     for (int q = 0; q < 2; q++)
                         for (int i = 0; i < 2; i++) {
                             W.key[q][i] = (uint32_t *)take(4 * (size_t)P);
@@ -1171,7 +1178,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "refill") && v >= 0 && v <= 64) c->refill = (uint32_t)v; // 0: per-kernel default
     else if (!std::strcmp(key, "refill_shadow") && v >= 0 && v <= 64) c->refill_shadow = (uint32_t)v;
     else if (!std::strcmp(key, "refill_camera") && v >= 0 && v <= 64) c->refill_camera = (uint32_t)v;
-    else if (!std::strcmp(key, "wf_sort") && (v == 0 || v == 1)) c->wf_sort = (int)v;
+    else if (!std::strcmp(key, "wf_sort") && v >= -1 && v <= 1) c->wf_sort = (int)v;
     else if (!std::strcmp(key, "wf_world_keys") && v >= 0 && v <= 64) c->wf_world_keys = (int)v;
     else if (!std::strcmp(key, "wf_world_bits") && v >= 1 && v <= 10) c->wf_world_bits = (uint32_t)v;
     else if (!std::strcmp(key, "wf_sort_min") && v >= 0 && v <= (1ll << 31)) c->wf_sort_min = (uint32_t)v;

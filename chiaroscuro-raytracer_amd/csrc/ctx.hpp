@@ -74,7 +74,8 @@ struct cr_ctx {
     uint32_t refill_shadow = 0; // wavefront shadow trace; 0: refill if set, else 56
     uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: refill if set, else 64
     uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
-    int wf_sort = 1;                // wavefront: sort large shadow / secondary queues for coherence
+    int wf_sort = -1;               // wavefront: sort large shadow / secondary queues for coherence (-1: scenes
+                                    // of at least SORT_MIN_TRIS triangles, cabi.cpp)
     uint32_t wf_sort_min = 1u << 20; // ... of at least this many rays
     // sweep (1080p x 128 spp, refill 56): no sort 807; (8x8 px, 8x8 dirs) 891; (16x16, 16x16) 912;
     // (16x16, 32x32 Morton) 930; (32x32, 32x32) 914 Mray/s

@@ -67,6 +67,24 @@ def test_wavefront_sorted_queues_bitexact(ca, sponza, nanobox, tile_dir, leaf):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
+@pytest.mark.parametrize("sort", [-1, 0, 1])
+def test_wavefront_sort_choice_bitexact(ca, cornell_mm, sponza, sort):
+    """Queue sorting on (1), off (0) or by scene size (-1, the default: only scenes of at least
+    1024 triangles sort; cornell_box's 36 trace in append order), every queue of the render eligible
+    (wf_sort_min 0): the same bits and counters."""
+    for pair, (x, y, s) in ((cornell_mm, (45, 37, 4)), (sponza, (96, 54, 3))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_sort", sort)
+        pair.dev.set_option("wf_sort_min", 0)
+        try:
+            g, gc, o, oc = _render_both(ca, pair, x, y, s)
+        finally:
+            pair.dev.set_option("wf_sort", -1)
+            pair.dev.set_option("wf_sort_min", 1 << 20)
+        assert_bitwise(g, o, "wf_sort %d %dx%dx%d" % (sort, x, y, s))
+        assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
 @pytest.mark.parametrize("fold,resolve_paths", [(1, 16), (2, 16), (0, 0), (0, 1), (0, 4), (0, 64)])
 def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_paths):
     """The NEE term of a bounce and the fold of an ended path: by default (wf_fold 0) wf_resolve's
