@@ -14,7 +14,7 @@
 enum { S_QUERIES, S_KD_OCC, S_KD_INNER, S_KD_LEAVES, S_KD_TESTS, S_BVH_FOUND, S_BVH_NODES, S_BVH_TESTS,
        S_BVH_VIS_NODES, S_BVH_VIS_TESTS, S_KD_VIS_INNER, S_KD_VIS_LEAVES, S_KD_VIS_TESTS, S_MISMATCH_FOUND,
        S_MISMATCH_OCC, S_BVH_OCC_NODES, S_BVH_OCC_TESTS, S_KD_OCC_INNER, S_KD_OCC_LEAVES, S_KD_OCC_TESTS,
-       S_BVH_LEAVES, S_N };
+       S_BVH_LEAVES, S_PR_FOUND, S_PR_NODES, S_PR_TESTS, S_PR_VIS_NODES, S_PR_VIS_TESTS, S_PR_MISS, S_N };
 
 /* kdtree.cpp:293-320 (float, no contraction: gcc -ffp-contract=off) */
 static int mt(const float o[3], const float d[3], const float *tri, float tmax, float *tout) {
@@ -82,6 +82,9 @@ static int kd_node(const Kd *T, uint32_t n, const float o[3], const float d[3], 
 typedef struct {
     float lo[3], hi[3];
     uint32_t left, first, count; /* inner: count 0, children left, left + 1 */
+    /* proof data (double): cone of normal LINES (axis, half-angle), max E = |e1|_1 + |e2|_1, max g = E^2/|N| */
+    double ax[3], rho, E, g;
+    int degen;
 } BNode;
 typedef struct {
     BNode *n;
@@ -266,6 +269,165 @@ static int bvh_any(const Bvh *B, const float o[3], const float d[3], float D, ui
     }
 }
 
+static void tri_normal(const float *p, double n[3], double *E, double *g, int *degen) {
+    double e1[3], e2[3];
+    for (int i = 0; i < 3; i++) {
+        e1[i] = (double)(p[3 + i] - p[i]);
+        e2[i] = (double)(p[6 + i] - p[i]);
+    }
+    double N[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+    double l = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+    *E = (fabs(e1[0]) + fabs(e1[1]) + fabs(e1[2])) + (fabs(e2[0]) + fabs(e2[1]) + fabs(e2[2]));
+    *degen = !(l > 0);
+    *g = l > 0 ? (*E) * (*E) / l : INFINITY;
+    for (int i = 0; i < 3; i++) n[i] = l > 0 ? N[i] / l : 0;
+}
+static double angle_lines(const double a[3], const double b[3]) {
+    double c = fabs(a[0] * b[0] + a[1] * b[1] + a[2] * b[2]);
+    return acos(c > 1 ? 1 : c);
+}
+/* cones bottom-up: leaves from their triangles (axis = principal direction of n n^T), inner nodes from
+   the children's cones (axis = sign-aligned sum, rho = max child offset + child rho) */
+static void bvh_cones(Bvh *B, uint32_t node) {
+    BNode *N = &B->n[node];
+    if (N->count) {
+        double M[9] = {0}, E = 0, g = 0;
+        int degen = 0;
+        for (uint32_t j = N->first; j < N->first + N->count; j++) {
+            double n[3], e, gg;
+            int dg;
+            tri_normal(B->pos + 9 * (size_t)B->ids[j], n, &e, &gg, &dg);
+            E = fmax(E, e);
+            g = fmax(g, gg);
+            degen |= dg;
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) M[3 * a + b] += n[a] * n[b];
+        }
+        double v[3] = {0.577, 0.577, 0.577};
+        for (int it = 0; it < 50; it++) {
+            double w[3] = {M[0] * v[0] + M[1] * v[1] + M[2] * v[2], M[3] * v[0] + M[4] * v[1] + M[5] * v[2],
+                           M[6] * v[0] + M[7] * v[1] + M[8] * v[2]};
+            double l = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            if (!(l > 0)) break;
+            for (int i = 0; i < 3; i++) v[i] = w[i] / l;
+        }
+        double rho = 0;
+        for (uint32_t j = N->first; j < N->first + N->count; j++) {
+            double n[3], e, gg;
+            int dg;
+            tri_normal(B->pos + 9 * (size_t)B->ids[j], n, &e, &gg, &dg);
+            if (!dg) rho = fmax(rho, angle_lines(n, v));
+        }
+        memcpy(N->ax, v, sizeof v);
+        N->rho = rho + 1e-9;
+        N->E = E;
+        N->g = g;
+        N->degen = degen;
+        return;
+    }
+    bvh_cones(B, N->left);
+    bvh_cones(B, N->left + 1);
+    const BNode *a = &B->n[N->left], *b = &B->n[N->left + 1];
+    double s = (a->ax[0] * b->ax[0] + a->ax[1] * b->ax[1] + a->ax[2] * b->ax[2]) < 0 ? -1 : 1;
+    double v[3] = {a->ax[0] + s * b->ax[0], a->ax[1] + s * b->ax[1], a->ax[2] + s * b->ax[2]};
+    double l = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (l > 0)
+        for (int i = 0; i < 3; i++) v[i] /= l;
+    else
+        memcpy(v, a->ax, sizeof v);
+    memcpy(N->ax, v, sizeof v);
+    N->rho = fmin(M_PI / 2, fmax(angle_lines(v, a->ax) + a->rho, angle_lines(v, b->ax) + b->rho) + 1e-9);
+    N->E = fmax(a->E, b->E);
+    N->g = fmax(a->g, b->g);
+    N->degen = a->degen | b->degen;
+}
+
+/* The proof walk (census, double precision): a node is skipped when no triangle below can pass
+ * Moller-Trumbore with t < D for this ray:
+ *   regime i  (the ray meets every normal of the node's cone at cos >= C1): the segment misses the
+ *             node box padded by the leaf-cull bound at cb = C1 (leafcull.hpp, S from the box);
+ *   plane     (otherwise): |h| > D cb_max + eps -- an accepting test needs the origin's distance h to the
+ *             triangle's plane within D |d.n| + 10u g (D + S) (MT's t = s.N / (-d.N));
+ * else the node is descended, and a leaf's triangles are tested exactly (float MT). */
+#ifndef C1
+#define C1 0.05
+#endif
+static int bvh_proof(const Bvh *B, const float o[3], const float d[3], float D, uint32_t excl, uint64_t *c) {
+    const double u = 0x1p-24;
+    uint32_t stk[128], sp = 0, n = 0;
+    for (;;) {
+        const BNode *N = &B->n[n];
+        c[0]++;
+        int skip = 0;
+        double X[8][3], S = 0, R = 0, pmin = INFINITY, pmax = -INFINITY;
+        for (int k = 0; k < 8; k++) {
+            X[k][0] = (k & 1) ? N->hi[0] : N->lo[0];
+            X[k][1] = (k & 2) ? N->hi[1] : N->lo[1];
+            X[k][2] = (k & 4) ? N->hi[2] : N->lo[2];
+            double r2 = 0;
+            for (int i = 0; i < 3; i++) {
+                const double dd = fabs((double)o[i] - X[k][i]);
+                S = fmax(S, dd);
+                r2 += dd * dd;
+            }
+            R = fmax(R, sqrt(r2));
+            const double pa = N->ax[0] * X[k][0] + N->ax[1] * X[k][1] + N->ax[2] * X[k][2];
+            pmin = fmin(pmin, pa);
+            pmax = fmax(pmax, pa);
+        }
+        if (!N->degen && N->g < 1e15) {
+            const double phi = angle_lines(N->ax, (const double[3]){d[0], d[1], d[2]});
+            /* angle between d and a normal line: within [phi - rho, phi + rho]; |cos| of the angle between d
+               and the plane's normal */
+            const double cbmin = cos(fmin(phi + N->rho, M_PI / 2)), cbmax = cos(fmax(phi - N->rho, 0.0));
+            if (cbmin >= C1) {
+                const double pad = (20.11 * u * (N->E + 2 * S) * N->g / C1 + 6.21 * u * N->E + u * S) * 1.01 + 1e-12;
+                const double dt = 10.06 * u * S * N->g / C1 * 1.01, t_hi = D * (1 + 10.06 * u * N->g / C1) * 1.01 + dt;
+                double tn = -dt, tf = t_hi;
+                for (int i = 0; i < 3; i++) {
+                    const double lo = N->lo[i] - pad - o[i], hi = N->hi[i] + pad - o[i];
+                    if (d[i] == 0) {
+                        if (lo > 0 || hi < 0) tn = INFINITY;
+                        continue;
+                    }
+                    double a = lo / d[i], b = hi / d[i];
+                    if (a > b) {
+                        const double t = a;
+                        a = b;
+                        b = t;
+                    }
+                    tn = fmax(tn, a);
+                    tf = fmin(tf, b);
+                }
+                skip = tn > tf;
+            } else {
+                const double po = N->ax[0] * o[0] + N->ax[1] * o[1] + N->ax[2] * o[2];
+                const double dista = fmax(0.0, fmax(po - pmax, pmin - po));
+                const double eps = 10.1 * u * N->g * (D + S) + 1e-9;
+                skip = dista - sin(N->rho) * R > D * cbmax * 1.001 + eps;
+            }
+        }
+        if (!skip) {
+            if (N->count) {
+                c[2]++;
+                for (uint32_t j = N->first; j < N->first + N->count; j++) {
+                    const uint32_t id = B->ids[j];
+                    if (id == excl) continue;
+                    c[1]++;
+                    float t;
+                    if (mt(o, d, B->pos + 9 * (size_t)id, D, &t)) return 1;
+                }
+            } else {
+                stk[sp++] = N->left + 1;
+                n = N->left;
+                continue;
+            }
+        }
+        if (!sp) return 0;
+        n = stk[--sp];
+    }
+}
+
 void census(uint32_t nn, const uint32_t *is_leaf, const uint32_t *axis, const float *split, const uint32_t *child,
             const uint32_t *first, const uint32_t *count, const uint32_t *refs, const float *box, const float *pos,
             uint32_t ntris, uint32_t nr, const float *orig, const float *dir, const float *dist, const uint32_t *excl,
@@ -283,6 +445,7 @@ void census(uint32_t nn, const uint32_t *is_leaf, const uint32_t *axis, const fl
     }
     bvh_alloc(&B);
     bvh_build(&B, 0, 0, ntris);
+    bvh_cones(&B, 0);
     *bvh_nodes = B.nn;
     memset(out, 0, sizeof(uint64_t) * S_N);
 #pragma omp parallel
@@ -331,6 +494,16 @@ void census(uint32_t nn, const uint32_t *is_leaf, const uint32_t *axis, const fl
                 st[S_KD_VIS_LEAVES] += kc[0];
                 st[S_KD_VIS_TESTS] += kc[1];
             }
+            uint64_t pc[3] = {0, 0, 0};
+            const int pfound = bvh_proof(&B, o, d, dist[r], excl[r], pc);
+            st[S_PR_FOUND] += pfound;
+            st[S_PR_NODES] += pc[0];
+            st[S_PR_TESTS] += pc[1];
+            if (!occ) {
+                st[S_PR_VIS_NODES] += pc[0];
+                st[S_PR_VIS_TESTS] += pc[1];
+            }
+            st[S_PR_MISS] += occ && !pfound; /* must be 0 */
             st[S_MISMATCH_FOUND] += found && !occ; /* BVH found, kd VISIBLE: the kd answer rules */
             st[S_MISMATCH_OCC] += occ && !found;   /* must be 0: the BVH proof would be wrong */
         }

@@ -21,7 +21,7 @@ os.environ.setdefault("CHIARO_QUIET", "1")
 NAMES = ("queries", "kd_occ", "kd_inner", "kd_leaves", "kd_tests", "bvh_found", "bvh_nodes", "bvh_tests",
          "bvh_vis_nodes", "bvh_vis_tests", "kd_vis_inner", "kd_vis_leaves", "kd_vis_tests", "mismatch_found",
          "mismatch_occ", "bvh_occ_nodes", "bvh_occ_tests", "kd_occ_inner", "kd_occ_leaves", "kd_occ_tests",
-         "bvh_leaves")
+         "bvh_leaves", "pr_found", "pr_nodes", "pr_tests", "pr_vis_nodes", "pr_vis_tests", "pr_miss")
 
 
 def main():
@@ -30,9 +30,10 @@ def main():
     ap.add_argument("--res", default="320x180")
     ap.add_argument("--spp", type=int, default=2)
     ap.add_argument("--leaf", type=int, default=4)
+    ap.add_argument("--c1", type=float, default=0.05, help="proof walk: regime-i cosine threshold")
     args = ap.parse_args()
-    so = "/tmp/bvh_census_%d.so" % args.leaf
-    subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-DLEAF=%d" % args.leaf, "-shared", "-fPIC", "-o",
+    so = "/tmp/bvh_census_%d_%g.so" % (args.leaf, args.c1)
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-DLEAF=%d" % args.leaf, "-DC1=%r" % args.c1, "-shared", "-fPIC", "-o",
                     so, str(ROOT / "scripts/bvh_census.c"), "-lm"], check=True)
     L = C.CDLL(so)
     import chiaroscuro_amd as ca
@@ -89,9 +90,11 @@ def main():
     occ = max(s["kd_occ"], 1)
     vis = max(s["queries"] - s["kd_occ"], 1)
     s["per_query"] = {k: round(s[k] / q, 2) for k in ("kd_inner", "kd_leaves", "kd_tests", "bvh_nodes", "bvh_tests",
-                                                       "bvh_leaves")}
+                                                       "bvh_leaves", "pr_nodes", "pr_tests")}
+    s["pr_found_frac"] = round(s["pr_found"] / q, 4)
     s["per_visible"] = {k: round(s[k] / vis, 2) for k in ("kd_vis_inner", "kd_vis_leaves", "kd_vis_tests",
-                                                           "bvh_vis_nodes", "bvh_vis_tests")}
+                                                           "bvh_vis_nodes", "bvh_vis_tests", "pr_vis_nodes",
+                                                           "pr_vis_tests")}
     s["per_occluded"] = {k: round(s[k] / occ, 2) for k in ("kd_occ_inner", "kd_occ_leaves", "kd_occ_tests",
                                                             "bvh_occ_nodes", "bvh_occ_tests")}
     s["occluded_frac"] = round(s["kd_occ"] / q, 4)
