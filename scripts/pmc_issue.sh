@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_issue
 mkdir -p $OUT
-ARGS="${@:-"--config sponza --steps 16 --warmup 0 --no-cpu-baseline"} --no-perf-pass"
+ARGS="${@:-"--config sponza --steps 16 --warmup 0 --no-cpu-baseline"} --no-perf-pass --parity-rows 0 --single-layer-steps 0"
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/a -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/a.log 2>&1 || { echo "pass a failed"; exit 1; }
 echo "pass a ok"

@@ -5,7 +5,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
-ARGS="${@:-"--config sponza --spp 8 --steps 2 --warmup 1 --no-cpu-baseline"} --no-perf-pass"
+ARGS="${@:-"--config sponza --spp 8 --steps 2 --warmup 1 --no-cpu-baseline"} --no-perf-pass --parity-rows 0 --single-layer-steps 0"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
