@@ -376,6 +376,7 @@ def run_rank(args, world, backend):
     dev.set_option("counters", 0)  # (the timed, lean build: the counting build renders one layer per pass)
     p1 = ca.render_params(xres, yres, spp, k, seed, layer=1, rank=rank, nranks=world, tile=tile)
     nl_pass, _ = fr.plan_layers(p1, args.layers_per_pass)  # (every rank the same: plan_layers agrees)
+    fr.reserve(min(nl_pass, args.steps))  # (the timed group's gather buffers, allocated before the clock)
     groups = []
 
     def step(layer, n, record):

@@ -170,6 +170,20 @@ class DistributedFrame:
                     return nl, m
         return 1, 1
 
+    def reserve(self, nlayers: int):
+        """Allocate the group buffers of up to nlayers layers now (the tile buffers of a rank and the
+        root's gathered [nranks][nlayers] buffers), so a timed group does not allocate them."""
+        import torch
+        L = self.layout
+        if L.nranks == 1 or self.gather != "torch" or nlayers < 2:
+            return
+        if self.tiles_multi is None or self.tiles_multi.shape[0] < nlayers:
+            self.tiles_multi = torch.zeros((nlayers,) + tuple(self.tiles.shape), dtype=self.tiles.dtype,
+                                           device=self.tiles.device)
+        if self.rank == 0 and (self.gathered_multi is None or self.gathered_multi.shape[1] != nlayers):
+            self.gathered_multi = torch.zeros((L.nranks, nlayers) + tuple(self.tiles.shape), dtype=self.tiles.dtype,
+                                              device=self.tiles.device)
+
     def render_layers(self, cam, params, nlayers: int, stream: int = 0, pieces: int = 1):
         """Layers params.layer .. + nlayers - 1 as ONE render pass group of my tiles (of each
         of `pieces` frame pieces on a single rank) -- cr_render_layers_device /
