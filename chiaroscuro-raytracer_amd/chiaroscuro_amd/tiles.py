@@ -85,7 +85,7 @@ class DistributedFrame:
         self.tiles = torch.zeros((L.max_tiles, tile, tile, 3), **f32) if split else None
         self.gathered = torch.zeros((nranks, L.max_tiles, tile, tile, 3), **f32) if split and rank == 0 else None
         self.tiles_multi = None  # [nlayers][max_tiles][tile][tile][3] of render_layers
-        self.gathered_multi = None  # root: [nranks][nlayers][max_tiles][tile][tile][3] of render_layers
+        self.gathered_multi = None  # root: flat store of [nranks][nlayers][max_tiles][tile][tile][3] (render_layers)
         self._stats_begin()
         if nranks > 1 and gather == "cabi":
             uid = [dev.comm_unique_id() if rank == 0 else None]
@@ -180,9 +180,20 @@ class DistributedFrame:
         if self.tiles_multi is None or self.tiles_multi.shape[0] < nlayers:
             self.tiles_multi = torch.zeros((nlayers,) + tuple(self.tiles.shape), dtype=self.tiles.dtype,
                                            device=self.tiles.device)
-        if self.rank == 0 and (self.gathered_multi is None or self.gathered_multi.shape[1] != nlayers):
-            self.gathered_multi = torch.zeros((L.nranks, nlayers) + tuple(self.tiles.shape), dtype=self.tiles.dtype,
-                                              device=self.tiles.device)
+        if self.rank == 0:
+            self._gathered_view(nlayers)
+
+    def _gathered_view(self, nlayers: int):
+        """The root's [nranks][nlayers][max_tiles][T][T][3] gather buffer: a view of the front of a flat
+        store that only grows (groups of different sizes reuse it)."""
+        import torch
+        shape = (self.layout.nranks, nlayers) + tuple(self.tiles.shape)
+        n = 1
+        for x in shape:
+            n *= x
+        if self.gathered_multi is None or self.gathered_multi.numel() < n:
+            self.gathered_multi = torch.zeros(n, dtype=self.tiles.dtype, device=self.tiles.device)
+        return self.gathered_multi[:n].view(shape)
 
     def render_layers(self, cam, params, nlayers: int, stream: int = 0, pieces: int = 1):
         """Layers params.layer .. + nlayers - 1 as ONE render pass group of my tiles (of each
@@ -230,12 +241,10 @@ class DistributedFrame:
                                                 self.frame.data_ptr(), stream)
             return
         # one gather of the whole group: rank r's nlayers buffers land at the root's [r], then one blend
-        if self.rank == 0 and (self.gathered_multi is None or self.gathered_multi.shape[1] != nlayers):
-            self.gathered_multi = torch.zeros((L.nranks,) + tuple(mine.shape), dtype=mine.dtype, device=mine.device)
-        self.dist.gather(mine, [self.gathered_multi[r] for r in range(L.nranks)] if self.rank == 0 else None, dst=0)
+        g = self._gathered_view(nlayers) if self.rank == 0 else None
+        self.dist.gather(mine, [g[r] for r in range(L.nranks)] if self.rank == 0 else None, dst=0)
         if self.rank == 0:
-            self.dev.blend_tiles_layers_device(params, nlayers, self.gathered_multi.data_ptr(), self.frame.data_ptr(),
-                                               stream)
+            self.dev.blend_tiles_layers_device(params, nlayers, g.data_ptr(), self.frame.data_ptr(), stream)
 
     # the device's counters, pass time and trace stats summed over the passes of the last
     # render_layer(s) call
