@@ -317,6 +317,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cxy = (float2 *)take(8 * (size_t)P);
                 W.ended = (uint32_t *)take(4 * (size_t)P);
                 W.fold = c->wf_fold;
+                W.shade_waves = c->wf_shade_waves;
                 W.sort = sort && nkeys <= (1ull << 32);
                 W.key_bits = key_bits;
                 W.key_bits_pixel = key_bits_pixel;
@@ -1199,6 +1200,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_leaf_keys") && (v == 0 || v == 1)) c->wf_leaf_keys = (int)v;
     else if (!std::strcmp(key, "wf_resolve_paths") && v >= 0 && v <= 64) c->wf_resolve_paths = (uint32_t)v;
     else if (!std::strcmp(key, "wf_fold") && v >= 0 && v <= 2) c->wf_fold = (int)v;
+    else if (!std::strcmp(key, "wf_shade_waves") && (v == 6 || v == 8)) c->wf_shade_waves = (int)v;
     else if (!std::strcmp(key, "wf_leaf_shift") && v >= 0 && v <= 24) c->wf_leaf_shift = (uint32_t)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;

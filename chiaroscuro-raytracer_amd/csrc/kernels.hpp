@@ -250,6 +250,7 @@ struct WfArgs {
     // they are read next (wf_shade(g + 1), or wf_tail at pickup).  0: wf_resolve (round 3)
     int fold;
     uint32_t *ended;    // [P] paths that ended at the generation being folded
+    int shade_waves;    // wf_shade's build: 8 waves per SIMD (64 VGPRs, spills) or else its natural 6
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

@@ -493,7 +493,9 @@ __device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32
 // Every closest ray of generation g: misses finish their path with the
 // background; hits run shade_next and append their NEE ray to shadow queue g and
 // their next ray to closest queue g + 1.
-__global__ void __launch_bounds__(256) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
+// MINW: waves per SIMD the build is held to (6: its 75 VGPRs, no spills; 8: 64 VGPRs, the rest spilled)
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
     __shared__ uint32_t app[5];
     if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
@@ -1353,14 +1355,23 @@ void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks) {
 // Grid of the grid-stride wf_shade: every block resident at once.  wf_shade needs 71 VGPRs,
 // so a SIMD holds 7 of its waves, not 8: with 8 blocks per CU the eighth started only when
 // another had finished its whole share (the grid-stride loop gives every block the same).
-static uint32_t shade_grid(int num_cus) {
-    static std::atomic<int> per_cu{0};
-    int b = per_cu.load();
+static uint32_t shade_grid(int num_cus, int waves) {
+    static std::atomic<int> per_cu[2] = {0, 0};
+    const int i = waves == 8 ? 1 : 0;
+    int b = per_cu[i].load();
     if (!b) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, wf_shade, 256, 0) != hipSuccess || b <= 0) b = 8;
-        per_cu.store(b);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8> : wf_shade<1>, 256, 0) != hipSuccess || b <= 0)
+            b = 8;
+        per_cu[i].store(b);
     }
     return (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)std::min(b, 8);
+}
+// wf_shade at the ctx's option "wf_shade_waves" (6 default, 8)
+static void launch_shade(const RenderArgs &A, const WfArgs &W, uint32_t g, int num_cus, hipStream_t st) {
+    if (W.shade_waves == 8)
+        hipLaunchKernelGGL(wf_shade<8>, dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
+    else
+        hipLaunchKernelGGL(wf_shade<1>, dim3(shade_grid(num_cus, 6)), dim3(256), 0, st, A, W, g);
 }
 
 int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, hipStream_t st, const WfStreams &ss,
@@ -1414,7 +1425,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     }
     closest(1, st, nullptr, W.gstack); // camera rays: path order is already coherent
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
-        hipLaunchKernelGGL(wf_shade, dim3(shade_grid(num_cus)), dim3(256), 0, st, A, W, g);
+        launch_shade(A, W, g, num_cus, st);
         uint32_t cnt[2] = {0u, 0u}; // shadow queue g, closest queue g + 1
         if ((err = (int)hipMemcpyAsync(&cnt[0], W.cnt + WF_G + g, 4, hipMemcpyDeviceToHost, st)) ||
             (err = (int)hipMemcpyAsync(&cnt[1], W.cnt + g + 1, 4, hipMemcpyDeviceToHost, st)) ||
@@ -1507,7 +1518,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         err = trace_event(te, s, kind, false);
     };
     auto shade = [&](WfLane &ln, Run &r) { // wf_shade(g), then the queue lengths to the host, async
-        hipLaunchKernelGGL(wf_shade, dim3(shade_grid(num_cus)), dim3(256), 0, ln.st, A, r.W, r.g);
+        launch_shade(A, r.W, r.g, num_cus, ln.st);
         if ((err = (int)hipMemcpyAsync(&ln.hcnt[0], r.W.cnt + WF_G + r.g, 4, hipMemcpyDeviceToHost, ln.st)) ||
             (err = (int)hipMemcpyAsync(&ln.hcnt[1], r.W.cnt + r.g + 1, 4, hipMemcpyDeviceToHost, ln.st)) ||
             (err = (int)hipEventRecord(ln.ready, ln.st)))
