@@ -337,6 +337,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.tail_overlap = c->wf_tail_overlap;
                 W.sort_g1 = c->wf_sort_g1;
                 W.cam_lean = c->wf_cam_lean;
+                W.cam_fused = c->wf_cam_fuse;
                 W.tail_waves = c->wf_tail_waves;
                 if (sort) {
                     for (int q = 0; q < 2; q++)
@@ -1156,6 +1157,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_tail_overlap") && (v == 0 || v == 1)) c->wf_tail_overlap = (int)v;
     else if (!std::strcmp(key, "wf_sort_g1") && v >= 0 && v <= 3) c->wf_sort_g1 = (uint32_t)v;
     else if (!std::strcmp(key, "wf_cam_lean") && (v == 0 || v == 1)) c->wf_cam_lean = (int)v;
+    else if (!std::strcmp(key, "wf_cam_fuse") && (v == 0 || v == 1)) c->wf_cam_fuse = (int)v;
     else if (!std::strcmp(key, "wf_tail_waves") && v >= 4 && v <= 6) c->wf_tail_waves = (int)v;
     else if (!std::strcmp(key, "wf_side_priority") && (v == 0 || v == 1)) {
         // the second stream (closest trace g + 1 beside shadow trace g) at the device's highest

@@ -96,6 +96,7 @@ struct cr_ctx {
     int wf_tail_overlap = 0;
     uint32_t wf_sort_g1 = 3;        // generation-1 queues sorted: bit 0 shadow, bit 1 closest (WfArgs::sort_g1)
     int wf_cam_lean = 1;            // WfArgs::cam_lean
+    int wf_cam_fuse = 0;            // WfArgs::cam_fused: no wf_camera, the packet trace makes the rays
     int wf_tail_waves = 4;          // WfArgs::tail_waves
     uint32_t wf_dir_res_shadow = 0; // shadow queues' direction bins per axis with leaf keys (0: wf_dir_res)
     // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a

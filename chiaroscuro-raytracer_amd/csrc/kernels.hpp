@@ -244,13 +244,17 @@ struct WfArgs {
     uint32_t dir_res_s; // leaf keys: direction bins per axis of the SHADOW queues' keys
     int key_bits_s;     // significant bits of the shadow queues' keys
     int tail_waves;     // waves per SIMD of the lean tail launch (4, 5, 6)
-    // fold = 1 (option "wf_fold", the default): no sweep over the paths per generation -- wf_shade(g)
+    // fold = 1 (option "wf_fold"): no sweep over the paths per generation -- wf_shade(g)
     // lists the paths whose hit at g ends them (ended, count at cnt[4 WF_G + g]), wf_fold(g) folds
     // those after the shadow trace, and the paths that continue have their bounce g resolved where
-    // they are read next (wf_shade(g + 1), or wf_tail at pickup).  0: wf_resolve (round 3)
+    // they are read next (wf_shade(g + 1), or wf_tail at pickup).  0 (the default): wf_resolve
     int fold;
     uint32_t *ended;    // [P] paths that ended at the generation being folded
     int shade_waves;    // wf_shade's build: 8 waves per SIMD (64 VGPRs, spills) or else its natural 6
+    // 1: no wf_camera launch -- the packet camera trace derives each path's camera ray from its
+    // (pixel, sample) itself, and wf_shade(1) / wf_resolve(1) take path p = ray p and the eye as
+    // its origin (set per chunk by launch_wavefront_chunk; option "wf_cam_fuse")
+    int cam_fused;
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

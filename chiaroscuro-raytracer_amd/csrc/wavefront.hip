@@ -33,7 +33,8 @@
 
 namespace cr {
 
-enum : uint32_t { NO_SLOT = 0xffffffffu, NO_PATH = 0xffffffffu };
+// DEAD_RAY: the hit record .x of a partial-tile slot's camera ray when the camera is fused (.w = 0: no hit)
+enum : uint32_t { NO_SLOT = 0xffffffffu, NO_PATH = 0xffffffffu, DEAD_RAY = 1u };
 // sexcl[j]: the light triangle shadow ray j ignores, bit 31 set when the ray's path continues
 // (the overlapped tail traces those; triangle ids stay below 2^31)
 enum : uint32_t { SEXCL_CONT = 0x80000000u };
@@ -145,7 +146,7 @@ __device__ __forceinline__ void ctl_store(const WfArgs &W, uint32_t p, uint32_t 
 // wf_tail at once), wf_camera writes only slot 3 (the resolve mark): wf_shade derives generation 1's
 // RNG state -- the camera sample's stream after its two jitter draws -- from the path's (pixel, sample)
 // instead of reading it.
-__device__ __forceinline__ bool camera_state_lean(const WfArgs &W) { return W.cam_lean && W.P >= W.tail_min; }
+__host__ __device__ __forceinline__ bool camera_state_lean(const WfArgs &W) { return W.cam_lean && W.P >= W.tail_min; }
 __device__ __forceinline__ Rng camera_rng(const RenderArgs &A, const WfArgs &W, uint32_t p) {
     const uint32_t w = W.w0 + p, item = w / A.s_count, s = A.s0 + (w - item * A.s_count);
     uint32_t px = 0, py = 0;
@@ -504,6 +505,9 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
     const float4 *rays = W.ray[g & 1];
     const uint4 *hits = W.hit[g & 1];
     float4 *next_rays = W.ray[(g + 1) & 1];
+    // fused camera (WfArgs::cam_fused): ray i of generation 1 is path i's, from the eye; no wf_camera
+    // cleared its resolve mark or counted it
+    const bool fused = g == 1 && W.cam_fused;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
         const bool in = i < n;
@@ -511,10 +515,15 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (in) {
             h = hits[i];
-            r0 = rays[2 * (size_t)i];
+            if (fused) r0 = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(h.x == DEAD_RAY && !h.w ? NO_PATH : i));
+            else r0 = rays[2 * (size_t)i];
         }
         const uint32_t p = __float_as_uint(r0.w);
         const bool hit = in && h.w != 0u;
+        if (fused) {
+            if (in && !hit) PS(W, 3, i) = make_float4(0.f, 0.f, 0.f, 0.f); // no resolve mark (wf_resolve)
+            tally(tl, T_PATHS, in && p != NO_PATH);
+        }
         // (fold: bounce g - 1 of every path read here, hit or miss, before it is folded or shaded on)
         if (W.fold == 1 && g >= 2 && in && p != NO_PATH) resolve_prev(W, p, g - 1);
         bool textured = false, nee = false, cont = false;
@@ -593,7 +602,7 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
     const uint4 *hits = W.hit[g & 1];
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         if (hits[i].w == 0u) continue;
-        const uint32_t p = __float_as_uint(rays[2 * (size_t)i].w);
+        const uint32_t p = g == 1 && W.cam_fused ? i : __float_as_uint(rays[2 * (size_t)i].w);
         const float4 s3 = PS(W, 3, p);
         // (overlapped tail: the tail may already have rewritten a continuing path's PS3 -- the mark
         // then no longer names generation g)
@@ -809,7 +818,9 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
     const uint32_t gid = blockIdx.x * bdim + tid, gstride = W.gstride;
     uint32_t *ring = pring_lds;
     uint2 *gstk = W.gstack;
-    const uint32_t n = *cnt_closest(W, 1);
+    // fused: every path of the chunk has its camera ray here (wf_camera's queue length, set for wf_shade)
+    const uint32_t n = W.cam_fused ? W.P : *cnt_closest(W, 1);
+    if (W.cam_fused && gid == 0) *cnt_closest(W, 1) = W.P;
     uint32_t *work = work_closest(W, 1);
     const float4 *rays = W.ray[1];
     uint4 *hits = W.hit[1];
@@ -852,17 +863,34 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             tmin[s] = tmax[s] = csx[s] = csy[s] = 0.f;
             found[s] = false;
             if (live[s]) {
-                if (PC) pc.vb += 32;
-                const float4 r0 = rays[2 * (size_t)idx[s]], r1 = rays[2 * (size_t)idx[s] + 1];
-                d[s] = ld3(r1);
-                if (__float_as_uint(r0.w) == NO_PATH) { // partial-tile slot: no query
-                    hits[idx[s]] = make_uint4(0u, 0u, 0u, 0u);
+                bool dead;
+                if (W.cam_fused) { // wf_camera's ray, here: rayTracer.cpp:58-62
+                    const uint32_t w = W.w0 + idx[s], item = w / A.s_count, sm = A.s0 + (w - item * A.s_count);
+                    uint32_t px = 0, py = 0;
+                    dead = !(w < A.n_work && item_pixel(A, item, px, py));
+                    if (!dead) {
+                        Rng rng = path_rng(A, py * A.xres + px, sm);
+                        float2 q;
+                        d[s] = camera_dir(A, px, py, rng, &q);
+                        csx[s] = q.x;
+                        csy[s] = q.y;
+                    }
+                } else {
+                    if (PC) pc.vb += 32;
+                    const float4 r0 = rays[2 * (size_t)idx[s]], r1 = rays[2 * (size_t)idx[s] + 1];
+                    d[s] = ld3(r1);
+                    dead = __float_as_uint(r0.w) == NO_PATH;
+                    if (!dead) {
+                        if (PC) pc.vb += 8;
+                        const float2 q = W.cxy[idx[s]];
+                        csx[s] = q.x;
+                        csy[s] = q.y;
+                    }
+                }
+                if (dead) { // partial-tile slot: no query (fused: the record says so to wf_shade)
+                    hits[idx[s]] = make_uint4(W.cam_fused ? DEAD_RAY : 0u, 0u, 0u, 0u);
                     live[s] = false;
                 } else {
-                    if (PC) pc.vb += 8;
-                    const float2 q = W.cxy[idx[s]];
-                    csx[s] = q.x;
-                    csy[s] = q.y;
                     issued++;
                     Trav T;
                     bool in;
@@ -1218,6 +1246,12 @@ int num_wf_variants() { return kNumWf; }
 static void (*camera_kernel(const WfVariant &v, const RenderArgs &A))(RenderArgs, WfArgs, uint32_t) {
     return (v.packet && A.eye_on_split) ? kWf[15].camera : v.camera;
 }
+// The chunk's camera rays come from the packet trace itself (WfArgs::cam_fused) when the ctx asks for it
+// (W.cam_fused on entry), the camera kernel is the packet trace, generation 1 runs as its own launches
+// (not handed to wf_tail, which reads wf_camera's rays) and wf_shade derives generation 1's RNG state.
+static bool camera_fuses(const WfVariant &v, const RenderArgs &A, const WfArgs &W) {
+    return W.cam_fused && v.packet && !A.eye_on_split && camera_state_lean(W);
+}
 bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].cull; }
 bool wf_variant_available(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].closest; }
 
@@ -1418,7 +1452,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
                            lds, s, A, Wc, g);
         err = trace_event(te, s, kind, false);
     };
-    hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
+    W.cam_fused = camera_fuses(v, A, W) ? 1 : 0;
+    if (!W.cam_fused) hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, st, A, W);
     if (W.P < W.tail_min) {
         tail(1, st, W);
         return err ? err : (int)hipGetLastError();
@@ -1532,7 +1567,8 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         r.g = 1;
         r.past_camera = false;
         if ((err = (int)hipMemsetAsync(r.W.cnt, 0, WF_CNT * sizeof(uint32_t), ln.st))) return;
-        hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, ln.st, A, r.W);
+        r.W.cam_fused = camera_fuses(v, A, r.W) ? 1 : 0;
+        if (!r.W.cam_fused) hipLaunchKernelGGL(wf_camera, dim3(sgrid), dim3(256), 0, ln.st, A, r.W);
         if (P < r.W.tail_min) {
             tail(ln, r.W, 1);
             r.phase = 0;

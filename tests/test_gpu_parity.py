@@ -119,6 +119,41 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
             pair.dev.set_option("wf_paths", 256 << 20)
 
 
+@pytest.mark.parametrize("fuse,fold,resolve_paths", [(1, 0, 16), (1, 0, 0), (1, 1, 16), (0, 0, 16)])
+def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, fold, resolve_paths):
+    """wf_cam_fuse 1: no wf_camera launch -- the packet camera trace makes each path's ray from its
+    (pixel, sample), wf_shade(1) takes path p = ray p from the eye, clears the resolve mark of a path
+    that missed and counts the paths; partial-tile slots carry a dead-ray record.  The same bits and
+    counters over layers 1..3 on the same buffers (a mark an earlier layer or chunk left must not
+    resolve a path), one chunk and wf_paths 4096 chunks, partial tiles (96 x 54, 3 x 2)."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4)), (nanobox, (3, 2, 1))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_cam_fuse", fuse)
+        pair.dev.set_option("wf_fold", fold)
+        pair.dev.set_option("wf_resolve_paths", resolve_paths)
+        pair.dev.set_option("counters", 0)  # the lean builds: the packet camera trace
+        cam = pair.camera(ca, x, y)
+        keys = ("closest", "shadow", "hit", "texhit", "paths")
+        try:
+            for paths in (256 << 20, 4096):
+                pair.dev.set_option("wf_paths", paths)
+                o = None
+                for layer in (1, 2, 3):
+                    p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=layer)
+                    g = pair.dev.render(cam, p, None)
+                    gc = pair.dev.counters()
+                    assert pair.dev.last_trace_build() in (43, 44)
+                    o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
+                    assert_bitwise(g, o, "cam_fuse %d fold %d wf_paths %d layer %d" % (fuse, fold, paths, layer))
+                    assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
+        finally:
+            pair.dev.set_option("counters", 1)
+            pair.dev.set_option("wf_cam_fuse", 0)
+            pair.dev.set_option("wf_fold", 0)
+            pair.dev.set_option("wf_resolve_paths", 16)
+            pair.dev.set_option("wf_paths", 256 << 20)
+
+
 @pytest.mark.parametrize("xcd,sort_min,variant", [(7, 0, 15), (7, 1 << 20, 15), (1, 0, 15), (2, 0, 15), (4, 0, 18),
                                                    (7, 0, 26), (0, 0, 26), (7, 0, 18), (0, 0, 18)])
 def test_wavefront_xcd_partition_bitexact(ca, sponza, nanobox, xcd, sort_min, variant):
