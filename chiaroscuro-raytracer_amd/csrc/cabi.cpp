@@ -338,6 +338,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.sort_g1 = c->wf_sort_g1;
                 W.cam_lean = c->wf_cam_lean;
                 W.cam_fused = c->wf_cam_fuse;
+                W.ctl_ray = c->wf_ctl_ray;
                 W.tail_waves = c->wf_tail_waves;
                 if (sort) {
                     for (int q = 0; q < 2; q++)
@@ -1158,6 +1159,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_sort_g1") && v >= 0 && v <= 3) c->wf_sort_g1 = (uint32_t)v;
     else if (!std::strcmp(key, "wf_cam_lean") && (v == 0 || v == 1)) c->wf_cam_lean = (int)v;
     else if (!std::strcmp(key, "wf_cam_fuse") && (v == 0 || v == 1)) c->wf_cam_fuse = (int)v;
+    else if (!std::strcmp(key, "wf_ctl_ray") && (v == 0 || v == 1)) c->wf_ctl_ray = (int)v;
     else if (!std::strcmp(key, "wf_tail_waves") && v >= 4 && v <= 6) c->wf_tail_waves = (int)v;
     else if (!std::strcmp(key, "wf_side_priority") && (v == 0 || v == 1)) {
         // the second stream (closest trace g + 1 beside shadow trace g) at the device's highest

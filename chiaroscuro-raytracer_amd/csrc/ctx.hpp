@@ -96,7 +96,12 @@ struct cr_ctx {
     int wf_tail_overlap = 0;
     uint32_t wf_sort_g1 = 3;        // generation-1 queues sorted: bit 0 shadow, bit 1 closest (WfArgs::sort_g1)
     int wf_cam_lean = 1;            // WfArgs::cam_lean
-    int wf_cam_fuse = 0;            // WfArgs::cam_fused: no wf_camera, the packet trace makes the rays
+    // WfArgs::cam_fused (no wf_camera: the packet trace makes the rays) and WfArgs::ctl_ray (the RNG
+    // counter in the closest ray, no control slot for generations >= 2); round 4, two interleaved rounds,
+    // ms per layer: sponza 1080p x 128 spp 321.8 / 322.3 -> fused 320.1 / 320.5 -> both 318.8 / 319.4;
+    // cornell_box 1024^2 x 500 spp 112.9 / 112.4 -> both 108.5 / 106.0 (C2 moves path state, not rays)
+    int wf_cam_fuse = 1;
+    int wf_ctl_ray = 1;
     int wf_tail_waves = 4;          // WfArgs::tail_waves
     uint32_t wf_dir_res_shadow = 0; // shadow queues' direction bins per axis with leaf keys (0: wf_dir_res)
     // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a

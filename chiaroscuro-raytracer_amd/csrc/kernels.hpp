@@ -255,6 +255,10 @@ struct WfArgs {
     // (pixel, sample) itself, and wf_shade(1) / wf_resolve(1) take path p = ray p and the eye as
     // its origin (set per chunk by launch_wavefront_chunk; option "wf_cam_fuse")
     int cam_fused;
+    // 1: a secondary closest ray carries its path's RNG counter in the direction's w and the key is
+    // re-derived from the path's (pixel, sample) -- wf_shade neither reads nor writes the control slot
+    // (PS_CTL) of generations >= 2; wf_tail writes it at pickup (option "wf_ctl_ray")
+    int ctl_ray;
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position

@@ -147,13 +147,15 @@ __device__ __forceinline__ void ctl_store(const WfArgs &W, uint32_t p, uint32_t 
 // RNG state -- the camera sample's stream after its two jitter draws -- from the path's (pixel, sample)
 // instead of reading it.
 __host__ __device__ __forceinline__ bool camera_state_lean(const WfArgs &W) { return W.cam_lean && W.P >= W.tail_min; }
-__device__ __forceinline__ Rng camera_rng(const RenderArgs &A, const WfArgs &W, uint32_t p) {
+// the key of path p's RNG stream: a function of its (pixel, sample) alone
+__device__ __forceinline__ uint32_t path_key(const RenderArgs &A, const WfArgs &W, uint32_t p) {
     const uint32_t w = W.w0 + p, item = w / A.s_count, s = A.s0 + (w - item * A.s_count);
     uint32_t px = 0, py = 0;
     item_pixel(A, item, px, py);
-    Rng rng = path_rng(A, py * A.xres + px, s);
-    rng.ctr = 2u; // camera_dir's y- and x-jitter draws
-    return rng;
+    return path_rng(A, py * A.xres + px, s).key;
+}
+__device__ __forceinline__ Rng camera_rng(const RenderArgs &A, const WfArgs &W, uint32_t p) {
+    return Rng{path_key(A, W, p), 2u}; // (camera_dir's y- and x-jitter draws)
 }
 
 // ---------------------------------------------------------------- camera --
@@ -431,8 +433,9 @@ __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W
 // dw[2(k-1)] = {direct, shadow slot (set by the caller)}, PS3 = {contrib, 2k | ended}:
 // the mark 2k tells wf_resolve's path-order sweep which paths hit at bounce k.
 // A continuing path gets W_k in dw[2(k-1)+1] and its next closest ray (org, wi).
+// ctr: W.ctl_ray -- the RNG counter the closest ray carries (in: this bounce's, out: the next ray's)
 __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t k, f3 ro, uint4 h,
-                                           bool &textured, ShadowRay &sh, bool &cont, f3 &org, f3 &wi) {
+                                           bool &textured, ShadowRay &sh, bool &cont, f3 &org, f3 &wi, uint32_t &ctr) {
     const DevScene &S = A.S;
     const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
     textured = hs.textured;
@@ -440,6 +443,8 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
     Rng rng;
     if (cam) {
         rng = camera_rng(A, W, p);
+    } else if (W.ctl_ray && k >= 2u) {
+        rng = Rng{path_key(A, W, p), ctr};
     } else {
         const float4 ctl = PS(W, PS_CTL, p);
         rng = Rng{__float_as_uint(ctl.y), __float_as_uint(ctl.z)};
@@ -467,7 +472,8 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
             const float cosine = fabsf(dot(hs.normal, wi));
             const f3 w = divs(muls(hs.fcol, cosine), pdf * Kmax);
             W.dw[(size_t)(2 * (k - 1) + 1) * W.P + p] = pk(w, 0u);
-            ctl_store(W, p, k + 1, rng);
+            if (W.ctl_ray) ctr = rng.ctr;
+            else ctl_store(W, p, k + 1, rng);
             org = next;
             cont = true;
         }
@@ -513,10 +519,12 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         const bool in = i < n;
         uint4 h = make_uint4(0u, 0u, 0u, 0u);
         float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t ctr = 0; // W.ctl_ray: the RNG counter in the closest ray's w (in the cache line of r0)
         if (in) {
             h = hits[i];
             if (fused) r0 = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(h.x == DEAD_RAY && !h.w ? NO_PATH : i));
             else r0 = rays[2 * (size_t)i];
+            if (W.ctl_ray && g >= 2 && h.w) ctr = __float_as_uint(rays[2 * (size_t)i + 1].w);
         }
         const uint32_t p = __float_as_uint(r0.w);
         const bool hit = in && h.w != 0u;
@@ -532,7 +540,7 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         if (in && !hit) {
             if (p != NO_PATH) finish_path(A, W, p, g, mk(A.bg[0], A.bg[1], A.bg[2]));
         } else if (hit) {
-            nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi);
+            nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi, ctr);
         }
         const uint32_t j = block_append(cnt_shadow(W, g), nee, app);
         if (nee) {
@@ -555,7 +563,7 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         const uint32_t jc = block_append(cnt_closest(W, g + 1), cont, app);
         if (cont) {
             next_rays[2 * (size_t)jc] = pk(org, p);
-            next_rays[2 * (size_t)jc + 1] = pk(wi, 0u);
+            next_rays[2 * (size_t)jc + 1] = pk(wi, W.ctl_ray ? ctr : 0u);
             if (W.sort) {
                 W.key[1][0][jc] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res * W.dir_res) + dir_bin(wi, W.dir_res)
                                   : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
@@ -688,6 +696,9 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                     o = ld3(r0);
                     d = ld3(r1);
                     p = __float_as_uint(r0.w);
+                    // W.ctl_ray: the path's control words from its ray (bounce g0, the ray's RNG counter)
+                    if (W.ctl_ray && g0 >= 2 && p != NO_PATH)
+                        ctl_store(W, p, g0, Rng{path_key(A, W, p), __float_as_uint(r1.w)});
                     const uint32_t slot = (gs && p != NO_PATH)
                                               ? __float_as_uint(W.dw[(size_t)(2 * (gs - 1)) * W.P + p].w) : NO_SLOT;
                     if (slot != NO_SLOT) { // overlapped: this path's generation-gs shadow query first

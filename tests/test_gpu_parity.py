@@ -119,16 +119,19 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
             pair.dev.set_option("wf_paths", 256 << 20)
 
 
-@pytest.mark.parametrize("fuse,fold,resolve_paths", [(1, 0, 16), (1, 0, 0), (1, 1, 16), (0, 0, 16)])
-def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, fold, resolve_paths):
+@pytest.mark.parametrize("fuse,ctl,fold,resolve_paths", [(1, 0, 0, 16), (1, 0, 0, 0), (1, 0, 1, 16), (0, 0, 0, 16),
+                                                         (0, 1, 0, 16), (1, 1, 0, 16), (1, 1, 1, 16), (1, 1, 0, 0)])
+def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, resolve_paths):
     """wf_cam_fuse 1: no wf_camera launch -- the packet camera trace makes each path's ray from its
     (pixel, sample), wf_shade(1) takes path p = ray p from the eye, clears the resolve mark of a path
     that missed and counts the paths; partial-tile slots carry a dead-ray record.  The same bits and
     counters over layers 1..3 on the same buffers (a mark an earlier layer or chunk left must not
-    resolve a path), one chunk and wf_paths 4096 chunks, partial tiles (96 x 54, 3 x 2)."""
+    resolve a path), one chunk and wf_paths 4096 chunks, partial tiles (96 x 54, 3 x 2).  wf_ctl_ray 1: a
+    secondary closest ray carries its path's RNG counter, the key is re-derived from (pixel, sample)."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4)), (nanobox, (3, 2, 1))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_cam_fuse", fuse)
+        pair.dev.set_option("wf_ctl_ray", ctl)
         pair.dev.set_option("wf_fold", fold)
         pair.dev.set_option("wf_resolve_paths", resolve_paths)
         pair.dev.set_option("counters", 0)  # the lean builds: the packet camera trace
@@ -144,11 +147,12 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, fold, resolv
                     gc = pair.dev.counters()
                     assert pair.dev.last_trace_build() in (43, 44)
                     o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
-                    assert_bitwise(g, o, "cam_fuse %d fold %d wf_paths %d layer %d" % (fuse, fold, paths, layer))
+                    assert_bitwise(g, o, "cam_fuse %d ctl_ray %d fold %d wf_paths %d layer %d" % (fuse, ctl, fold, paths, layer))
                     assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
         finally:
             pair.dev.set_option("counters", 1)
-            pair.dev.set_option("wf_cam_fuse", 0)
+            pair.dev.set_option("wf_cam_fuse", 1)
+            pair.dev.set_option("wf_ctl_ray", 1)
             pair.dev.set_option("wf_fold", 0)
             pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_paths", 256 << 20)
@@ -349,19 +353,21 @@ def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
 
 
 @pytest.mark.parametrize("tail_min", [1 << 30, 12000, 3000])
-@pytest.mark.parametrize("overlap,fold", [(1, 1), (0, 1), (1, 2), (0, 2), (1, 0), (0, 0)])
-def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap, fold):
+@pytest.mark.parametrize("overlap,fold,ctl", [(1, 1, 0), (0, 1, 0), (1, 2, 0), (0, 2, 0), (1, 0, 0), (0, 0, 0),
+                                              (1, 0, 1), (0, 0, 1), (0, 1, 1)])
+def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap, fold, ctl):
     """wf_tail (the last generations of a chunk in one launch, per-path bodies
     shared with wf_shade / wf_bounce): from generation 1 (every queue is below
     1 << 30) and from later generations, counting and lean builds; after the last shadow trace
     (default) or overlapped (option wf_tail_overlap: the tail starts beside that trace and traces
     its own paths' shadow rays of that generation, the shadow trace and wf_resolve keep the paths
-    that ended)."""
+    that ended); wf_ctl_ray 1: the tail takes a path's RNG counter from its ray at pickup."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4)), (cornell, (64, 64, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_tail_min", tail_min)
         pair.dev.set_option("wf_tail_overlap", overlap)
         pair.dev.set_option("wf_fold", fold)
+        pair.dev.set_option("wf_ctl_ray", ctl)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
             pair.dev.set_option("counters", 0)
@@ -372,6 +378,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
             pair.dev.set_option("wf_tail_min", 0)
             pair.dev.set_option("wf_tail_overlap", 0)
             pair.dev.set_option("wf_fold", 0)
+            pair.dev.set_option("wf_ctl_ray", 1)
         assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
         assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
@@ -806,8 +813,8 @@ def test_default_build_by_scene_size(ca, sponza, nanobox):
     assert masks["sponza"] > 0 and masks["nanobox"] == 0, masks
 
 
-@pytest.mark.parametrize("tail_min", [0, 1 << 30])
-def test_layers_per_pass_bitexact(ca, sponza, nanobox, tail_min):
+@pytest.mark.parametrize("tail_min,ctl", [(0, 0), (1 << 30, 0), (0, 1)])
+def test_layers_per_pass_bitexact(ca, sponza, nanobox, tail_min, ctl):
     """Several progressive layers in ONE render pass (cr_render_layers_device /
     cr_render_tiles_layers_device: the paths of all layers in one chunk, each with its
     layer's RNG streams, src/rayTracer.cpp:18-33) equal one pass per layer bit for bit:
@@ -821,6 +828,8 @@ def test_layers_per_pass_bitexact(ca, sponza, nanobox, tail_min):
         dev.set_option("kernel", 2)
         dev.set_option("counters", 0)
         dev.set_option("wf_tail_min", tail_min)
+        dev.set_option("wf_ctl_ray", ctl)
+        dev.set_option("wf_cam_fuse", ctl)
         try:
             p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=1)
             assert dev.layers_per_pass(p, 3) == 3
@@ -849,6 +858,8 @@ def test_layers_per_pass_bitexact(ca, sponza, nanobox, tail_min):
                     assert_bitwise(both[j].cpu().numpy(), one.cpu().numpy(), "rank %d layer %d tiles" % (r, 2 + j))
         finally:
             dev.set_option("wf_tail_min", 0)
+            dev.set_option("wf_ctl_ray", 1)
+            dev.set_option("wf_cam_fuse", 1)
             dev.set_option("counters", 1)
             torch.cuda.synchronize()
 
