@@ -1,6 +1,7 @@
 """Per-phase time of each wavefront render pass from a rocprofv3 kernel trace.
     python scripts/pass_breakdown.py gpurun_out/prof_r01/trace/trace_kernel_trace.csv
-A pass starts at wf_camera; trace launches are numbered by generation (closest and
+A pass starts at wf_camera, or at the packet camera trace when no wf_camera precedes it (the
+fused camera, WfArgs::cam_fused); trace launches are numbered by generation (closest and
 shadow separately: shadow g runs beside closest g + 1).  pass_ms sums kernel
 times, busy_ms is the union of their intervals, overlap_ms the difference.  The
 counting launch (FULL build) is marked "counting" and is not a timed pass.
@@ -13,13 +14,15 @@ import sys
 
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-    passes, cur = [], None
+    passes, cur, prev = [], None, ""
     for r in rows:
-        if "wf_camera" in r["Kernel_Name"]:
+        n = r["Kernel_Name"]
+        if "wf_camera" in n or ("wf_trace_packet" in n and "wf_camera" not in prev):
             cur = []
             passes.append(cur)
         if cur is not None:
             cur.append(r)
+        prev = n
     for p in passes:
         g, gs, acc, tot, counting = 0, 0, {}, 0.0, False
         for r in p:
@@ -36,7 +39,7 @@ def main():
             elif "wf_tail" in n:
                 k = "tail (g%d..)" % (gs + 1)
                 counting |= "wf_tail<true" in n
-            elif "rocprim" in n:
+            elif "rocprim" in n or "rs_upsweep" in n or "rs_downsweep" in n or "rs_scan" in n:
                 k = "sort"
             elif "wf_shade" in n or "wf_bounce" in n or "wf_resolve" in n:
                 k = "shade+resolve"
