@@ -281,7 +281,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             // bytes of the buffers of a chunk of Pn paths with kb-bit sort keys
             auto need_for = [&](uint64_t Pn, int kb) -> size_t {
                 const size_t st = sort ? cr::wf_sort_tmp_bytes((uint32_t)Pn, kb, c->wf_sort_lib != 0) : 0;
-                return (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 20 * (size_t)Pn +
+                return (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 21 * (size_t)Pn +
                        (sort ? 32 * (size_t)Pn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
             };
             const size_t sort_tmp = sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
@@ -316,6 +316,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
                 W.cxy = (float2 *)take(8 * (size_t)P);
                 W.ended = (uint32_t *)take(4 * (size_t)P);
+                W.mark = (uint8_t *)take((size_t)P);
                 W.fold = c->wf_fold;
                 W.shade_waves = c->wf_shade_waves;
                 W.sort = sort && nkeys <= (1ull << 32);
@@ -339,6 +340,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cam_lean = c->wf_cam_lean;
                 W.cam_fused = c->wf_cam_fuse;
                 W.ctl_ray = c->wf_ctl_ray;
+                W.vis_dw = c->wf_vis_dw;
                 W.tail_waves = c->wf_tail_waves;
                 if (sort) {
                     for (int q = 0; q < 2; q++)
@@ -1160,6 +1162,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_cam_lean") && (v == 0 || v == 1)) c->wf_cam_lean = (int)v;
     else if (!std::strcmp(key, "wf_cam_fuse") && (v == 0 || v == 1)) c->wf_cam_fuse = (int)v;
     else if (!std::strcmp(key, "wf_ctl_ray") && (v == 0 || v == 1)) c->wf_ctl_ray = (int)v;
+    else if (!std::strcmp(key, "wf_vis_dw") && (v == 0 || v == 1)) c->wf_vis_dw = (int)v;
     else if (!std::strcmp(key, "wf_tail_waves") && v >= 4 && v <= 6) c->wf_tail_waves = (int)v;
     else if (!std::strcmp(key, "wf_side_priority") && (v == 0 || v == 1)) {
         // the second stream (closest trace g + 1 beside shadow trace g) at the device's highest

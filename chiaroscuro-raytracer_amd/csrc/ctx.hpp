@@ -102,6 +102,9 @@ struct cr_ctx {
     // cornell_box 1024^2 x 500 spp 112.9 / 112.4 -> both 108.5 / 106.0 (C2 moves path state, not rays)
     int wf_cam_fuse = 1;
     int wf_ctl_ray = 1;
+    // WfArgs::vis_dw; round 4, two interleaved rounds: sponza 318.1 / 317.9 -> 318.0 / 318.3 ms per layer,
+    // cornell_box 105.7 / 106.1 -> 105.1 / 105.1 ms per pass
+    int wf_vis_dw = 1;
     int wf_tail_waves = 4;          // WfArgs::tail_waves
     uint32_t wf_dir_res_shadow = 0; // shadow queues' direction bins per axis with leaf keys (0: wf_dir_res)
     // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a

@@ -259,10 +259,17 @@ struct WfArgs {
     // re-derived from the path's (pixel, sample) -- wf_shade neither reads nor writes the control slot
     // (PS_CTL) of generations >= 2; wf_tail writes it at pickup (option "wf_ctl_ray")
     int ctl_ray;
+    // [P] resolve marks, one byte per path: (k << 1) | ended of the path's last closest hit (wf_shade), 0 for
+    // a path that missed -- wf_resolve's path-order sweep reads these, not the 16-B PS3 records
+    uint8_t *mark;
+    // 1: the shadow trace writes each query's result over the slot in the w of its path's dw record of
+    // that bounce (SHADOW_VIS / SHADOW_OCC) instead of occ[slot] -- wf_resolve then reads no occ entries,
+    // which a sorted shadow queue scatters over the paths (option "wf_vis_dw")
+    int vis_dw;
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
-// camera sample position
-inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4; }
+// camera sample position, ended list, resolve mark
+inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4 + 1; }
 // Second stream and fork / join events of a render (shadow trace g beside closest trace g + 1).
 struct WfStreams {
     hipStream_t side;

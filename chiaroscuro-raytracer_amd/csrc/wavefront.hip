@@ -133,7 +133,7 @@ __device__ __forceinline__ void finish_path(const RenderArgs &A, const WfArgs &W
 }
 
 // Path state slots [slot][P]: 0 {direct, -}  1 {fcol, -}  2 {normal, -}  (wf_tail's bounce only)
-//                             3 {contrib, shadow slot / resolve mark}  4 {next origin, -}
+//                             3 {contrib, shadow slot}  4 {next origin, -}
 //                             5 {k, rng.key, rng.ctr, -}: the control words, one 16-B slot (the
 //                               per-generation kernels write only this one, not slots 0-2)
 __device__ __forceinline__ float4 &PS(const WfArgs &W, int slot, uint32_t p) { return W.ps[(size_t)slot * W.P + p]; }
@@ -143,7 +143,7 @@ __device__ __forceinline__ void ctl_store(const WfArgs &W, uint32_t p, uint32_t 
 }
 
 // Path state (PS above).  When generation 1 runs as wavefront launches (the chunk is not handed to
-// wf_tail at once), wf_camera writes only slot 3 (the resolve mark): wf_shade derives generation 1's
+// wf_tail at once), wf_camera writes only the resolve mark: wf_shade derives generation 1's
 // RNG state -- the camera sample's stream after its two jitter draws -- from the path's (pixel, sample)
 // instead of reading it.
 __host__ __device__ __forceinline__ bool camera_state_lean(const WfArgs &W) { return W.cam_lean && W.P >= W.tail_min; }
@@ -182,17 +182,30 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
             const f3 d = camera_dir(A, px, py, rng, &sxy);
             if (A.cull) W.cxy[p] = sxy;
             if (!camera_state_lean(W)) ctl_store(W, p, 1u, rng); // (wf_tail from generation 1 reads it)
-            PS(W, 3, p) = make_float4(0.f, 0.f, 0.f, 0.f); // no resolve mark (wf_resolve)
+            W.mark[p] = 0; // no resolve mark (wf_resolve)
             W.ray[1][2 * (size_t)p] = make_float4(A.cam[0], A.cam[1], A.cam[2], __uint_as_float(p));
             W.ray[1][2 * (size_t)p + 1] = pk(d, 0u);
         } else if (p < W.P) {
-            PS(W, 3, p) = make_float4(0.f, 0.f, 0.f, 0.f);
+            W.mark[p] = 0;
             W.ray[1][2 * (size_t)p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(NO_PATH));
             W.ray[1][2 * (size_t)p + 1] = make_float4(0.f, 0.f, 1.f, 0.f);
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_closest(W, 1) = W.P;
     flush_tallies(A, tl);
+}
+
+// The result of shadow query idx of generation g: occ[idx] or, with WfArgs::vis_dw, the w of the path's
+// dw record of bounce g (idx is then the path), which held the query's slot (SHADOW_VIS / SHADOW_OCC
+// replace it; NO_SLOT -- no NEE ray -- is never written here).
+enum : uint32_t { SHADOW_VIS = 0u, SHADOW_OCC = 1u };
+__device__ __forceinline__ void shadow_store(const WfArgs &W, uint32_t g, uint32_t idx, bool occluded) {
+    if (W.vis_dw) ((uint32_t *)(W.dw + (size_t)(2 * (g - 1)) * W.P + idx))[3] = occluded ? SHADOW_OCC : SHADOW_VIS;
+    else W.occ[idx] = occluded ? 1u : 0u;
+}
+// true: the NEE ray of a bounce whose dw record's w is `slot` found no occluder
+__device__ __forceinline__ bool nee_visible(const WfArgs &W, uint32_t slot) {
+    return slot != NO_SLOT && (W.vis_dw ? slot == SHADOW_VIS : W.occ[slot] == 0u);
 }
 
 // ----------------------------------------------------------------- trace --
@@ -278,6 +291,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                         o = ld3(r0);
                         d = ld3(r1);
                         if (SHADOW) exclude = W.sexcl[idx] & ~SEXCL_CONT;
+                        if (SHADOW && W.vis_dw) idx = __float_as_uint(r0.w); // the result goes to path idx's dw
                         if (CULL) { // ray idx of generation 1 is path idx's camera ray
                             const float2 q = W.cxy[idx];
                             csx = q.x;
@@ -290,7 +304,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                             if (FULL) diag_begin(&dg);
                         } else if (SHADOW) {
                             if (PC) pc.vb += 4;
-                            W.occ[idx] = 0u; // culled: visible (kdtree.cpp:285-287)
+                            shadow_store(W, g, idx, false); // culled: visible (kdtree.cpp:285-287)
                         } else {
                             if (PC) pc.vb += 16;
                             W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u);
@@ -315,7 +329,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
                 A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr);
             if (r != busy_st) {
                 if (PC) pc.vb += SHADOW ? 4u : 16u;
-                if (SHADOW) W.occ[idx] = r == ST_OCCLUDED ? 1u : 0u;
+                if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
                                                            __float_as_uint(d.y), T.node + 1u) // w: the hit's leaf + 1
                                               : make_uint4(0u, 0u, 0u, 0u);
@@ -430,7 +444,7 @@ __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W
 // need the shadow result (rayTracer.cpp:80-134): hit shading, emission, the NEE
 // light sample and -- for k < K -- the BRDF sample and Russian roulette, in the
 // reference's draw order.  The NEE term stays pending for wf_resolve:
-// dw[2(k-1)] = {direct, shadow slot (set by the caller)}, PS3 = {contrib, 2k | ended}:
+// dw[2(k-1)] = {direct, shadow slot (set by the caller)}, PS3 = {contrib, -}, mark = 2k | ended:
 // the mark 2k tells wf_resolve's path-order sweep which paths hit at bounce k.
 // A continuing path gets W_k in dw[2(k-1)+1] and its next closest ray (org, wi).
 // ctr: W.ctl_ray -- the RNG counter the closest ray carries (in: this bounce's, out: the next ray's)
@@ -479,7 +493,8 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
         }
     }
     W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(hs.direct, NO_SLOT);
-    PS(W, 3, p) = pk(contrib, (k << 1) | (cont ? 0u : 1u));
+    PS(W, 3, p) = pk(contrib, 0u);
+    W.mark[p] = (uint8_t)((k << 1) | (cont ? 0u : 1u));
     return nee;
 }
 
@@ -492,7 +507,7 @@ __device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32
     const float4 d4 = dk;
     const uint32_t slot = __float_as_uint(d4.w);
     f3 direct = ld3(d4);
-    if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(PS(W, 3, p)));
+    if (nee_visible(W, slot)) direct = add(direct, ld3(PS(W, 3, p)));
     dk = pk(direct, 0u);
 }
 
@@ -529,7 +544,7 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         const uint32_t p = __float_as_uint(r0.w);
         const bool hit = in && h.w != 0u;
         if (fused) {
-            if (in && !hit) PS(W, 3, i) = make_float4(0.f, 0.f, 0.f, 0.f); // no resolve mark (wf_resolve)
+            if (in && !hit) W.mark[i] = 0; // no resolve mark (wf_resolve)
             tally(tl, T_PATHS, in && p != NO_PATH);
         }
         // (fold: bounce g - 1 of every path read here, hit or miss, before it is folded or shaded on)
@@ -580,29 +595,29 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
 // --------------------------------------------------------------- resolve --
 // After the shadow trace of generation g: the bounce's direct term
 // D_k = direct + (visible ? contrib : 0) (rayTracer.cpp:96-99), and the
-// back-to-front fold of every path that ended at this bounce.
-__device__ __forceinline__ void resolve_path(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t g, float4 s3) {
+// back-to-front fold of every path that ended at this bounce (ended: bit 0 of its mark).
+// The contribution (PS3) is read only for a visible NEE ray.
+__device__ __forceinline__ void resolve_path(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t g, bool ended) {
     float4 &dk = W.dw[(size_t)(2 * (g - 1)) * W.P + p];
     const float4 d4 = dk;
     const uint32_t slot = __float_as_uint(d4.w);
     f3 direct = ld3(d4);
-    if (slot != NO_SLOT && W.occ[slot] == 0u) direct = add(direct, ld3(s3));
-    if (__float_as_uint(s3.w) & 1u) finish_path(A, W, p, g, direct);
+    if (nee_visible(W, slot)) direct = add(direct, ld3(PS(W, 3, p)));
+    if (ended) finish_path(A, W, p, g, direct);
     else dk = pk(direct, 0u);
 }
 
 // A long queue (at least P / resolve_paths rays) is swept in PATH order: the hits of generation g are the
-// paths whose PS3 carries the mark 2g (wf_camera clears it, shade_next sets it), so
-// the path-state, dw and sample accesses are coalesced instead of scattered in the
-// queue's leaf order.  A short queue is swept in queue order (fewer bytes than a
-// pass over all P slots).  Each path's arithmetic is the same either way.
+// paths whose byte mark (WfArgs::mark) is 2g | ended (wf_camera / wf_shade(1) clear it, shade_next sets
+// it), so the dw and sample accesses are coalesced instead of scattered in the queue's leaf order, and
+// the sweep reads one byte per path.  A short queue is swept in queue order (fewer bytes than a pass
+// over all P slots).  Each path's arithmetic is the same either way.
 __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32_t g) {
     const uint32_t n = *cnt_closest(W, g);
     if (W.resolve_paths && (uint64_t)n * W.resolve_paths >= (uint64_t)W.P) {
         for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < W.P; p += gridDim.x * blockDim.x) {
-            const float4 s3 = PS(W, 3, p);
-            if ((__float_as_uint(s3.w) >> 1) == g && (!W.ended_only || (__float_as_uint(s3.w) & 1u)))
-                resolve_path(A, W, p, g, s3);
+            const uint32_t m = W.mark[p];
+            if ((m >> 1) == g && (!W.ended_only || (m & 1u))) resolve_path(A, W, p, g, m & 1u);
         }
         return;
     }
@@ -611,11 +626,10 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         if (hits[i].w == 0u) continue;
         const uint32_t p = g == 1 && W.cam_fused ? i : __float_as_uint(rays[2 * (size_t)i].w);
-        const float4 s3 = PS(W, 3, p);
-        // (overlapped tail: the tail may already have rewritten a continuing path's PS3 -- the mark
-        // then no longer names generation g)
-        if (W.ended_only && (__float_as_uint(s3.w) >> 1 != g || !(__float_as_uint(s3.w) & 1u))) continue;
-        resolve_path(A, W, p, g, s3);
+        const uint32_t m = W.mark[p]; // (2g | ended: a hit of this queue)
+        // (overlapped tail: a continuing path is the tail's, which resolves this bounce itself)
+        if (W.ended_only && !(m & 1u)) continue;
+        resolve_path(A, W, p, g, m & 1u);
     }
 }
 
@@ -625,10 +639,8 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
 __global__ void __launch_bounds__(256) wf_fold(RenderArgs A, WfArgs W, uint32_t g) {
     const uint32_t n = *cnt_ended(W, g);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t p = W.ended[i];
-        const float4 s3 = PS(W, 3, p);
         // (overlapped tail: only the ended paths are here, which the tail never takes)
-        resolve_path(A, W, p, g, s3);
+        resolve_path(A, W, W.ended[i], g, true);
     }
     // fold 2: the paths that go on -- closest queue g + 1 -- have their bounce g resolved here too (beside
     // the closest trace of g + 1, off the critical path), unless an overlapped tail resolves them itself

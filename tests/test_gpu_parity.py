@@ -22,6 +22,7 @@ ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit",
 TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
 # builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="37 38"
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
+VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 
 
 @pytest.fixture(scope="module")
@@ -85,8 +86,9 @@ def test_wavefront_sort_choice_bitexact(ca, cornell_mm, sponza, sort):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("fold,resolve_paths", [(1, 16), (2, 16), (0, 0), (0, 1), (0, 4), (0, 64)])
-def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_paths):
+@pytest.mark.parametrize("fold,resolve_paths,vis", [(1, 16, 0), (2, 16, 0), (0, 0, 0), (0, 1, 0), (0, 4, 0), (0, 64, 0),
+                                                   (0, 16, 1), (0, 0, 1), (1, 16, 1), (2, 16, 1)])
+def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_paths, vis):
     """The NEE term of a bounce and the fold of an ended path: by default (wf_fold 0) wf_resolve's
     sweep after each shadow trace, in queue order (resolve_paths 0) or, for queues of at least
     P / resolve_paths rays, in path order by the PS3 bounce mark (default 16; 64: nearly every
@@ -94,10 +96,12 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
     trace, and a path that goes on has its bounce resolved where it is read next (1: wf_shade of the next
     generation, wf_tail at pickup) or beside the next closest trace from its queue (2).  The same bits and
     counters over progressive layers 1..3 on the same buffers (a mark left by an earlier layer or chunk
-    must not resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks."""
+    must not resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks.  wf_vis_dw 1: the
+    shadow trace writes each result over the slot in the path's dw record instead of occ[slot]."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_fold", fold)
+        pair.dev.set_option("wf_vis_dw", vis)
         pair.dev.set_option("wf_resolve_paths", resolve_paths)
         pair.dev.set_option("wf_sort_min", 0)
         cam = pair.camera(ca, x, y)
@@ -114,6 +118,7 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
                     assert {k: gc[k] for k in ORACLE_KEYS} == oc
         finally:
             pair.dev.set_option("wf_fold", 0)
+            pair.dev.set_option("wf_vis_dw", VIS_DEFAULT)
             pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_paths", 256 << 20)
@@ -353,9 +358,10 @@ def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
 
 
 @pytest.mark.parametrize("tail_min", [1 << 30, 12000, 3000])
-@pytest.mark.parametrize("overlap,fold,ctl", [(1, 1, 0), (0, 1, 0), (1, 2, 0), (0, 2, 0), (1, 0, 0), (0, 0, 0),
-                                              (1, 0, 1), (0, 0, 1), (0, 1, 1)])
-def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap, fold, ctl):
+@pytest.mark.parametrize("overlap,fold,ctl,vis", [(1, 1, 0, 0), (0, 1, 0, 0), (1, 2, 0, 0), (0, 2, 0, 0), (1, 0, 0, 0),
+                                                  (0, 0, 0, 0), (1, 0, 1, 0), (0, 0, 1, 0), (0, 1, 1, 0), (1, 0, 1, 1),
+                                                  (0, 0, 1, 1), (1, 1, 1, 1), (1, 2, 1, 1)])
+def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap, fold, ctl, vis):
     """wf_tail (the last generations of a chunk in one launch, per-path bodies
     shared with wf_shade / wf_bounce): from generation 1 (every queue is below
     1 << 30) and from later generations, counting and lean builds; after the last shadow trace
@@ -368,6 +374,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
         pair.dev.set_option("wf_tail_overlap", overlap)
         pair.dev.set_option("wf_fold", fold)
         pair.dev.set_option("wf_ctl_ray", ctl)
+        pair.dev.set_option("wf_vis_dw", vis)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
             pair.dev.set_option("counters", 0)
@@ -379,6 +386,7 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
             pair.dev.set_option("wf_tail_overlap", 0)
             pair.dev.set_option("wf_fold", 0)
             pair.dev.set_option("wf_ctl_ray", 1)
+            pair.dev.set_option("wf_vis_dw", VIS_DEFAULT)
         assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
         assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
