@@ -130,7 +130,9 @@ struct cr_ctx {
     // sweep 322.5 / 322.9, fold 2 (resolved beside the closest trace from its queue) 325.6 / 325.3 --
     // the sweep runs beside the closest trace of g + 1, off the critical path, and reads in path order)
     int wf_fold = 0;
-    int wf_shade_waves = 6;         // WfArgs::shade_waves (option "wf_shade_waves": 6 or 8)
+    // WfArgs::shade_waves (option "wf_shade_waves": 6 or 8); round 4, two interleaved rounds: sponza
+    // 322.5 / 322.9 vs 322.6 / 322.2 ms per layer, cornell_box 108.4 / 108.7 vs 107.6 / 107.3 ms per pass
+    int wf_shade_waves = 8;
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

@@ -124,6 +124,25 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
             pair.dev.set_option("wf_paths", 256 << 20)
 
 
+@pytest.mark.parametrize("waves", [6, 8])
+def test_wavefront_shade_waves_bitexact(ca, sponza, nanobox, waves):
+    """wf_shade built for 8 waves per SIMD (the default; 64 VGPRs, spills) or its natural 6: the same
+    bits and counters, counting and lean builds."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_shade_waves", waves)
+        try:
+            g, gc, o, oc = _render_both(ca, pair, x, y, s)
+            pair.dev.set_option("counters", 0)
+            g_lean = pair.dev.render(pair.camera(ca, x, y), ca.render_params(x, y, s, 6, 0xC41A05C0))
+        finally:
+            pair.dev.set_option("counters", 1)
+            pair.dev.set_option("wf_shade_waves", 8)
+        assert_bitwise(g, o, "wf_shade_waves %d" % waves)
+        assert_bitwise(g_lean, o, "wf_shade_waves %d lean" % waves)
+        assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
 @pytest.mark.parametrize("fuse,ctl,fold,resolve_paths", [(1, 0, 0, 16), (1, 0, 0, 0), (1, 0, 1, 16), (0, 0, 0, 16),
                                                          (0, 1, 0, 16), (1, 1, 0, 16), (1, 1, 1, 16), (1, 1, 0, 0)])
 def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, resolve_paths):
