@@ -3,7 +3,9 @@
 tile-split over the ranks and gathered to rank 0 (chiaroscuro_amd.tiles.
 DistributedFrame), on 1 GPU or under torch.distributed.run on N.
 
-Reports per-layer device time and wall time, the whole-run Mray/s, and checks
+Layers run in pass groups of up to --layers-per-pass layers (DistributedFrame.plan_layers /
+render_layers; 1 = one layer per pass).  Reports per-group device time and wall
+time, the whole-run Mray/s, and checks
 the finished frame against the oracle on every --check-ystep-th full row (all 30
 layers rendered and blended by the oracle the same way; bit-exact), plus that
 the frame stays finite and non-negative.
@@ -33,6 +35,7 @@ def main():
     ap.add_argument("--check-ystep", type=int, default=135,
                     help="oracle check on rows 0, ystep, 2 ystep, ... (0: no check; one oracle thread per row)")
     ap.add_argument("--gather", default="torch")
+    ap.add_argument("--layers-per-pass", type=int, default=32)
     args = ap.parse_args()
     import torch
     import chiaroscuro_amd as ca
@@ -64,17 +67,22 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for L in range(1, args.layers + 1):
+    L = 1
+    while L <= args.layers:
         p = ca.render_params(xres, yres, spp, k, seed, layer=L, rank=rank, nranks=world, tile=32)
+        n, pieces = fr.plan_layers(p, min(args.layers_per_pass, args.layers - L + 1))
         tl = time.perf_counter()
-        fr.render_layer(cam, p, stream)
+        fr.render_layers(cam, p, n, stream, pieces)
         torch.cuda.synchronize()
-        c = dev.counters()
+        st = fr.last_stats()
+        c = st["counters"]
         rays += c["closest"] + c["shadow"]
-        layers.append({"layer": L, "wall_ms": round((time.perf_counter() - tl) * 1e3, 2),
-                       "render_ms": round(dev.last_kernel_ms(), 2)})
+        layers.append({"layers": [L, L + n - 1], "pieces": pieces, "passes": st["passes"],
+                       "wall_ms": round((time.perf_counter() - tl) * 1e3, 2),
+                       "render_ms": round(st["kernel_ms"], 2)})
         if rank == 0:
-            print("layer %d: %s" % (L, layers[-1]), file=sys.stderr, flush=True)
+            print("group %s" % (layers[-1],), file=sys.stderr, flush=True)
+        L += n
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -83,11 +91,11 @@ def main():
         t = torch.tensor([rays], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
         rays = float(t.item())
-    out = {"config": "C5 %s %dx%d, %d layers x %d spp, %d rank(s), gather %s" % (
-        args.config, xres, yres, args.layers, spp, world, args.gather if world > 1 else "-"),
+    out = {"config": "C5 %s %dx%d, %d layers x %d spp, %d rank(s), gather %s, up to %d layers per pass" % (
+        args.config, xres, yres, args.layers, spp, world, args.gather if world > 1 else "-", args.layers_per_pass),
         "wall_s": round(wall, 3), "rays": int(rays), "mray_s": round(rays / wall / 1e6, 2),
-        "layer_wall_ms_median": float(np.median([x["wall_ms"] for x in layers])),
-        "layers": layers}
+        "ms_per_layer": round(wall * 1e3 / args.layers, 2), "trace_build": dev.last_trace_build(),
+        "groups": layers}
     if rank == 0:
         f = fr.frame.cpu().numpy()
         out["frame_finite_nonneg"] = bool(np.isfinite(f).all() and (f >= 0).all())

@@ -15,3 +15,5 @@ python scripts/pmc_issue_summary.py gpurun_out/pmc_issue/a/pmc_counter_collectio
 timeout -k 10 600 python bench.py --config $CFG --steps 16 --warmup 1 > profiles/${TAG}_bench_$CFG.json 2> gpurun_out/bench_$CFG.log || { echo "bench $CFG failed"; tail -20 gpurun_out/bench_$CFG.log; exit 1; }
 cat profiles/${TAG}_bench_$CFG.json
 cp -r profiles/. gpurun_out/profiles/
+# the raw rocprofv3 csvs stay on the box (their summaries are in profiles/): gpurun returns at most 64 MiB
+rm -rf gpurun_out/prof_${TAG}_$CFG gpurun_out/pmc_issue
