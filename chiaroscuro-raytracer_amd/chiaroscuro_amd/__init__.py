@@ -20,7 +20,8 @@ from pathlib import Path
 import numpy as np
 
 PKG_ROOT = Path(__file__).resolve().parent.parent
-LIB_DIR = PKG_ROOT / "lib"
+# CHIARO_LIB_DIR: another build of both libraries (A/B timing of two builds, scripts/gpu_ab_libs.sh)
+LIB_DIR = Path(os.environ["CHIARO_LIB_DIR"]) if os.environ.get("CHIARO_LIB_DIR") else PKG_ROOT / "lib"
 
 CR_OK = 0
 CR_ERRORS = {-1: "CR_E_INVALID", -2: "CR_E_HIP", -3: "CR_E_NOSCENE", -4: "CR_E_DEPTH", -5: "CR_E_OOM",

@@ -64,6 +64,47 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, u
     return slot;
 }
 
+// N appends of one block at once (wf_shade's shadow and closest queues): one barrier round and
+// the N global atomics in flight together instead of one after another.  lds: [2][4 N + N] words,
+// the half `buf` alternating between consecutive calls (so no barrier is needed before the next
+// call writes it: the one after that is separated from this one by the next call's barriers).
+template <int N>
+__device__ __forceinline__ void block_append_n(uint32_t *const (&counter)[N], const bool (&pred)[N], uint32_t *lds,
+                                               uint32_t buf, uint32_t (&slot)[N]) {
+    uint32_t *L = lds + buf * 5u * N;
+    const uint32_t wave = threadIdx.x >> 6;
+    uint64_t m[N];
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+        m[q] = __ballot(pred[q]);
+        if ((threadIdx.x & 63u) == 0) L[4 * q + wave] = (uint32_t)__popcll(m[q]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot[N];
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+            uint32_t s = 0;
+            for (uint32_t w = 0; w < (blockDim.x >> 6); w++) {
+                const uint32_t c = L[4 * q + w];
+                L[4 * q + w] = s;
+                s += c;
+            }
+            tot[q] = s;
+        }
+        uint32_t base[N];
+#pragma unroll
+        for (int q = 0; q < N; q++) base[q] = tot[q] ? atomicAdd(counter[q], tot[q]) : 0u;
+#pragma unroll
+        for (int q = 0; q < N; q++) L[4 * N + q] = base[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < N; q++)
+        slot[q] = L[4 * N + q] + L[4 * q + wave] +
+                  __builtin_amdgcn_mbcnt_hi((uint32_t)(m[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[q], 0u));
+}
+
 __device__ __forceinline__ uint32_t *cnt_closest(const WfArgs &W, uint32_t g) { return W.cnt + g; }
 __device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + WF_G + g; }
 __device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 2 * WF_G + g; }
@@ -448,8 +489,10 @@ __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W
 // the mark 2k tells wf_resolve's path-order sweep which paths hit at bounce k.
 // A continuing path gets W_k in dw[2(k-1)+1] and its next closest ray (org, wi).
 // ctr: W.ctl_ray -- the RNG counter the closest ray carries (in: this bounce's, out: the next ray's)
+// direct: the bounce's emission + direct term, for the caller's dw[2(k-1)] = {direct, shadow slot}
 __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t k, f3 ro, uint4 h,
-                                           bool &textured, ShadowRay &sh, bool &cont, f3 &org, f3 &wi, uint32_t &ctr) {
+                                           bool &textured, ShadowRay &sh, bool &cont, f3 &org, f3 &wi, uint32_t &ctr,
+                                           f3 &direct) {
     const DevScene &S = A.S;
     const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
     textured = hs.textured;
@@ -492,7 +535,7 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
             cont = true;
         }
     }
-    W.dw[(size_t)(2 * (k - 1)) * W.P + p] = pk(hs.direct, NO_SLOT);
+    direct = hs.direct;
     PS(W, 3, p) = pk(contrib, 0u);
     W.mark[p] = (uint8_t)((k << 1) | (cont ? 0u : 1u));
     return nee;
@@ -519,17 +562,19 @@ __device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
-    __shared__ uint32_t app[5];
+    __shared__ uint32_t app[5], app2[2 * 5 * 2];
     if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t n = *cnt_closest(W, g);
     const float4 *rays = W.ray[g & 1];
     const uint4 *hits = W.hit[g & 1];
     float4 *next_rays = W.ray[(g + 1) & 1];
+    uint32_t *const queues[2] = {cnt_shadow(W, g), cnt_closest(W, g + 1)};
+    uint32_t it = 0;
     // fused camera (WfArgs::cam_fused): ray i of generation 1 is path i's, from the eye; no wf_camera
     // cleared its resolve mark or counted it
     const bool fused = g == 1 && W.cam_fused;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x, it++) {
         const uint32_t i = base + threadIdx.x;
         const bool in = i < n;
         uint4 h = make_uint4(0u, 0u, 0u, 0u);
@@ -551,15 +596,19 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         if (W.fold == 1 && g >= 2 && in && p != NO_PATH) resolve_prev(W, p, g - 1);
         bool textured = false, nee = false, cont = false;
         ShadowRay sh = {mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, 0u};
-        f3 org = mk(0.f, 0.f, 0.f), wi = mk(0.f, 0.f, 0.f);
+        f3 org = mk(0.f, 0.f, 0.f), wi = mk(0.f, 0.f, 0.f), direct = mk(0.f, 0.f, 0.f);
         if (in && !hit) {
             if (p != NO_PATH) finish_path(A, W, p, g, mk(A.bg[0], A.bg[1], A.bg[2]));
         } else if (hit) {
-            nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi, ctr);
+            nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi, ctr, direct);
         }
-        const uint32_t j = block_append(cnt_shadow(W, g), nee, app);
+        // shadow queue g and closest queue g + 1 in one barrier round (uniform: the whole block)
+        const bool want[2] = {nee, cont};
+        uint32_t slots[2];
+        block_append_n<2>(queues, want, app2, it & 1u, slots);
+        const uint32_t j = slots[0], jc = slots[1];
+        if (hit) W.dw[(size_t)(2 * (g - 1)) * W.P + p] = pk(direct, nee ? j : NO_SLOT);
         if (nee) {
-            W.dw[(size_t)(2 * (g - 1)) * W.P + p].w = __uint_as_float(j);
             W.sray[2 * (size_t)j] = pk(sh.o, p);
             W.sray[2 * (size_t)j + 1] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
             W.sexcl[j] = sh.light | (cont ? SEXCL_CONT : 0u);
@@ -575,7 +624,6 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
             const uint32_t je = block_append(cnt_ended(W, g), ends, app);
             if (ends) W.ended[je] = p;
         }
-        const uint32_t jc = block_append(cnt_closest(W, g + 1), cont, app);
         if (cont) {
             next_rays[2 * (size_t)jc] = pk(org, p);
             next_rays[2 * (size_t)jc + 1] = pk(wi, W.ctl_ray ? ctr : 0u);
