@@ -213,6 +213,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         uint64_t chunk = std::max<uint64_t>(1, c->sample_buf / std::max<uint64_t>(per_sample, 1));
         chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(1, (1ull << 31) / std::max<uint32_t>(A.n_items, 1)));
         chunk = std::min<uint64_t>(chunk, spp_pass);
+        // a chunk of a multiple of 16 samples (sum_samples_lds stages 16 at a time and needs runs of a
+        // multiple of 4; the last chunk then has spp mod 4 == its own mod 4)
+        if (chunk < spp_pass && chunk >= 16) chunk &= ~(uint64_t)15;
         const bool chunked = chunk < spp_pass;
         if (nl > 1 && chunked) return fail(c, CR_E_INVALID, "layers per pass: the samples do not fit one buffer");
         // wavefront: a second stack-overflow area for the closest trace that runs beside a
@@ -403,7 +406,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
                 e = cr::launch_persistent(A, c->waves_per_cu, c->num_cus, st);
             }
-            if (!e) e = cr::launch_sum_samples(A, s0 == 0, s0 + A.s_count == spp_pass, st);
+            if (!e) e = cr::launch_sum_samples(A, s0 == 0, s0 + A.s_count == spp_pass, st, c->sum_lds, c->sum_staged != 0);
             if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
         }
         HIPCHK(hipEventRecord(c->ev1, st));
@@ -1163,6 +1166,8 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_cam_fuse") && (v == 0 || v == 1)) c->wf_cam_fuse = (int)v;
     else if (!std::strcmp(key, "wf_ctl_ray") && (v == 0 || v == 1)) c->wf_ctl_ray = (int)v;
     else if (!std::strcmp(key, "wf_vis_dw") && (v == 0 || v == 1)) c->wf_vis_dw = (int)v;
+    else if (!std::strcmp(key, "sum_lds") && v >= 0 && v <= 65536) c->sum_lds = (uint32_t)v;
+    else if (!std::strcmp(key, "sum_staged") && (v == 0 || v == 1)) c->sum_staged = (int)v;
     else if (!std::strcmp(key, "wf_tail_waves") && v >= 4 && v <= 6) c->wf_tail_waves = (int)v;
     else if (!std::strcmp(key, "wf_side_priority") && (v == 0 || v == 1)) {
         // the second stream (closest trace g + 1 beside shadow trace g) at the device's highest

@@ -105,6 +105,8 @@ struct cr_ctx {
     // WfArgs::vis_dw; round 4, two interleaved rounds: sponza 318.1 / 317.9 -> 318.0 / 318.3 ms per layer,
     // cornell_box 105.7 / 106.1 -> 105.1 / 105.1 ms per pass
     int wf_vis_dw = 1;
+    uint32_t sum_lds = 0;           // launch_sum_samples' LDS reservation per block (occupancy cap)
+    int sum_staged = 1;             // sum_samples_lds (sample runs staged through LDS) when aligned
     int wf_tail_waves = 4;          // WfArgs::tail_waves
     uint32_t wf_dir_res_shadow = 0; // shadow queues' direction bins per axis with leaf keys (0: wf_dir_res)
     // per-sample buffer budget of one sample chunk (cr_set_option "sample_buf_bytes"); a

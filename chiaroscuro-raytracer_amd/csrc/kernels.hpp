@@ -174,7 +174,7 @@ inline size_t persistent_pathbuf_bytes(int K, uint32_t threads) {
 enum : uint64_t { SAMPLE_BUF_BYTES = 4ull << 30 };
 int launch_persistent(const RenderArgs &A, uint32_t waves_per_cu, int num_cus, hipStream_t st);
 // Per-pixel in-order sum of one chunk's samples; `last` blends / writes the pixel.
-int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t st);
+int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t st, uint32_t lds = 0, bool staged = true);
 
 // Wavefront path tracer (wavefront.hip, cr_set_option "kernel" 2): the paths of
 // work items [w0, w0 + P) advance one bounce per generation through separate

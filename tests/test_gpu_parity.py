@@ -665,6 +665,44 @@ def test_c5_sample_chunking_progressive(ca, sponza, nanobox, kernel):
             pair.dev.set_option("kernel", 2)
 
 
+@pytest.mark.parametrize("staged", [1, 0])
+def test_sum_samples_staged_bitexact(ca, nanobox, staged):
+    """sum_samples_lds (the default when a pass's samples per pixel are a multiple of 4: the runs staged
+    through LDS 16 samples at a time) and the thread-per-pixel sum_samples add the same samples in the
+    same order: spp 20 and 36 (chunks straddling the 16-sample stage), sample chunks of 8 + 8 + 4
+    (sample_buf_bytes), and 3 layers of 20 spp in one pass (layer boundaries inside a stage),
+    bit-exact against the oracle."""
+    import torch
+    pair, (x, y) = nanobox, (70, 45)
+    dev = pair.dev
+    cam = pair.camera(ca, x, y)
+    dev.set_option("kernel", 2)
+    dev.set_option("counters", 0)
+    dev.set_option("sum_staged", staged)
+    try:
+        for spp, buf in ((20, 4 << 30), (36, 4 << 30), (20, x * y * 12 * 8)):
+            dev.set_option("sample_buf_bytes", buf)
+            o = None
+            for layer in (1, 2):
+                g = dev.render(cam, ca.render_params(x, y, spp, 6, 0xC41A05C0, layer=layer), None)
+                o, _ = pair.oracle.render(cam.as_array(), x, y, spp, 6, 0xC41A05C0, layer=layer, pixels=o)
+                assert_bitwise(g, o, "sum_staged %d spp %d buf %d layer %d" % (staged, spp, buf, layer))
+        dev.set_option("sample_buf_bytes", 4 << 30)
+        p = ca.render_params(x, y, 20, 6, 0xC41A05C0, layer=1)
+        assert dev.layers_per_pass(p, 3) == 3
+        frame = torch.zeros((y, x, 3), dtype=torch.float32, device="cuda")
+        dev.render_layers_device(cam, p, 3, frame.data_ptr())
+        torch.cuda.synchronize()
+        o = None
+        for layer in (1, 2, 3):
+            o, _ = pair.oracle.render(cam.as_array(), x, y, 20, 6, 0xC41A05C0, layer=layer, pixels=o)
+        assert_bitwise(frame.cpu().numpy(), o, "sum_staged %d, 3 layers x 20 spp in one pass" % staged)
+    finally:
+        dev.set_option("sum_staged", 1)
+        dev.set_option("sample_buf_bytes", 4 << 30)
+        dev.set_option("counters", 1)
+
+
 @pytest.mark.parametrize("lanes", [1, 2])
 def test_c5_multi_chunk_wavefront(ca, sponza, nanobox, lanes):
     """More work items than path slots: the wavefront runs chunk after chunk of
