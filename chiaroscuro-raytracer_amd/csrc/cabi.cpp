@@ -344,6 +344,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cam_fused = c->wf_cam_fuse;
                 W.ctl_ray = c->wf_ctl_ray;
                 W.vis_dw = c->wf_vis_dw;
+                W.nee_skip = c->wf_nee_skip;
                 W.tail_waves = c->wf_tail_waves;
                 if (sort) {
                     for (int q = 0; q < 2; q++)
@@ -1167,6 +1168,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_ctl_ray") && (v == 0 || v == 1)) c->wf_ctl_ray = (int)v;
     else if (!std::strcmp(key, "wf_vis_dw") && (v == 0 || v == 1)) c->wf_vis_dw = (int)v;
     else if (!std::strcmp(key, "sum_lds") && v >= 0 && v <= 65536) c->sum_lds = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_nee_skip") && (v == 0 || v == 1)) c->wf_nee_skip = (int)v;
     else if (!std::strcmp(key, "sum_staged") && (v == 0 || v == 1)) c->sum_staged = (int)v;
     else if (!std::strcmp(key, "wf_tail_waves") && v >= 4 && v <= 6) c->wf_tail_waves = (int)v;
     else if (!std::strcmp(key, "wf_side_priority") && (v == 0 || v == 1)) {

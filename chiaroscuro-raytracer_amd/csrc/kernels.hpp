@@ -266,6 +266,10 @@ struct WfArgs {
     // that bounce (SHADOW_VIS / SHADOW_OCC) instead of occ[slot] -- wf_resolve then reads no occ entries,
     // which a sorted shadow queue scatters over the paths (option "wf_vis_dw")
     int vis_dw;
+    // 1: an NEE query whose contribution is exactly zero is answered without a trace (wavefront.hip
+    // nee_zero; lean builds only -- the counting and performed-work builds trace every query) and
+    // counted as a shadow query (option "wf_nee_skip")
+    int nee_skip;
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position, ended list, resolve mark

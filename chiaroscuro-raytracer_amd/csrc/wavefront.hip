@@ -244,6 +244,14 @@ __device__ __forceinline__ void shadow_store(const WfArgs &W, uint32_t g, uint32
     if (W.vis_dw) ((uint32_t *)(W.dw + (size_t)(2 * (g - 1)) * W.P + idx))[3] = occluded ? SHADOW_OCC : SHADOW_VIS;
     else W.occ[idx] = occluded ? 1u : 0u;
 }
+// WfArgs::nee_skip: an NEE term of exactly (+0, +0, +0) -- the reference's geometric factor max(0, ...)
+// is 0 (the surface or the light faces away), or the product underflows -- adds nothing whatever the
+// shadow query answers (direct + (+0) == direct: direct is +0 or positive, rayTracer.cpp:85), so the
+// query is answered without a traversal and counted as the root-box culls are.
+__device__ __forceinline__ bool nee_zero(const WfArgs &W, const RenderArgs &A, f3 contrib) {
+    return W.nee_skip && !A.full_counters && !A.perf_counters &&
+           (__float_as_uint(contrib.x) | __float_as_uint(contrib.y) | __float_as_uint(contrib.z)) == 0u;
+}
 // true: the NEE ray of a bounce whose dw record's w is `slot` found no occluder
 __device__ __forceinline__ bool nee_visible(const WfArgs &W, uint32_t slot) {
     return slot != NO_SLOT && (W.vis_dw ? slot == SHADOW_VIS : W.occ[slot] == 0u);
@@ -436,7 +444,7 @@ __device__ __forceinline__ bool shade_path(const RenderArgs &A, const WfArgs &W,
         sh.d = e.dir;
         sh.dist = e.distance;
         sh.light = e.light;
-        nee = true;
+        nee = !nee_zero(W, A, contrib); // (the caller counts the query either way)
     }
     PS(W, 0, p) = pk(hs.direct, 0u);
     PS(W, 1, p) = pk(hs.fcol, 0u);
@@ -489,10 +497,11 @@ __device__ __forceinline__ bool bounce_path(const RenderArgs &A, const WfArgs &W
 // the mark 2k tells wf_resolve's path-order sweep which paths hit at bounce k.
 // A continuing path gets W_k in dw[2(k-1)+1] and its next closest ray (org, wi).
 // ctr: W.ctl_ray -- the RNG counter the closest ray carries (in: this bounce's, out: the next ray's)
+// skipped: the NEE query was answered without a trace (nee_zero; the return value is then false)
 // direct: the bounce's emission + direct term, for the caller's dw[2(k-1)] = {direct, shadow slot}
 __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t k, f3 ro, uint4 h,
                                            bool &textured, ShadowRay &sh, bool &cont, f3 &org, f3 &wi, uint32_t &ctr,
-                                           f3 &direct) {
+                                           f3 &direct, bool &skipped) {
     const DevScene &S = A.S;
     const HitShade hs = shade_hit(S, ro, h.x, __uint_as_float(h.y), __uint_as_float(h.z), (int)k);
     textured = hs.textured;
@@ -517,6 +526,8 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
         sh.dist = e.distance;
         sh.light = e.light;
         nee = true;
+        skipped = nee_zero(W, A, contrib);
+        nee = !skipped;
     }
     cont = false;
     if ((int)k != A.K) {
@@ -594,14 +605,15 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         }
         // (fold: bounce g - 1 of every path read here, hit or miss, before it is folded or shaded on)
         if (W.fold == 1 && g >= 2 && in && p != NO_PATH) resolve_prev(W, p, g - 1);
-        bool textured = false, nee = false, cont = false;
+        bool textured = false, nee = false, cont = false, skipped = false;
         ShadowRay sh = {mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, 0u};
         f3 org = mk(0.f, 0.f, 0.f), wi = mk(0.f, 0.f, 0.f), direct = mk(0.f, 0.f, 0.f);
         if (in && !hit) {
             if (p != NO_PATH) finish_path(A, W, p, g, mk(A.bg[0], A.bg[1], A.bg[2]));
         } else if (hit) {
-            nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi, ctr, direct);
+            nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi, ctr, direct, skipped);
         }
+        tally(tl, T_SHADOW, skipped); // (a query, answered here)
         // shadow queue g and closest queue g + 1 in one barrier round (uniform: the whole block)
         const bool want[2] = {nee, cont};
         uint32_t slots[2];
@@ -809,6 +821,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                     nshadow++;
                     state = trav_begin(S, o, d, true, sh.dist, T) ? ST_SHADOW : ST_VISIBLE;
                 } else {
+                    if (S.nlights) nshadow++; // (nee_zero: a query answered without a trace)
                     state = ST_OCCLUDED; // no NEE term: bounce without the contribution
                 }
             } else { // ST_VISIBLE / ST_OCCLUDED: the bounce

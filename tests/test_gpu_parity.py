@@ -23,6 +23,7 @@ TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
 # builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="37 38"
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
+SKIP_DEFAULT = 0  # ctx.hpp wf_nee_skip
 
 
 @pytest.fixture(scope="module")
@@ -143,21 +144,26 @@ def test_wavefront_shade_waves_bitexact(ca, sponza, nanobox, waves):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("fuse,ctl,fold,resolve_paths", [(1, 0, 0, 16), (1, 0, 0, 0), (1, 0, 1, 16), (0, 0, 0, 16),
-                                                         (0, 1, 0, 16), (1, 1, 0, 16), (1, 1, 1, 16), (1, 1, 0, 0)])
-def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, resolve_paths):
+@pytest.mark.parametrize("fuse,ctl,fold,resolve_paths,skip", [(1, 0, 0, 16, 0), (1, 0, 0, 0, 0), (1, 0, 1, 16, 0),
+                                                              (0, 0, 0, 16, 0), (0, 1, 0, 16, 0), (1, 1, 0, 16, 0),
+                                                              (1, 1, 1, 16, 0), (1, 1, 0, 0, 0), (1, 1, 0, 16, 1),
+                                                              (1, 1, 1, 16, 1), (0, 0, 0, 0, 1)])
+def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, resolve_paths, skip):
     """wf_cam_fuse 1: no wf_camera launch -- the packet camera trace makes each path's ray from its
     (pixel, sample), wf_shade(1) takes path p = ray p from the eye, clears the resolve mark of a path
     that missed and counts the paths; partial-tile slots carry a dead-ray record.  The same bits and
     counters over layers 1..3 on the same buffers (a mark an earlier layer or chunk left must not
     resolve a path), one chunk and wf_paths 4096 chunks, partial tiles (96 x 54, 3 x 2).  wf_ctl_ray 1: a
-    secondary closest ray carries its path's RNG counter, the key is re-derived from (pixel, sample)."""
+    secondary closest ray carries its path's RNG counter, the key is re-derived from (pixel, sample).
+    wf_nee_skip 1: an NEE query whose contribution is exactly zero is answered without a trace and
+    counted -- the shadow-query count stays the oracle's."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4)), (nanobox, (3, 2, 1))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_cam_fuse", fuse)
         pair.dev.set_option("wf_ctl_ray", ctl)
         pair.dev.set_option("wf_fold", fold)
         pair.dev.set_option("wf_resolve_paths", resolve_paths)
+        pair.dev.set_option("wf_nee_skip", skip)
         pair.dev.set_option("counters", 0)  # the lean builds: the packet camera trace
         cam = pair.camera(ca, x, y)
         keys = ("closest", "shadow", "hit", "texhit", "paths")
@@ -177,6 +183,7 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, r
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_cam_fuse", 1)
             pair.dev.set_option("wf_ctl_ray", 1)
+            pair.dev.set_option("wf_nee_skip", SKIP_DEFAULT)
             pair.dev.set_option("wf_fold", 0)
             pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_paths", 256 << 20)
@@ -377,10 +384,11 @@ def test_wavefront_two_lanes_bitexact(ca, sponza, nanobox, cornell, lanes):
 
 
 @pytest.mark.parametrize("tail_min", [1 << 30, 12000, 3000])
-@pytest.mark.parametrize("overlap,fold,ctl,vis", [(1, 1, 0, 0), (0, 1, 0, 0), (1, 2, 0, 0), (0, 2, 0, 0), (1, 0, 0, 0),
-                                                  (0, 0, 0, 0), (1, 0, 1, 0), (0, 0, 1, 0), (0, 1, 1, 0), (1, 0, 1, 1),
-                                                  (0, 0, 1, 1), (1, 1, 1, 1), (1, 2, 1, 1)])
-def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap, fold, ctl, vis):
+@pytest.mark.parametrize("overlap,fold,ctl,vis,skip", [(1, 1, 0, 0, 0), (0, 1, 0, 0, 0), (1, 2, 0, 0, 0), (0, 2, 0, 0, 0),
+                                                       (1, 0, 0, 0, 0), (0, 0, 0, 0, 0), (1, 0, 1, 0, 0), (0, 0, 1, 0, 0),
+                                                       (0, 1, 1, 0, 0), (1, 0, 1, 1, 0), (0, 0, 1, 1, 0), (1, 1, 1, 1, 0),
+                                                       (1, 2, 1, 1, 0), (1, 0, 1, 1, 1), (0, 0, 1, 1, 1), (1, 1, 1, 1, 1)])
+def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap, fold, ctl, vis, skip):
     """wf_tail (the last generations of a chunk in one launch, per-path bodies
     shared with wf_shade / wf_bounce): from generation 1 (every queue is below
     1 << 30) and from later generations, counting and lean builds; after the last shadow trace
@@ -394,10 +402,12 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
         pair.dev.set_option("wf_fold", fold)
         pair.dev.set_option("wf_ctl_ray", ctl)
         pair.dev.set_option("wf_vis_dw", vis)
+        pair.dev.set_option("wf_nee_skip", skip)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
             pair.dev.set_option("counters", 0)
             g_lean = pair.dev.render(pair.camera(ca, x, y), ca.render_params(x, y, s, 6, 0xC41A05C0))
+            lc = pair.dev.counters()
             ts = pair.dev.trace_stats()
         finally:
             pair.dev.set_option("counters", 1)
@@ -406,8 +416,10 @@ def test_wavefront_tail_bitexact(ca, sponza, nanobox, cornell, tail_min, overlap
             pair.dev.set_option("wf_fold", 0)
             pair.dev.set_option("wf_ctl_ray", 1)
             pair.dev.set_option("wf_vis_dw", VIS_DEFAULT)
+            pair.dev.set_option("wf_nee_skip", SKIP_DEFAULT)
         assert_bitwise(g, o, "wavefront tail_min %d %dx%dx%d" % (tail_min, x, y, s))
         assert_bitwise(g_lean, o, "wavefront tail_min %d lean" % tail_min)
+        assert (lc["closest"], lc["shadow"]) == (oc["closest"], oc["shadow"])
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
         assert ts["tail"]["launches"] == 1
         if tail_min == 1 << 30:
