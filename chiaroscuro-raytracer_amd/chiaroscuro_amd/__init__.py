@@ -47,7 +47,7 @@ class CrRenderParams(C.Structure):
 COUNTER_NAMES = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths", "pixels",
                  "wave_desc", "wave_tri", "wave_round", "wave_query", "wave_desc_uniform", "wave_tri_uniform",
                  "wave_desc_lines", "wave_tri_lines",
-                 "leaf_rounds", "leaf_distinct", "leaf_records", "leaf_fit21", "leaf_fit56")
+                 "leaf_rounds", "leaf_distinct", "leaf_records", "leaf_fit21", "leaf_fit56", "nee_answered")
 
 
 class CrCounters(C.Structure):

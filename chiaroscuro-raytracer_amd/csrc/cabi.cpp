@@ -424,7 +424,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
     c->last = cr_counters{h[0], h[1],  h[2],  h[3],  h[4],  h[5],  h[6],  h[7], h[8],
                           h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16],
-                          h[17], h[18], h[19], h[20], h[21]};
+                          h[17], h[18], h[19], h[20], h[21], h[cr::CTR_NEE]};
     for (int i = 0; i < cr::DIAG_N; i++) c->last_diag[i] = h[cr::CTR_DIAG + i];
     for (int i = 0; i < cr::TK_N * cr::PERF_N; i++) c->last_perf[i] = h[cr::CTR_PERF + i];
     c->last_trace = cr_trace_stats{};
@@ -1111,7 +1111,7 @@ static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, cons
     if (e != hipSuccess) return hip_fail(c, e, "intersect");
     c->last = cr_counters{h[0], h[1],  h[2],  h[3],  h[4],  h[5],  h[6],  h[7], h[8],
                           h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16],
-                          h[17], h[18], h[19], h[20], h[21]};
+                          h[17], h[18], h[19], h[20], h[21], h[cr::CTR_NEE]};
     return CR_OK;
 }
 

@@ -16,6 +16,8 @@ enum { TK_CAMERA = 0, TK_CLOSEST = 1, TK_SHADOW = 2, TK_TAIL = 3, TK_N = 4 };
 // Counting builds of the trace kernels also tally inner / leaf / tritest per kind
 // (not the tail): slots CTR_TRACE + 3 * kind + {0, 1, 2}.
 enum { CTR_TRACE = 24 };
+// slot of cr_counters::nee_answered (shadow queries answered without a trace, WfArgs::nee_skip)
+enum { CTR_NEE = 22 };
 // Leaf-round and repeated-miss diagnostics of counting builds (cr_get_diag, DIAG_* order),
 // for the trace kinds in RenderArgs::diag_kinds (bit 1 << TK_*): slots CTR_DIAG + i.
 enum { CTR_DIAG = 40, DIAG_N = 16 };

@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(256, MINW) render_dynamic(RenderArgs A) {
     }
     flush_counters(A.counters, c, 0u);
     __syncthreads();
-    if (threadIdx.x < T_N && tl[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], tl[threadIdx.x]);
+    if (threadIdx.x < T_N && tl[threadIdx.x]) atomicAdd(&A.counters[tally_slot(threadIdx.x)], tl[threadIdx.x]);
 }
 
 // Per pixel: add this launch's samples in sample order onto the running sum

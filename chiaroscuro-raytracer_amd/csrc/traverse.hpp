@@ -779,7 +779,9 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
 
 // Per-query tallies are wave-aggregated LDS atomics: the callers run in
 // divergent code, so a wave total cannot be kept wave-uniform in registers.
-enum : int { T_CLOSEST = 0, T_SHADOW = 1, T_HIT = 5, T_TEXHIT = 6, T_PATHS = 7, T_PIXELS = 8, T_N = 9 };
+enum : int { T_CLOSEST = 0, T_SHADOW = 1, T_HIT = 5, T_TEXHIT = 6, T_PATHS = 7, T_PIXELS = 8, T_NEE = 9, T_N = 10 };
+// the device counter slot of tally i (T_NEE: CTR_NEE, past the cr_counters fields of the Ctr order)
+__device__ __forceinline__ int tally_slot(int i) { return i == T_NEE ? CTR_NEE : i; }
 __device__ __forceinline__ void tally(unsigned long long *tl, int i, bool pred) {
     const uint64_t b = __ballot(pred);
     if (b && wave_leader()) atomicAdd(&tl[i], (unsigned long long)__popcll(b));

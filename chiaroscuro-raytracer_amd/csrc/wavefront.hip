@@ -156,7 +156,7 @@ __device__ __forceinline__ uint32_t sort_key(const RenderArgs &A, const WfArgs &
 
 __device__ __forceinline__ void flush_tallies(const RenderArgs &A, unsigned long long *tl) {
     __syncthreads();
-    if (threadIdx.x < T_N && tl[threadIdx.x]) atomicAdd(&A.counters[threadIdx.x], tl[threadIdx.x]);
+    if (threadIdx.x < T_N && tl[threadIdx.x]) atomicAdd(&A.counters[tally_slot(threadIdx.x)], tl[threadIdx.x]);
 }
 
 // Back-to-front fold of a finished path (r_j = D_j + W_j * r_{j+1}) into samples[w].
@@ -614,6 +614,7 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
             nee = shade_next(A, W, p, g, ld3(r0), h, textured, sh, cont, org, wi, ctr, direct, skipped);
         }
         tally(tl, T_SHADOW, skipped); // (a query, answered here)
+        tally(tl, T_NEE, skipped);
         // shadow queue g and closest queue g + 1 in one barrier round (uniform: the whole block)
         const bool want[2] = {nee, cont};
         uint32_t slots[2];
@@ -821,7 +822,10 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                     nshadow++;
                     state = trav_begin(S, o, d, true, sh.dist, T) ? ST_SHADOW : ST_VISIBLE;
                 } else {
-                    if (S.nlights) nshadow++; // (nee_zero: a query answered without a trace)
+                    if (S.nlights) { // (nee_zero: a query answered without a trace)
+                        nshadow++;
+                        tally(tl, T_NEE, true);
+                    }
                     state = ST_OCCLUDED; // no NEE term: bounce without the contribution
                 }
             } else { // ST_VISIBLE / ST_OCCLUDED: the bounce

@@ -159,6 +159,9 @@ typedef struct {
     uint64_t leaf_records;
     uint64_t leaf_fit21;
     uint64_t leaf_fit56;
+    /* of `shadow`: NEE queries answered without a trace because their contribution is exactly zero
+     * (cr_set_option "wf_nee_skip"; lean wavefront builds) */
+    uint64_t nee_answered;
 } cr_counters;
 
 cr_ctx *cr_create(int device);

@@ -179,6 +179,10 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, r
                     o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
                     assert_bitwise(g, o, "cam_fuse %d ctl_ray %d fold %d wf_paths %d layer %d" % (fuse, ctl, fold, paths, layer))
                     assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
+                    if not skip:
+                        assert gc["nee_answered"] == 0
+                    elif pair is sponza:  # (its ceilings and arches face away from the sky light)
+                        assert 0 < gc["nee_answered"] <= gc["shadow"]
         finally:
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_cam_fuse", 1)
