@@ -363,7 +363,7 @@ def run_rank(args, world, backend):
     stream = backend.stream()
     fr = DistributedFrame(dev, xres, yres, rank, world, tile, dist, device=backend.device, gather=args.gather)
 
-    totals = {"rays": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0,
+    totals = {"rays": 0, "nee_answered": 0, "kernel_ms": 0.0, "bytes": 0, "launches": 0, "tritest": 0, "px": 0,
               "trace_ms": [0.0] * 4, "trace_launches": [0] * 4}
     wavefront = args.kernel in (-1, 2)
 
@@ -395,6 +395,7 @@ def run_rank(args, world, backend):
             st = fr.last_stats()
             c = st["counters"]
             totals["rays"] += c["closest"] + c["shadow"]
+            totals["nee_answered"] += c.get("nee_answered", 0)
             totals["kernel_ms"] += st["kernel_ms"]
             totals["px"] += c["pixels"]
             totals["launches"] += n  # layers: kernel_ms / launches is the render time per layer
@@ -460,8 +461,8 @@ def run_rank(args, world, backend):
                 times.append((time.perf_counter() - ts) * 1e3)
         single_ms = sum(times) / len(times)
     # per rank: wall time, device time of its render passes (HIP events), rays
-    mine = torch.tensor([elapsed, totals["kernel_ms"] / max(totals["launches"], 1), totals["rays"]],
-                        dtype=torch.float64, device=backend.device)
+    mine = torch.tensor([elapsed, totals["kernel_ms"] / max(totals["launches"], 1), totals["rays"],
+                         totals["nee_answered"]], dtype=torch.float64, device=backend.device)
     if dist:
         per_rank = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(per_rank, mine)
@@ -470,6 +471,7 @@ def run_rank(args, world, backend):
         per_rank = [mine.cpu().tolist()]
     elapsed = max(r[0] for r in per_rank)   # the step ends with the slowest rank
     rays_all = float(sum(r[2] for r in per_rank))
+    nee_all = float(sum(r[3] for r in per_rank))
     rank_render_ms = [round(r[1], 3) for r in per_rank]
 
     # counting pass (untimed): algorithmic bytes of one launch of this rank
@@ -644,6 +646,9 @@ def run_rank(args, world, backend):
             "config": {"workload": label, "spp_per_step": spp, "k": k, "tile": tile,
                        "parallelism": "tile-split x%d" % world, "gather": args.gather if world > 1 else None,
                        "rays": int(rays_all),
+                       # of those, NEE shadow queries whose contribution is exactly zero, answered without a
+                       # traversal (wf_nee_skip; the image cannot change) -- counted as the reference traces them
+                       "rays_answered_untraced": int(nee_all),
                        "rank_render_ms": rank_render_ms, "layers_per_pass": nl_pass,
                        "pass_groups": [list(g) for g in groups], "trace_build": timed_build,
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},

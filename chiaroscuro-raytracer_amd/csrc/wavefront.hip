@@ -246,11 +246,17 @@ __device__ __forceinline__ void shadow_store(const WfArgs &W, uint32_t g, uint32
 }
 // WfArgs::nee_skip: an NEE term of exactly (+0, +0, +0) -- the reference's geometric factor max(0, ...)
 // is 0 (the surface or the light faces away), or the product underflows -- adds nothing whatever the
-// shadow query answers (direct + (+0) == direct: direct is +0 or positive, rayTracer.cpp:85), so the
-// query is answered without a traversal and counted as the root-box culls are.
-__device__ __forceinline__ bool nee_zero(const WfArgs &W, const RenderArgs &A, f3 contrib) {
+// shadow query answers: direct + (+0) == direct bit for bit unless a component of direct is -0 or a NaN
+// (rayTracer.cpp:85 makes it +0 or positive; checked anyway), so the query is answered without a
+// traversal and counted as the root-box culls are.
+__device__ __forceinline__ bool keeps_plus_zero(float v) { // v + (+0) has v's bits
+    const uint32_t b = __float_as_uint(v);
+    return b != 0x80000000u && (b & 0x7fffffffu) <= 0x7f800000u;
+}
+__device__ __forceinline__ bool nee_zero(const WfArgs &W, const RenderArgs &A, f3 contrib, f3 direct) {
     return W.nee_skip && !A.full_counters && !A.perf_counters &&
-           (__float_as_uint(contrib.x) | __float_as_uint(contrib.y) | __float_as_uint(contrib.z)) == 0u;
+           (__float_as_uint(contrib.x) | __float_as_uint(contrib.y) | __float_as_uint(contrib.z)) == 0u &&
+           keeps_plus_zero(direct.x) && keeps_plus_zero(direct.y) && keeps_plus_zero(direct.z);
 }
 // true: the NEE ray of a bounce whose dw record's w is `slot` found no occluder
 __device__ __forceinline__ bool nee_visible(const WfArgs &W, uint32_t slot) {
@@ -444,7 +450,7 @@ __device__ __forceinline__ bool shade_path(const RenderArgs &A, const WfArgs &W,
         sh.d = e.dir;
         sh.dist = e.distance;
         sh.light = e.light;
-        nee = !nee_zero(W, A, contrib); // (the caller counts the query either way)
+        nee = !nee_zero(W, A, contrib, hs.direct); // (the caller counts the query either way)
     }
     PS(W, 0, p) = pk(hs.direct, 0u);
     PS(W, 1, p) = pk(hs.fcol, 0u);
@@ -526,7 +532,7 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
         sh.dist = e.distance;
         sh.light = e.light;
         nee = true;
-        skipped = nee_zero(W, A, contrib);
+        skipped = nee_zero(W, A, contrib, hs.direct);
         nee = !skipped;
     }
     cont = false;

@@ -23,7 +23,7 @@ TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
 # builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="37 38"
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
-SKIP_DEFAULT = 0  # ctx.hpp wf_nee_skip
+SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
 
 
 @pytest.fixture(scope="module")
