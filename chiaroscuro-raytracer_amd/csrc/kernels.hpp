@@ -160,6 +160,8 @@ struct RenderArgs {
     uint32_t diag_kinds;          // counting builds: trace kinds (1 << TK_*) the DIAG_* slots describe
     int lc_debug;                 // measurement only: leaf-cull masks 1 = every reference, 2 = none (wrong images)
     uint32_t lc_min;              // leaf-cull builds: leaves with fewer references are tested without the check
+    uint32_t desc_quorum;         // lean wavefront traces: a round's descent stops once at most desc_quorum / 64
+                                  // of its lanes still descend (they go on next round); 0: every lane reaches a leaf
 };
 int num_persistent_variants();
 

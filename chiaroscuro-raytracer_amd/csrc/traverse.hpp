@@ -315,8 +315,14 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
-                                               Prof *pf = nullptr, Pc *pc = nullptr) {
+                                               Prof *pf = nullptr, Pc *pc = nullptr, uint32_t quorum = 0) {
     uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
+    // quorum (lean FAT builds without the camera cull): the wave's descent stops at a fetch once at most
+    // quorum / 64 of the lanes that entered the round still descend; those keep T.node (the node to fetch)
+    // and their interval and go on next round -- the same node visits with the same intervals, so the
+    // same answers -- while the others test their leaves now instead of idling
+    const uint32_t nbusy = quorum ? (uint32_t)__popcll(__ballot(1)) : 0u;
+    bool pending = false;
     if (pf) pt0 = prof_now();
     if (pc && wave_leader()) pc->waves++;
     // performed-work accounting of record loads (pc: perf builds)
@@ -350,7 +356,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         const uint32_t a = nd.y & 3u;
         const float split = __uint_as_float(nd.x);
         const float oa = comp(o, a), da = comp(d, a);
-        const float tsplit = FD ? div_by_rcp(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
+        const float tsplit = FD ? div_by_rcp_wave(split - oa, da, comp(T.r, a)) : split_distance(split, oa, da);
         const uint32_t below = (oa < split) || (oa == split && da <= 0);
         const uint32_t child = nd.y >> 2;
         uint32_t k;
@@ -454,6 +460,10 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             nd = k ? make_uint2(f1.x, f1.y) : make_uint2(f0.z, f0.w);
             if ((nd.y & 3u) == 3u) break;
             step(nd);
+            if (!FULL && !CULL && quorum && (uint32_t)__popcll(__ballot(1)) * 64u <= nbusy * quorum) {
+                pending = true;
+                break;
+            }
             fetch(T.node);
         }
     } else {
@@ -465,6 +475,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             nd = load_node<SC>(S, T.node);
         }
     }
+    if (pending) return shadow ? ST_SHADOW : ST_CLOSEST; // descends on next round from T.node
     if (FULL) {
         c.leaf++;
         if (wave_leader()) c.wave_round++;

@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
         if (state == busy_st) {
             const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC>(A.lc_debug, A.lc_min,
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
-                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr);
+                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr, A.desc_quorum);
             if (r != busy_st) {
                 if (PC) pc.vb += SHADOW ? 4u : 16u;
                 if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
@@ -925,6 +925,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
     auto rfl = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
     const float box_lo[3] = {rfl(Sc.bmin.x - eye.x), rfl(Sc.bmin.y - eye.y), rfl(Sc.bmin.z - eye.z)};
     const float box_hi[3] = {rfl(Sc.bmax.x - eye.x), rfl(Sc.bmax.y - eye.y), rfl(Sc.bmax.z - eye.z)};
+    const float eye_s[3] = {rfl(eye.x), rfl(eye.y), rfl(eye.z)};
     const uint32_t INACTIVE = 0xffffffffu;
     Ctr c = {};
     Pc pc = {};
@@ -1143,7 +1144,33 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                 }
                 const uint32_t a = nd.y & 3u, child = nd.y >> 2;
                 const float split = __uint_as_float(nd.x);
-                const float oa = comp(eye, a);
+                // the split axis is wave-uniform: the lanes' components are picked by scalar branches
+                // (one move per value, kept apart by the asm) instead of two v_cndmask per value
+                float oa, da[S], ya[S];
+                auto pick = [&](float e, const float (&dv)[S], const float (&yv)[S]) {
+                    oa = e;
+#pragma unroll
+                    for (int s = 0; s < S; s++) {
+                        asm volatile("v_mov_b32 %0, %1" : "=v"(da[s]) : "v"(dv[s]));
+                        asm volatile("v_mov_b32 %0, %1" : "=v"(ya[s]) : "v"(yv[s]));
+                    }
+                };
+                if (a == 0) {
+                    float dv[S], yv[S];
+#pragma unroll
+                    for (int s = 0; s < S; s++) dv[s] = d[s].x, yv[s] = y[s].x;
+                    pick(eye_s[0], dv, yv);
+                } else if (a == 1) {
+                    float dv[S], yv[S];
+#pragma unroll
+                    for (int s = 0; s < S; s++) dv[s] = d[s].y, yv[s] = y[s].y;
+                    pick(eye_s[1], dv, yv);
+                } else {
+                    float dv[S], yv[S];
+#pragma unroll
+                    for (int s = 0; s < S; s++) dv[s] = d[s].z, yv[s] = y[s].z;
+                    pick(eye_s[2], dv, yv);
+                }
                 const uint32_t below = oa < split ? 1u : 0u; // uniform: the eye is not on the plane
                 const uint32_t nearc = child + (1u - below), farc = child + below;
                 // (bitwise logic on the lane masks: no short-circuit branches)
@@ -1152,8 +1179,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
 #pragma unroll
                 for (int s = 0; s < S; s++) {
                     if (PC) pc.steps += active[s] ? 1u : 0u;
-                    tsp[s] = FD ? div_by_rcp_wave(split - oa, comp(d[s], a), comp(y[s], a))
-                                : split_distance(split, oa, comp(d[s], a));
+                    tsp[s] = FD ? div_by_rcp_wave(split - oa, da[s], ya[s]) : split_distance(split, oa, da[s]);
                     crosses[s] = !(tsp[s] >= tmax[s]) & !(tsp[s] < 0.f); // !near_only
                     after[s] = !(tsp[s] <= tmin[s]);                     // far_only = crosses & !after
                     to_near[s] = active[s] & (!crosses[s] | after[s]);

@@ -24,6 +24,7 @@ TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
+QUORUM_DEFAULT = 0  # ctx.hpp desc_quorum
 
 
 @pytest.fixture(scope="module")
@@ -191,6 +192,34 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, r
             pair.dev.set_option("wf_fold", 0)
             pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_paths", 256 << 20)
+
+
+@pytest.mark.parametrize("quorum", [1, 16, 32, 64])
+def test_wavefront_desc_quorum_bitexact(ca, sponza, nanobox, quorum):
+    """desc_quorum q: a wave's descent round stops at a node fetch once at most q / 64 of its lanes still
+    descend; those lanes keep their node and interval and descend on next round (64: after every fetch).
+    The lean builds 43 / 44, sorted queues, several layers: the same bits and query counters."""
+    for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("desc_quorum", quorum)
+        pair.dev.set_option("wf_sort_min", 0)
+        pair.dev.set_option("counters", 0)
+        cam = pair.camera(ca, x, y)
+        keys = ("closest", "shadow", "hit", "texhit", "paths")
+        try:
+            o = None
+            for layer in (1, 2):
+                p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=layer)
+                g = pair.dev.render(cam, p, None)
+                gc = pair.dev.counters()
+                assert pair.dev.last_trace_build() in (43, 44)
+                o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
+                assert_bitwise(g, o, "desc_quorum %d layer %d" % (quorum, layer))
+                assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
+        finally:
+            pair.dev.set_option("counters", 1)
+            pair.dev.set_option("desc_quorum", QUORUM_DEFAULT)
+            pair.dev.set_option("wf_sort_min", 1 << 20)
 
 
 @pytest.mark.parametrize("xcd,sort_min,variant", [(7, 0, 15), (7, 1 << 20, 15), (1, 0, 15), (2, 0, 15), (4, 0, 18),
