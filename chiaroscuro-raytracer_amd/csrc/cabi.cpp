@@ -117,7 +117,11 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.diag_kinds = c->diag_kinds;
     A.lc_debug = c->lc_debug;
     A.lc_min = c->lc_min;
-    A.desc_quorum = c->desc_quorum;
+    // descent rounds end once at most 8 / 64 of a wave's lanes still descend, on scenes that take the leaf-cull
+    // build (sponza: 299.9 / 300.6 -> 296.1 / 296.5 ms per layer; 4 / 12 / 16 / 20 / 32 / 48: 297.8 / 296.3 /
+    // 298.2 / 299.9 / 314 / 358); smaller ones keep full descents (nanobox 145.8 -> 148.9 ms at 8, cornell_box
+    // within noise)
+    A.desc_quorum = c->desc_quorum >= 0 ? (uint32_t)c->desc_quorum : (c->n_tris >= LEAF_CULL_MIN_TRIS ? 8u : 0u);
     // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783);
     // re-swept under leaf-keyed queues (scripts/gpu_leaf_sweep.sh, 1080p x 128 spp, closest /
     // shadow): 56/48 397.4, 48/56 394.5, 48/48 395.9, 56/56 396.2 ms per pass; a rank of 8:
@@ -1187,7 +1191,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "diag_kinds") && v >= 0 && v <= 7) c->diag_kinds = (uint32_t)v;
     else if (!std::strcmp(key, "lc_debug") && v >= 0 && v <= 2) c->lc_debug = (int)v;
     else if (!std::strcmp(key, "lc_min") && v >= 0 && v <= 33) c->lc_min = (uint32_t)v;
-    else if (!std::strcmp(key, "desc_quorum") && v >= 0 && v <= 64) c->desc_quorum = (uint32_t)v;
+    else if (!std::strcmp(key, "desc_quorum") && v >= -1 && v <= 64) c->desc_quorum = (int)v;
     else if (!std::strcmp(key, "comm_timeout_ms") && v >= 1 && v <= 3600000) c->comm_timeout_ms = (uint32_t)v;
     else if (!std::strcmp(key, "variant") && v >= -1 && v < nvar) c->variant = (int)v; // -1 default; clamped per kernel
     else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;

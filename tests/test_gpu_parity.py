@@ -24,7 +24,7 @@ TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
-QUORUM_DEFAULT = 0  # ctx.hpp desc_quorum
+QUORUM_DEFAULT = -1  # ctx.hpp desc_quorum (8 on scenes of >= 65536 triangles, else 0)
 
 
 @pytest.fixture(scope="module")
@@ -194,7 +194,7 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, r
             pair.dev.set_option("wf_paths", 256 << 20)
 
 
-@pytest.mark.parametrize("quorum", [1, 16, 32, 64])
+@pytest.mark.parametrize("quorum", [0, 1, 8, 16, 32, 64])
 def test_wavefront_desc_quorum_bitexact(ca, sponza, nanobox, quorum):
     """desc_quorum q: a wave's descent round stops at a node fetch once at most q / 64 of its lanes still
     descend; those lanes keep their node and interval and descend on next round (64: after every fetch).
