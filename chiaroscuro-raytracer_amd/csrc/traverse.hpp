@@ -322,6 +322,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     // and their interval and go on next round -- the same node visits with the same intervals, so the
     // same answers -- while the others test their leaves now instead of idling
     const uint32_t nbusy = quorum ? (uint32_t)__popcll(__ballot(1)) : 0u;
+    constexpr uint32_t PENDING_LEAF = 0xfffffffeu;
     bool pending = false;
     if (pf) pt0 = prof_now();
     if (pc && wave_leader()) pc->waves++;
@@ -460,12 +461,14 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             nd = k ? make_uint2(f1.x, f1.y) : make_uint2(f0.z, f0.w);
             if ((nd.y & 3u) == 3u) break;
             step(nd);
-            if (!FULL && !CULL && quorum && (uint32_t)__popcll(__ballot(1)) * 64u <= nbusy * quorum) {
-                pending = true;
-                break;
-            }
-            fetch(T.node);
+            // (the quorum leaves through the loop's own exit -- a second exit would double the exec-mask
+            // bookkeeping of this divergent loop on the scalar unit)
+            if (!FULL && !CULL && quorum && (uint32_t)__popcll(__ballot(1)) * 64u <= nbusy * quorum)
+                nd = make_uint2(PENDING_LEAF, 3u); // (an empty "leaf" no real leaf shares `first` with)
+            else
+                fetch(T.node);
         }
+        pending = !FULL && !CULL && quorum && nd.x == PENDING_LEAF;
     } else {
         pc_load(pc, SC && wave_uniform(T.node), 8);
         nd = load_node<SC>(S, T.node);
