@@ -117,11 +117,12 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.diag_kinds = c->diag_kinds;
     A.lc_debug = c->lc_debug;
     A.lc_min = c->lc_min;
-    // descent rounds end once at most 8 / 64 of a wave's lanes still descend, on scenes that take the leaf-cull
-    // build (sponza: 299.9 / 300.6 -> 296.1 / 296.5 ms per layer; 4 / 12 / 16 / 20 / 32 / 48: 297.8 / 296.3 /
-    // 298.2 / 299.9 / 314 / 358); smaller ones keep full descents (nanobox 145.8 -> 148.9 ms at 8, cornell_box
-    // within noise)
-    A.desc_quorum = c->desc_quorum >= 0 ? (uint32_t)c->desc_quorum : (c->n_tris >= LEAF_CULL_MIN_TRIS ? 8u : 0u);
+    // descent rounds end once at most 8 / 64 of a wave's lanes still descend (sponza: 299.9 / 300.6 -> 296.1 /
+    // 296.5 ms per layer, 293 with the loop-exit form; 4 / 6 / 12 / 16 / 20 / 32 / 48 slower; cornell_box 97.6 ->
+    // 95.8 ms), except on scenes that sort their queues without the leaf-cull build, where full descents
+    // measured faster (nanobox stand-in 142.7 -> 146.1 ms at 8)
+    A.desc_quorum = c->desc_quorum >= 0 ? (uint32_t)c->desc_quorum
+                    : ((c->n_tris >= SORT_MIN_TRIS && c->n_tris < LEAF_CULL_MIN_TRIS) ? 0u : 8u);
     // wavefront: closest 56 / shadow 48 -> 811 Mray/s (48/48: 802, 64/48: 780, 40/48: 783);
     // re-swept under leaf-keyed queues (scripts/gpu_leaf_sweep.sh, 1080p x 128 spp, closest /
     // shadow): 56/48 397.4, 48/56 394.5, 48/48 395.9, 56/56 396.2 ms per pass; a rank of 8:

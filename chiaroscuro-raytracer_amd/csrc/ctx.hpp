@@ -63,7 +63,7 @@ struct cr_ctx {
     int full_counters = 1;
     int lc_debug = 0;                      // measurement only (RenderArgs::lc_debug)
     uint32_t lc_min = 0;                   // RenderArgs::lc_min
-    int desc_quorum = -1;                  // RenderArgs::desc_quorum; -1: 8 for scenes of LEAF_CULL_MIN_TRIS, else 0 (off)
+    int desc_quorum = -1;                  // RenderArgs::desc_quorum; -1: 8, 0 (off) for SORT_MIN_TRIS <= tris < LEAF_CULL_MIN_TRIS
     uint32_t diag_kinds = 0;               // counting renders: trace kinds of the DIAG_* census (1 << TK_*)
     unsigned long long last_diag[cr::DIAG_N] = {};
     int perf_counters = 0;                 // RenderArgs::perf_counters (option "perf_counters")

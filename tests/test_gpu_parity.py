@@ -24,7 +24,7 @@ TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
-QUORUM_DEFAULT = -1  # ctx.hpp desc_quorum (8 on scenes of >= 65536 triangles, else 0)
+QUORUM_DEFAULT = -1  # ctx.hpp desc_quorum (8, but 0 for 1024 <= triangles < 65536)
 
 
 @pytest.fixture(scope="module")
