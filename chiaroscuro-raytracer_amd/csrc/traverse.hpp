@@ -456,17 +456,19 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             }
         };
         fetch(T.node);
+        // one exit: a lane whose level-1 node is a leaf skips the second step and leaves at the loop test
+        // (a second exit would double the exec-mask bookkeeping of this divergent loop on the scalar
+        // unit); the quorum leaves the same way
         while ((nd.y & 3u) != 3u) {
             const uint32_t k = step(nd);
             nd = k ? make_uint2(f1.x, f1.y) : make_uint2(f0.z, f0.w);
-            if ((nd.y & 3u) == 3u) break;
-            step(nd);
-            // (the quorum leaves through the loop's own exit -- a second exit would double the exec-mask
-            // bookkeeping of this divergent loop on the scalar unit)
-            if (!FULL && !CULL && quorum && (uint32_t)__popcll(__ballot(1)) * 64u <= nbusy * quorum)
-                nd = make_uint2(PENDING_LEAF, 3u); // (an empty "leaf" no real leaf shares `first` with)
-            else
-                fetch(T.node);
+            if ((nd.y & 3u) != 3u) {
+                step(nd);
+                if (!FULL && !CULL && quorum && (uint32_t)__popcll(__ballot(1)) * 64u <= nbusy * quorum)
+                    nd = make_uint2(PENDING_LEAF, 3u); // (an empty "leaf" no real leaf shares `first` with)
+                else
+                    fetch(T.node);
+            }
         }
         pending = !FULL && !CULL && quorum && nd.x == PENDING_LEAF;
     } else {
