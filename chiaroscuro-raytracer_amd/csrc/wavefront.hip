@@ -855,7 +855,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
             const uint32_t r = trav_round<R, FULL, 1, false, true, true, LC != 0, 0, false, 0, 0, LC>(A.lc_debug, A.lc_min, S, ring_lds, W.gstack, W.gstride, gid, o, d,
                                                                         shadow, exclude, T, c, nullptr, 0.f, 0.f,
                                                                         nullptr, nullptr, nullptr, nullptr,
-                                                                        PC ? &pc : nullptr);
+                                                                        PC ? &pc : nullptr, FULL ? 0u : A.desc_quorum);
             if (r != (shadow ? ST_SHADOW : ST_CLOSEST)) state = r;
         }
     }
