@@ -128,7 +128,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // shadow): 56/48 397.4, 48/56 394.5, 48/48 395.9, 56/56 396.2 ms per pass; a rank of 8:
     // 59.96 vs 59.64 ms -> closest 48 / shadow 56
     A.refill = c->refill ? c->refill : (c->kernel == 2 ? 48u : 16u);
-    A.refill_shadow = c->refill_shadow ? c->refill_shadow : (c->refill ? c->refill : 56u);
+    // round 4: 60 on scenes whose queues are sorted (sponza 290.8 / 290.7 -> 289.8 / 290.1 ms per layer, nanobox
+    // 143.4 / 143.3 -> 141.8 / 141.6), 56 on the unsorted small ones (cornell_box 95.7 -> 97.7 ms at 60)
+    A.refill_shadow = c->refill_shadow ? c->refill_shadow
+                                       : (c->refill ? c->refill : (c->n_tris >= SORT_MIN_TRIS ? 60u : 56u));
     // camera rays (64 samples of one pixel per wave): lock-step is best, 64 -> 933 vs 56 -> 924 Mray/s
     A.refill_camera = c->refill_camera ? c->refill_camera : (c->refill ? c->refill : (c->kernel == 2 ? 64u : 16u));
     // wavefront trace builds (wavefront.hip kWf): 2 = LDS ring 8, 8 waves/SIMD, scalar loads for
