@@ -106,7 +106,7 @@ def cpu_baseline(osc, cam, xres, yres, spp, k, seed, budget_s):
 
     def leg(nthreads):
         t0 = time.time()
-        _, c = osc.render(cam, xres, yres, s_spp, k, seed, y0=0, y1=yres, ystep=ystep, threads=nthreads)
+        _, c = osc.render(cam, xres, yres, s_spp, k, seed, y0=0, y1=yres, ystep=ystep, threads=nthreads, lean=True)
         return c["closest"] + c["shadow"], time.time() - t0
 
     rays, dt1 = leg(1)
@@ -116,12 +116,15 @@ def cpu_baseline(osc, cam, xres, yres, spp, k, seed, budget_s):
     phys = physical_cores()
     sample = "%d of %d rows (every %d-th) x %d px x %d spp, %d rays" % (nr, yres, ystep, xres, s_spp, rays)
     return {"value": round(v_all, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "build": "oracle/liboracle_lean.so: oracle.c at the reference's -O3 (Makefile:5), -ffp-contract=off, "
+                     "the checker's work counters compiled out of the traversal (OR_LEAN); the same bits as the "
+                     "counting liboracle.so that checks the parity rows",
             "value_1t": round(v_1t, 4), "threads_all": threads, "physical_cores": phys,
             "parallel_efficiency": round(v_all / (v_1t * threads), 3) if v_1t > 0 else None,
             # linear in cores from the 1-thread rate: an upper bound for the whole host (the pool
             # gives one GPU's job a 16-thread CPU share, so the other cores are not timed)
             "projected_all_physical": round(v_1t * phys, 2) if phys else None,
-            "sample": "oracle/liboracle.so (OpenMP over rows, static schedule as src/rayTracer.cpp:55) on the "
+            "sample": "oracle/liboracle_lean.so (OpenMP over rows, static schedule as src/rayTracer.cpp:55) on the "
                       "same frame / seed, the same sample for both legs: %s; %d threads %.2f s (median of 3), "
                       "1 thread %.1f s" % (sample, threads, dtn, dt1)}
 
@@ -445,8 +448,10 @@ def run_rank(args, world, backend):
     # render pass (main.cpp:16, the preview's R key) -- a warmup pass, then --single-layer-steps passes
     # of the next layers (the frame's rows above are already taken), each bracketed like the steps
     single_ms = None
+    single_rays = 0.0
     if args.single_layer_steps > 0:
         times = []
+        srays = []
         for j in range(args.single_layer_steps + 1):
             p = ca.render_params(xres, yres, spp, k, seed, layer=layer + j, rank=rank, nranks=world, tile=tile)
             if dist:
@@ -459,10 +464,13 @@ def run_rank(args, world, backend):
                 dist.barrier()
             if j:
                 times.append((time.perf_counter() - ts) * 1e3)
+                c = fr.last_stats()["counters"]
+                srays.append(c.get("closest", 0) + c.get("shadow", 0))
         single_ms = sum(times) / len(times)
+        single_rays = sum(srays) / len(srays)
     # per rank: wall time, device time of its render passes (HIP events), rays
     mine = torch.tensor([elapsed, totals["kernel_ms"] / max(totals["launches"], 1), totals["rays"],
-                         totals["nee_answered"]], dtype=torch.float64, device=backend.device)
+                         totals["nee_answered"], single_rays], dtype=torch.float64, device=backend.device)
     if dist:
         per_rank = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(per_rank, mine)
@@ -472,6 +480,7 @@ def run_rank(args, world, backend):
     elapsed = max(r[0] for r in per_rank)   # the step ends with the slowest rank
     rays_all = float(sum(r[2] for r in per_rank))
     nee_all = float(sum(r[3] for r in per_rank))
+    single_rays_all = float(sum(r[4] for r in per_rank))  # one layer's rays over every rank's tiles
     rank_render_ms = [round(r[1], 3) for r in per_rank]
 
     # counting pass (untimed): algorithmic bytes of one launch of this rank
@@ -504,6 +513,9 @@ def run_rank(args, world, backend):
     out = None
     if rank == 0:
         value = rays_all / elapsed / 1e6
+        # the queries actually traversed: value less the zero-contribution NEE queries answered without
+        # a trace (rayTracer.cpp:104 issues every one; SURVEY §8d counts them, the line says how many)
+        value_traced = (rays_all - nee_all) / elapsed / 1e6
         kms = totals["kernel_ms"] / max(totals["launches"], 1)
         pass_bytes = totals["bytes"]  # counting pass: one render pass, same size as a timed one
         pass_gbs = pass_bytes / (kms / 1e3) / 1e9 if kms > 0 else 0.0
@@ -638,6 +650,10 @@ def run_rank(args, world, backend):
             # the same layer as ONE render pass (the reference's unit of work: one rayTrace call), wall
             # time per pass after the timed region; value and ms_per_step time the pass groups
             "single_layer_ms": round(single_ms, 3) if single_ms is not None else None,
+            # one layer's rays / single_layer_ms: the rate of one rayTrace call (main.cpp:16)
+            "single_layer_mray_s": round(single_rays_all / (single_ms / 1e3) / 1e6, 3) if single_ms else None,
+            # (rays - rays_answered_untraced) / the same wall time: the traversed queries' rate
+            "value_traced": round(value_traced, 3),
             "higher_is_better": True,
             "scaling": "strong",  # one fixed frame, tile-split over the ranks
             "vs_baseline": None,
@@ -654,6 +670,13 @@ def run_rank(args, world, backend):
                        "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            # value over the CPU baseline: the timed 16-thread share of the box, and the whole host's
+            # physical cores projected linearly from the 1-thread leg (an upper bound for the CPU)
+            "vs_cpu": {"share": round(value / cpu["value"], 1) if cpu and cpu.get("value") else None,
+                       "all_physical_projected": round(value / cpu["projected_all_physical"], 1)
+                       if cpu and cpu.get("projected_all_physical") else None,
+                       "traced_share": round(value_traced / cpu["value"], 1) if cpu and cpu.get("value") else None}
+            if cpu else None,
             "parity": parity,
         }
         if backend.name != "gpu":

@@ -169,7 +169,7 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
 }
 
 // path slots one wavefront chunk may hold: ~45% of the HBM that was free (plus the chunk buffers then
-// held) when the ctx first asked.  Queried once and kept: the plan of a pass group (cr_layers_per_group,
+// held) when the ctx first asked after its scene upload.  Kept until the next upload: the plan of a pass group (cr_layers_per_group,
 // cr_layers_per_pass) must not change as this ctx's own buffers grow, or ranks that asked at different
 // moments would plan different groups and their per-layer gathers would not pair up
 uint64_t wf_path_cap(cr_ctx *c, int k) {
@@ -547,6 +547,11 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     if (d->max_depth > 256) return fail(c, CR_E_DEPTH, "kd tree deeper than 256");
     HIPCHK(hipSetDevice(c->device));
     free_scene(c);
+    // a new scene re-queries the path budget at its first plan (wf_path_cap): buffers grown since the last
+    // query (gather and tile buffers, the caller's own tensors) must not leave the chunk cap above the HBM
+    // that is free now.  Ranks still agree on a group's plan: plan_layers' all-reduce MIN, and the per-group
+    // agreement of cr_render_dist_layers_device / cr_group_render_layers
+    c->wf_mem_budget = 0;
     const uint32_t nt = d->n_tris;
     // nodes -> {split bits | first, axis | child<<2}, validated first
     const uint32_t NN = d->n_nodes;

@@ -147,6 +147,8 @@ struct cr_ctx {
     uint32_t comm_timeout_ms = 120000; // cr_comm_init: peers must join within this (option "comm_timeout_ms")
     float *d_tiles = nullptr, *d_gathered = nullptr;
     size_t tiles_bytes = 0, gathered_bytes = 0;
+    int *d_flag = nullptr; // one word: the ranks' agreement on a pass group before its gather
+    size_t flag_bytes = 0;
 };
 
 

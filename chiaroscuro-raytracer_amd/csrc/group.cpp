@@ -41,8 +41,10 @@ void release_dist(cr_ctx *c) {
     c->comm_nranks = 1;
     if (c->d_tiles) hipFree(c->d_tiles);
     if (c->d_gathered) hipFree(c->d_gathered);
+    if (c->d_flag) hipFree(c->d_flag);
     c->d_tiles = c->d_gathered = nullptr;
-    c->tiles_bytes = c->gathered_bytes = 0;
+    c->d_flag = nullptr;
+    c->tiles_bytes = c->gathered_bytes = c->flag_bytes = 0;
 }
 
 // A non-blocking communicator's state once its pending work is enqueued (or failed).
@@ -70,6 +72,26 @@ static int wait_comm(cr_ctx *c, ncclComm_t comm, hipStream_t st, const char *wha
     ncclResult_t ae = ncclSuccess;
     if (comm && ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess) return nccl_fail(c, ae, what);
     return CR_OK;
+}
+
+// Every rank's verdict on a pass group before anything of it is rendered or exchanged: an all-reduce MIN
+// of `ok` over the communicator.  A rank whose share cannot hold the group (a plan that differs between
+// the ranks, a buffer that cannot grow) then makes EVERY rank fail here with the same error, instead of
+// returning before the grouped send / receive and leaving its peers blocked in it until comm_timeout_ms.
+static int agree(cr_ctx *c, bool ok, hipStream_t st, const char *what) {
+    if (int r = grow(c, (void **)&c->d_flag, c->flag_bytes, sizeof(int))) return r;
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)c->d_flag, ok ? 1 : 0, 1, st));
+    ncclResult_t r = ncclAllReduce(c->d_flag, c->d_flag, 1, ncclInt32, ncclMin, c->comm, st);
+    if (r == ncclInProgress) r = nccl_settle(c->comm);
+    if (r != ncclSuccess) return nccl_fail(c, r, what);
+    if (int rc = wait_comm(c, c->comm, st, what)) return rc;
+    int all = 0;
+    HIPCHK(hipMemcpy(&all, c->d_flag, sizeof(int), hipMemcpyDeviceToHost));
+    if (all == 1) return CR_OK;
+    return fail(c, CR_E_INVALID, std::string(what) + ": " +
+                                     (ok ? "another rank cannot render this pass group (plan the group with "
+                                           "cr_layers_per_group on every rank and agree on the minimum)"
+                                         : c->err));
 }
 
 // Elements of one rank's compact tile buffer (the root's largest: rank 0 owns
@@ -246,14 +268,20 @@ int cr_render_dist_layers_device(cr_ctx *c, const cr_camera *cam, const cr_rende
     // every rank's nlayers compact buffers in one piece: [nlayers][slot], the root's in its slot 0 of
     // [nranks][nlayers][slot]; ONE grouped send / receive of the whole group, one blend of its layers
     const size_t slot = slot_elems(&q), span = slot * nlayers;
-    float *mine;
-    if (root) {
-        if (int r = grow(c, (void **)&c->d_gathered, c->gathered_bytes, span * q.nranks * sizeof(float))) return r;
-        mine = c->d_gathered;
-    } else {
-        if (int r = grow(c, (void **)&c->d_tiles, c->tiles_bytes, span * sizeof(float))) return r;
-        mine = c->d_tiles;
+    // this rank's checks first, then every rank's verdict (agree): the group is rendered and exchanged
+    // only when the plan holds on all of them
+    uint32_t m = 1;
+    bool ok = group_layers(c, &q, nlayers, &m) == nlayers;
+    if (!ok) fail(c, CR_E_INVALID, "layers per pass: the rank's share does not fit " + std::to_string(nlayers) +
+                                      " layers in pieces");
+    float *mine = nullptr;
+    if (ok) {
+        const int r = root ? grow(c, (void **)&c->d_gathered, c->gathered_bytes, span * q.nranks * sizeof(float))
+                           : grow(c, (void **)&c->d_tiles, c->tiles_bytes, span * sizeof(float));
+        ok = r == CR_OK;
+        mine = root ? c->d_gathered : c->d_tiles;
     }
+    if (int rc = agree(c, ok, st, "pass group plan")) return rc;
     if (int rc = cr_render_tiles_layers_device(c, cam, &q, nlayers, mine, st)) return rc;
     ncclResult_t r = ncclGroupStart();
     if (r == ncclSuccess) {

@@ -1520,7 +1520,7 @@ static uint32_t shade_grid(int num_cus, int waves) {
     }
     return (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)std::min(b, 8);
 }
-// wf_shade at the ctx's option "wf_shade_waves" (6 default, 8)
+// wf_shade at the ctx's option "wf_shade_waves" (8, the default since round 4; or 6)
 static void launch_shade(const RenderArgs &A, const WfArgs &W, uint32_t g, int num_cus, hipStream_t st) {
     if (W.shade_waves == 8)
         hipLaunchKernelGGL(wf_shade<8>, dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
@@ -1594,7 +1594,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if (err) break;
         // overlapped tail: the rest of the chunk starts beside this generation's shadow trace, tracing
         // its own paths' shadow rays of generation g first (the paths that end at g stay with
-        // wf_trace / wf_resolve); needs NEE rays, which every hit has when the scene has lights
+        // wf_trace / wf_resolve); only for scenes with lights -- a hit whose NEE query was answered
+        // without a trace (nee_skip) has no shadow ray, and the tail reads its NO_SLOT as "nothing to trace"
         const bool overlap = !next && nc > 0 && W.tail_overlap && A.S.nlights > 0;
         if (next || overlap) {
             if ((err = (int)hipEventRecord(ss.fork, st)) || (err = (int)hipStreamWaitEvent(ss.side, ss.fork, 0))) break;

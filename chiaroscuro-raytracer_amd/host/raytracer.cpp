@@ -136,21 +136,28 @@ void RayTracer::rayTraceLayers(unsigned n, vec3 eye, vec3 center, vec3 up, float
     p.rank = 0;
     p.nranks = 1;
     p.tile = 32;
-    // a failed render leaves the device accumulator holding an unknown number of this call's layers
-    // (cr_render_layers blends group after group): the next rayTrace then starts over at layer 1,
-    // whose blend weight (L - 1 = 0) discards whatever the accumulator holds
+    // A failed render of several layers may leave the device accumulator holding an unknown number of this
+    // call's layers (cr_render_layers blends group after group), and so may a failure past the blend: the
+    // next rayTrace then starts over at layer 1, whose blend weight (L - 1 = 0) discards whatever the
+    // accumulator holds.  A one-layer call that fails with CR_E_INVALID (parameter checks) or CR_E_OOM (buffer
+    // growth) stopped before its only blend -- the pass's last kernel -- so the accumulator still holds
+    // layers 1 .. layers_ - 1 intact, and a retry continues at the same layer instead of discarding them.
+    auto rollback = [&](int rc) {
+        if (n == 1 && (rc == CR_E_INVALID || rc == CR_E_OOM)) layers_--;
+        else layers_ = 0;
+    };
     if (group_) {
-        if ((n == 1 ? cr_group_render(group_, &cam, &p, pixels.data())
-                    : cr_group_render_layers(group_, &cam, &p, n, pixels.data())) != CR_OK) {
-            layers_ = 0;
+        if (const int rc = n == 1 ? cr_group_render(group_, &cam, &p, pixels.data())
+                                  : cr_group_render_layers(group_, &cam, &p, n, pixels.data())) {
+            rollback(rc);
             throw std::runtime_error(std::string("chiaro: render failed: ") + cr_group_last_error(group_));
         }
         layers_ += n - 1; // layers p.layer .. p.layer + n - 1 are in the frame
         cr_group_get_counters(group_, &counters_);
     } else {
-        if ((n == 1 ? cr_render(ctx_, &cam, &p, pixels.data()) : cr_render_layers(ctx_, &cam, &p, n, pixels.data())) !=
-            CR_OK) {
-            layers_ = 0;
+        if (const int rc = n == 1 ? cr_render(ctx_, &cam, &p, pixels.data())
+                                  : cr_render_layers(ctx_, &cam, &p, n, pixels.data())) {
+            rollback(rc);
             throw std::runtime_error(std::string("chiaro: render failed: ") + cr_last_error(ctx_));
         }
         layers_ += n - 1; // layers p.layer .. p.layer + n - 1 are in the frame

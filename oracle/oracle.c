@@ -438,6 +438,15 @@ void or_camera(const float e[3], const float c[3], const float u_[3], float yvie
 
 /* ---------------------------------------------------------- traversal -- */
 typedef struct { uint64_t c[OR_C_COUNT]; } ctr_t;
+/* Work counters inside the hot recursion (inner nodes, leaves, triangle tests, hits, texture hits).
+ * OR_LEAN (liboracle_lean.so, the timed CPU baseline only): compiled out, so the baseline runs the
+ * reference's arithmetic without the checker's bookkeeping; the query and path counts stay (they
+ * are outside the recursion and give the baseline its ray count). */
+#ifdef OR_LEAN
+#define CT_HOT(ct, i) ((void)(ct))
+#else
+#define CT_HOT(ct, i) ((ct)->c[(i)]++)
+#endif
 
 /* kdtree.cpp:196-208 */
 static inline void ray_box(v3 o, v3 d, v3 mx, v3 mn, float *first, float *second) {
@@ -471,12 +480,12 @@ static int node_closest(const or_scene *s, v3 o, v3 d, uint32_t *tri, float *bx,
                         uint32_t ni, float tmin, float tmax, ctr_t *ct) {
     const node_t *nd = &s->nodes[ni];
     if (nd->is_leaf) {
-        ct->c[OR_C_LEAF]++;
+        CT_HOT(ct, OR_C_LEAF);
         int ret = 0;
         for (uint32_t j = 0; j < nd->count; j++) {
             uint32_t t = s->refs[nd->first + j];
             float px, py, pd;
-            ct->c[OR_C_TRITEST]++;
+            CT_HOT(ct, OR_C_TRITEST);
             if (tri_test(s, o, d, t, &px, &py, &pd) && pd < tmax) {
                 *bx = px; *by = py; tmax = pd; *tri = t; ret = 1;
             }
@@ -484,7 +493,7 @@ static int node_closest(const or_scene *s, v3 o, v3 d, uint32_t *tri, float *bx,
         *dist = tmax;
         return ret;
     }
-    ct->c[OR_C_INNER]++;
+    CT_HOT(ct, OR_C_INNER);
     const int a = (int)nd->axis;
     const float oa = comp(o, a), da = comp(d, a);
     const float tsplit = (nd->split - oa) / da;
@@ -531,17 +540,17 @@ static int node_shadow(const or_scene *s, v3 o, v3 d, uint32_t light, uint32_t n
                        ctr_t *ct) {
     const node_t *nd = &s->nodes[ni];
     if (nd->is_leaf) {
-        ct->c[OR_C_LEAF]++;
+        CT_HOT(ct, OR_C_LEAF);
         for (uint32_t j = 0; j < nd->count; j++) {
             uint32_t t = s->refs[nd->first + j];
             if (t != light) {
-                ct->c[OR_C_TRITEST]++;
+                CT_HOT(ct, OR_C_TRITEST);
                 if (shadow_tri(s, o, d, t, tmax)) return 1;
             }
         }
         return 0;
     }
-    ct->c[OR_C_INNER]++;
+    CT_HOT(ct, OR_C_INNER);
     const int a = (int)nd->axis;
     const float oa = comp(o, a), da = comp(d, a);
     const float tsplit = (nd->split - oa) / da;
@@ -653,7 +662,7 @@ static v3 send_ray(const itg_t *it, v3 origin, v3 dir, int k, rng_t *rng, ctr_t 
     const or_scene *s = it->s;
     uint32_t t; float bx, by, dist;
     if (!intersect_ray(s, origin, dir, &t, &bx, &by, &dist, ct)) return it->bg;
-    ct->c[OR_C_HIT]++;
+    CT_HOT(ct, OR_C_HIT);
     /* intersectRayKDTree */
     const v3 normal = s->nrm[t];
     const float bz = (1.f - bx - by);
@@ -664,7 +673,7 @@ static v3 send_ray(const itg_t *it, v3 origin, v3 dir, int k, rng_t *rng, ctr_t 
         c.x = (s->uvA[t].x * bz + s->uvB[t].x * bx) + s->uvC[t].x * by;
         c.y = (s->uvA[t].y * bz + s->uvB[t].y * bx) + s->uvC[t].y * by;
         Kd = tex_lookup(s, s->tex[t], c);
-        ct->c[OR_C_TEXHIT]++;
+        CT_HOT(ct, OR_C_TEXHIT);
     }
     const int emissive = s->is_light[t];
     const v3 fcol = muls(Kd, (float)M_1_PI); /* Diffuse::f = float(M_1_PI) * color, brdf.cpp:70 */

@@ -14,6 +14,9 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "liboracle.so"
+# the same oracle.c at -O3 without the hot-path work counters (OR_LEAN): bench.py's timed
+# cpu_baseline leg only; its query / path counts equal liboracle.so's and its pixels are the same bits
+LEAN_LIB = HERE / "liboracle_lean.so"
 REF_LIB = HERE / "_ref" / "libref_harness.so"
 
 FP = C.POINTER(C.c_float)
@@ -24,6 +27,7 @@ N_COUNTERS = 8
 COUNTER_NAMES = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit", "paths")
 
 _lib = None
+_lean = None
 
 
 def build() -> None:
@@ -76,6 +80,20 @@ def lib():
             fn.restype, fn.argtypes = res, args
         _lib = L
     return _lib
+
+
+def lean_lib():
+    """liboracle_lean.so's or_render (scenes are shared with liboracle.so: same source, same layout)."""
+    global _lean
+    if _lean is None:
+        if not LEAN_LIB.exists():
+            build()
+        L = C.CDLL(str(LEAN_LIB))
+        L.or_render.restype = None
+        L.or_render.argtypes = [P, FP, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, FP, C.c_uint32, C.c_uint32,
+                                C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, FP, C.POINTER(C.c_uint64)]
+        _lean = L
+    return _lean
 
 
 def _f(a):
@@ -160,10 +178,11 @@ class OracleScene:
         return out
 
     def render(self, cam, xres, yres, spp, k, seed, layer=1, bg=(0, 0, 0), pixels=None, y0=0, y1=None, ystep=1,
-               threads=0):
+               threads=0, lean=False):
+        """lean: the -O3 counter-free build (liboracle_lean.so): only closest / shadow / paths are counted."""
         pix = pixels if pixels is not None else np.zeros((yres, xres, 3), np.float32)
         ctr = np.zeros(N_COUNTERS, np.uint64)
-        lib().or_render(self.h, _p(_f(cam)), xres, yres, spp, k, _p(_f(bg)), seed & 0xFFFFFFFF, layer, y0,
+        (lean_lib() if lean else lib()).or_render(self.h, _p(_f(cam)), xres, yres, spp, k, _p(_f(bg)), seed & 0xFFFFFFFF, layer, y0,
                         yres if y1 is None else y1, ystep, threads, _p(pix), ctr.ctypes.data_as(C.POINTER(C.c_uint64)))
         return pix, dict(zip(COUNTER_NAMES, (int(x) for x in ctr)))
 

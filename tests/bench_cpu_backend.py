@@ -11,6 +11,7 @@ last_kernel_ms, trace_stats).  The product never imports this file.
 from __future__ import annotations
 
 import ctypes
+import os
 import sys
 import time
 from pathlib import Path
@@ -54,8 +55,10 @@ class OracleDevice:
         self.last["pixels"] = len(px)
         return mean
 
-    def render_tiles_device(self, cam, p, ptr, stream=0):
+    def render_tiles_device(self, cam, p, ptr, stream=0, _in_group=False):
         from chiaroscuro_amd.tiles import TileLayout
+        if not _in_group:
+            self._log_pass(p, 1)
         lay = TileLayout(p.xres, p.yres, p.nranks, p.tile)
         T = lay.tile
         buf = _view(ptr, (lay.max_tiles, T, T, 3))
@@ -99,6 +102,21 @@ class OracleDevice:
     def layers_per_pass(self, p, want):
         return want
 
+    def layers_per_group(self, p, want):
+        """cr_layers_per_group's stand-in: what this rank's share holds.  CHIARO_TEST_ODD_RANK_CAP=c caps
+        the odd ranks at c layers, so the ranks plan differently and DistributedFrame.plan_layers' all-reduce
+        MIN has to make them agree (tests/test_bench_distributed.py)."""
+        cap = int(os.environ.get("CHIARO_TEST_ODD_RANK_CAP", "0") or 0)
+        return min(want, cap) if cap and p.rank % 2 == 1 else want
+
+    def _log_pass(self, p, n):
+        """CHIARO_TEST_PLAN_LOG=dir: every rank appends the (first layer, layers) of each pass it renders to
+        dir/rank<r>.txt, so a test can check that all ranks rendered the same groups."""
+        d = os.environ.get("CHIARO_TEST_PLAN_LOG")
+        if d:
+            with open(os.path.join(d, "rank%d.txt" % p.rank), "a") as f:
+                f.write("%d %d\n" % (p.layer, n))
+
     def _layers(self, p, n, one):
         from chiaroscuro_amd.tiles import _with_layer
         tot, ms = {}, 0.0
@@ -111,9 +129,10 @@ class OracleDevice:
 
     def render_tiles_layers_device(self, cam, p, n, ptr, stream=0):
         from chiaroscuro_amd.tiles import TileLayout
+        self._log_pass(p, n)
         lay = TileLayout(p.xres, p.yres, p.nranks, p.tile)
         stride = lay.max_tiles * lay.tile * lay.tile * 3 * 4
-        self._layers(p, n, lambda j, q: self.render_tiles_device(cam, q, ptr + j * stride, stream))
+        self._layers(p, n, lambda j, q: self.render_tiles_device(cam, q, ptr + j * stride, stream, True))
 
     def render_layers_device(self, cam, p, n, frame_ptr, stream=0):
         self._layers(p, n, lambda j, q: self.render_device(cam, q, frame_ptr, stream))

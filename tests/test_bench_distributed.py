@@ -18,6 +18,7 @@ import sys
 from pathlib import Path
 
 import numpy as np
+import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 RES, SPP, WARMUP, STEPS = (40, 24), 2, 1, 3
@@ -64,6 +65,60 @@ def test_bench_two_ranks_gloo(tmp_path, ca, po, scenes):
     # value: the rays of all ranks over the slowest rank's wall time (ms_per_step is that / steps)
     want = rays / (line["ms_per_step"] * STEPS / 1e3) / 1e6
     assert abs(line["value"] - want) <= 1e-3 * want + 2e-3
+
+
+@pytest.mark.parametrize("nranks", [4, 8])
+def test_bench_ranks_gloo_ragged_uneven_plans(tmp_path, nranks, ca, po, scenes):
+    """The 8-rank protocol before an 8-GPU node runs it: bench.py --gpus 4 / 8 over gloo on a ragged
+    200 x 150 frame (7 x 5 tiles of 32, partial on both edges: ranks hold 9 / 8 or 5 / 4 tiles), pass groups
+    of up to 4 layers that the odd ranks' stand-in devices cap at 3 (CHIARO_TEST_ODD_RANK_CAP), so
+    DistributedFrame.plan_layers' all-reduce MIN must bring every rank to the same groups of 3: each rank
+    logs the (first layer, layers) of every pass it renders, and the logs must be identical; the frame rank 0
+    blends from the gathered [nranks][3][tiles] buffers must equal the oracle's progressive render bit for
+    bit, with one render time per rank in the line (src/rayTracer.cpp:55,64)."""
+    res, spp, warmup, steps = (200, 150), 1, 1, 7
+    frame, logs = tmp_path / "frame.npy", tmp_path / "plans"
+    logs.mkdir()
+    env = dict(os.environ, CHIARO_BENCH_BACKEND="%s:make" % (ROOT / "tests" / "bench_cpu_backend.py"),
+               MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", CHIARO_QUIET="1", CHIARO_TEST_ODD_RANK_CAP="3",
+               CHIARO_TEST_PLAN_LOG=str(logs))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(nranks), "--steps", str(steps), "--warmup",
+           str(warmup), "--config", "cornell", "--res", "%dx%d" % res, "--spp", str(spp), "--no-cpu-baseline",
+           "--layers-per-pass", "4", "--parity-rows", "4", "--save-frame", str(frame)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == nranks and line["config"]["parallelism"] == "tile-split x%d" % nranks
+    assert len(line["config"]["rank_render_ms"]) == nranks and all(v > 0 for v in line["config"]["rank_render_ms"])
+    # the agreed plan: groups of min(4, 3) layers, the 7 timed steps as 3 + 3 + 1
+    assert line["config"]["layers_per_pass"] == 3 and line["config"]["pass_groups"] == [[3, 1], [3, 1], [1, 1]]
+    plans = {p.name: p.read_text().split("\n") for p in logs.iterdir()}
+    assert sorted(plans) == sorted("rank%d.txt" % r for r in range(nranks))
+    want = ["1 1", "2 3", "5 3", "8 1"]  # warmup layer, the timed groups (then single layers, counting pass)
+    for name, got in plans.items():
+        assert got[:4] == want, (name, got)
+        assert got == plans["rank0.txt"], (name, got)
+    # the ranks' tile shares really are uneven (ragged frame)
+    from chiaroscuro_amd.tiles import TileLayout
+    lay = TileLayout(res[0], res[1], nranks, 32)
+    assert len({lay.tiles_for_rank(q) for q in range(nranks)}) == 2
+    sc = ca.Scene(scenes.config_rtc("cornell"), "xres", str(res[0]), "yres", str(res[1]))
+    i = sc.info
+    m = ca.Model(sc)
+    osc = po.OracleScene(m.triangles(), leaf_size=i["leaf_size"], textures=m.textures())
+    cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], res[0], res[1]).as_array()
+    ref, rays = None, 0
+    for L in range(1, warmup + steps + 1):
+        ref, c = osc.render(cam, res[0], res[1], spp, i["k"], i["seed"], layer=L, bg=i["background"], pixels=ref)
+        if L > warmup:
+            rays += c["closest"] + c["shadow"]
+    assert line["config"]["rays"] == rays
+    got = np.load(frame)
+    assert got.shape == ref.shape and (got.view(np.uint32) == ref.view(np.uint32)).all() and got.mean() > 0
+    assert line["parity"]["differing"] == 0 and line["parity"]["layers"] == warmup + steps
+    assert line["single_layer_mray_s"] > 0 and line["value_traced"] <= line["value"] + 1e-9
 
 
 def test_frame_parity_detects_one_flipped_bit(ca, po, scenes):

@@ -125,3 +125,21 @@ def test_preview_camera_matches_reference(ca):
         assert np.array_equal(got.view(np.uint32), want), np.argwhere(got.view(np.uint32) != want)[:5]
         n += len(s["ops"])
     assert n == 480
+
+
+def test_lean_oracle_is_the_same_render(po, ca):
+    """bench.py's timed cpu_baseline leg runs liboracle_lean.so (oracle.c at -O3, the hot recursion's work
+    counters compiled out): its pixels are the counting liboracle.so's bit for bit, and its query and path
+    counts -- the baseline's ray count -- are the same; the hot counters read 0."""
+    from chiaroscuro_amd import scenes
+    sc = ca.Scene(scenes.config_rtc("cornell"), "xres", "48", "yres", "40")
+    i = sc.info
+    m = ca.Model(sc)
+    osc = po.OracleScene(m.triangles(), leaf_size=i["leaf_size"], textures=m.textures())
+    cam = ca.camera(i["VP"], i["LA"], i["UP"], i["yview"], 48, 40).as_array()
+    a, ca_ = osc.render(cam, 48, 40, 3, i["k"], i["seed"], layer=2, ystep=3, threads=2)
+    b, cb = osc.render(cam, 48, 40, 3, i["k"], i["seed"], layer=2, ystep=3, threads=2, lean=True)
+    assert (a.view(np.uint32) == b.view(np.uint32)).all() and a.mean() > 0
+    for key in ("closest", "shadow", "paths"):
+        assert ca_[key] == cb[key] > 0
+    assert ca_["tritest"] > 0 and cb["tritest"] == cb["inner"] == cb["leaf"] == 0
