@@ -184,6 +184,12 @@ __device__ __forceinline__ void path_advance(const RenderArgs &A, Lane &L, uint3
     } while (state != ST_CLOSEST && state != ST_SHADOW && state != ST_DONE);
 }
 
+// the megakernel's traversal configuration (traverse.hpp TraceDefaults)
+template <int R_, bool FULL_, bool PF_, bool FD_> struct MegaCfg : TraceDefaults {
+    static constexpr int R = R_, PF = PF_ ? 1 : 0;
+    static constexpr bool FULL = FULL_, FD = FD_;
+};
+
 template <int R, bool FULL, bool PF, int MINW, bool FD>
 __global__ void __launch_bounds__(256, MINW) render_dynamic(RenderArgs A) {
     extern __shared__ uint2 ring_lds[];
@@ -228,7 +234,7 @@ __global__ void __launch_bounds__(256, MINW) render_dynamic(RenderArgs A) {
             continue;
         }
         if (go)
-            state = trav_round<R, FULL, PF, FD>(A.lc_debug, A.lc_min, S, ring_lds, A.gstack, gstride, gid, o, d, state == ST_SHADOW,
+            state = trav_round<MegaCfg<R, FULL, PF, FD>>(A.lc_debug, A.lc_min, S, ring_lds, A.gstack, gstride, gid, o, d, state == ST_SHADOW,
                                                 exclude, T, c);
     }
     flush_counters(A.counters, c, 0u);

@@ -308,14 +308,38 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 // lane reads its box (16 B) and, inside, the record (48 B).
 // LC (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a leaf's tests run only
 // for the references its cull record (leafcull.hpp) cannot exclude for this ray and segment.
-template <int R, bool FULL, int PF, bool FD, bool SC = false, bool FAT = false, bool BF = false, int TILE = 0,
-          bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0>
+// A trace build's configuration: every knob of trav_round and wf_trace (wavefront.hip), named.  The
+// defaults are the plain reference build; a build is a type deriving from this and restating what it
+// changes (wavefront.hip namespace tc), so a kernel reads e.g. wf_trace<cr::tc::ShadowLcFd>.
+struct TraceDefaults {
+    static constexpr bool SHADOW = false; // shadow (any-hit) queries, else closest-hit
+    static constexpr bool FULL = false;   // counting build: SURVEY §8d work counters and diagnostics
+    static constexpr int R = 8;           // LDS ring entries of the traversal stack per lane
+    static constexpr int MINW = 8;        // waves per SIMD the launch bounds ask for
+    static constexpr bool SC = false;     // scalar loads of wave-uniform nodes and leaves
+    static constexpr bool FD = false;     // exact short split division by the ray's RN(1/d)
+    static constexpr bool FAT = false;    // fat node records (a node and its children per load)
+    static constexpr int PF = 1;          // leaf loop: 1 one record ahead, 2 unrolled by two, 0 none
+    static constexpr bool CAM = false;    // the generation-1 closest (camera-ray) instantiation
+    static constexpr bool BF = false;     // branch-light steps and uniform-leaf tests by select
+    static constexpr int TILE = 0;        // fat records of the first TILE nodes in LDS
+    static constexpr bool UL2 = false;    // a uniform leaf's records two per scalar-load wait
+    static constexpr int CULL = 0;        // camera cull boxes: 1 references and leaves, 2 also subtrees
+    static constexpr int PLANE = 0;       // plane records of secondary / shadow rays
+    static constexpr int LC = 0;          // leaf cull records (1 per-ray, 2 passing culled leaves, 3 fixed, 4 packed)
+    static constexpr bool PROF = false;   // phase clock (measurement only)
+    static constexpr bool PC = false;     // performed-work counters (measurement only)
+};
+
+template <class C>
 __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
                                                float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
                                                Prof *pf = nullptr, Pc *pc = nullptr, uint32_t quorum = 0) {
+    static constexpr int R = C::R, PF = C::PF, TILE = C::TILE, CULL = C::CULL, PLANE = C::PLANE, LC = C::LC;
+    static constexpr bool FULL = C::FULL, FD = C::FD, SC = C::SC, FAT = C::FAT, BF = C::BF, UL2 = C::UL2;
     uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
     // quorum (lean FAT builds without the camera cull): the wave's descent stops at a fetch once at most
     // quorum / 64 of the lanes that entered the round still descend; those keep T.node (the node to fetch)

@@ -272,10 +272,11 @@ __device__ __forceinline__ bool nee_visible(const WfArgs &W, uint32_t slot) {
 // trace, so profiles and the bench roofline see it separately.
 // CULL (camera instantiation only): triangle tests skipped by the screen-space cull
 // boxes (camcull.hpp, A.cull); the lane keeps its sample's screen position.
-template <bool SHADOW, bool FULL, int R, int MINW, bool SC, bool FD = false, bool FAT = false, int PF = 1,
-          bool CAM = false, bool BF = false, int TILE = 0, bool UL2 = false, int CULL = 0, int PLANE = 0, int LC = 0,
-          bool PROF = false, bool PC = false>
-__global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
+// C: the build's configuration (traverse.hpp TraceDefaults; the builds: namespace tc below)
+template <class C>
+__global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
+    static constexpr bool SHADOW = C::SHADOW, FULL = C::FULL, CAM = C::CAM, PROF = C::PROF, PC = C::PC;
+    static constexpr int R = C::R, TILE = C::TILE, CULL = C::CULL;
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
@@ -379,7 +380,7 @@ __global__ void __launch_bounds__(256, MINW) wf_trace(RenderArgs A, WfArgs W, ui
             continue;
         }
         if (state == busy_st) {
-            const uint32_t r = trav_round<R, FULL, PF, FD, SC, FAT, BF, TILE, UL2, CULL, PLANE, LC>(A.lc_debug, A.lc_min,
+            const uint32_t r = trav_round<C>(A.lc_debug, A.lc_min,
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
                 A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr, A.desc_quorum);
             if (r != busy_st) {
@@ -733,6 +734,13 @@ __global__ void __launch_bounds__(256) wf_fold(RenderArgs A, WfArgs W, uint32_t 
 // which then takes only the paths that ended at gs; a lane first traces its path's generation-gs
 // shadow ray (slot in dw[2(gs-1)].w), resolves that bounce as wf_resolve does (same add), then
 // starts the path's closest query of g0.
+// the tail kernel's traversal configuration (traverse.hpp TraceDefaults): fat records, scalar loads, and
+// with leaf cull records the branch-light steps
+template <bool FULL_, int R_, int LC_> struct TailCfg : TraceDefaults {
+    static constexpr int R = R_, LC = LC_;
+    static constexpr bool FULL = FULL_, SC = true, FAT = true, BF = LC_ != 0;
+};
+
 template <bool FULL, int R, int MINW, int LC = 0, bool PC = false>
 __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uint32_t g0) {
     extern __shared__ uint2 ring_lds[];
@@ -852,7 +860,7 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
         }
         if (busy) {
             const bool shadow = state == ST_SHADOW;
-            const uint32_t r = trav_round<R, FULL, 1, false, true, true, LC != 0, 0, false, 0, 0, LC>(A.lc_debug, A.lc_min, S, ring_lds, W.gstack, W.gstride, gid, o, d,
+            const uint32_t r = trav_round<TailCfg<FULL, R, LC>>(A.lc_debug, A.lc_min, S, ring_lds, W.gstack, W.gstride, gid, o, d,
                                                                         shadow, exclude, T, c, nullptr, 0.f, 0.f,
                                                                         nullptr, nullptr, nullptr, nullptr,
                                                                         PC ? &pc : nullptr, FULL ? 0u : A.desc_quorum);
@@ -1232,120 +1240,148 @@ struct WfVariant {
     int packet; // the camera trace is a packet trace (needs a near child common to all camera rays)
     int lc;     // the tail kernel's leaf cull form (trav_round's LC; 0: none)
 };
+
+// The trace configurations of the builds (traverse.hpp TraceDefaults), by what they restate.
+namespace tc {
+// build 0: the plain reference build (4-deep ring, vector loads, one level per load)
+struct CameraRef : TraceDefaults { static constexpr int R = 4; static constexpr bool CAM = true; };
+struct ClosestRef : TraceDefaults { static constexpr int R = 4; };
+struct ShadowRef : TraceDefaults { static constexpr int R = 4; static constexpr bool SHADOW = true; };
+// fat records, scalar loads of wave-uniform nodes / leaves, branch-light steps (build 9's; 15, 18, 42, 44)
+struct Fat : TraceDefaults { static constexpr bool SC = true, FAT = true, BF = true; };
+struct ClosestFat : Fat {};
+struct ShadowFat : Fat { static constexpr bool SHADOW = true; };
+// build 15's camera trace: cull boxes of references, leaves and subtrees
+struct CameraCull : Fat { static constexpr bool CAM = true; static constexpr int CULL = 2; };
+// + packed fixed-pad leaf cull records (build 26's; 40, 43)
+struct ClosestFatLc : Fat { static constexpr int LC = 4; };
+struct ShadowFatLc : ClosestFatLc { static constexpr bool SHADOW = true; };
+// + the exact short split division by the ray's RN(1/d) in the shadow trace (43; 44 without the leaf cull)
+struct ShadowFatLcFd : ShadowFatLc { static constexpr bool FD = true; };
+struct ShadowFatFd : ShadowFat { static constexpr bool FD = true; };
+// the performed-work counting instances (RenderArgs::perf_counters; measurement only)
+struct ClosestFatLcPerf : ClosestFatLc { static constexpr bool PC = true; };
+struct ShadowFatLcPerf : ShadowFatLc { static constexpr bool PC = true; };
+struct ClosestFatPerf : ClosestFat { static constexpr bool PC = true; };
+struct ShadowFatPerf : ShadowFat { static constexpr bool PC = true; };
+// the counting build (SURVEY §8d work counters, diagnostics: RenderArgs::full_counters), 1 wave per SIMD
+struct Count : TraceDefaults { static constexpr bool FULL = true; static constexpr int MINW = 1; };
+struct CameraCount : Count { static constexpr bool CAM = true; };
+struct ClosestCount : Count {};
+struct ShadowCount : Count { static constexpr bool SHADOW = true; };
+#ifdef CR_ALL_VARIANTS
+// the measured and superseded builds, by their knobs in TraceDefaults order
+template <bool SHADOW_, int R_, int MINW_, bool SC_, bool FD_, bool FAT_, int PF_, bool CAM_, bool BF_, int TILE_,
+          bool UL2_, int CULL_, int PLANE_, int LC_, bool PROF_ = false>
+struct Cfg : TraceDefaults {
+    static constexpr bool SHADOW = SHADOW_, SC = SC_, FD = FD_, FAT = FAT_, CAM = CAM_, BF = BF_, UL2 = UL2_, PROF = PROF_;
+    static constexpr int R = R_, MINW = MINW_, PF = PF_, TILE = TILE_, CULL = CULL_, PLANE = PLANE_, LC = LC_;
+};
+#endif
+} // namespace tc
+
+// (macro arguments with commas come parenthesised: CR_UNPAREN strips the parentheses)
+#define CR_ID(...) __VA_ARGS__
+#define CR_UNPAREN(x) CR_ID x
+#define CR_WF3(CAM, CL, SH, ...) {wf_trace<CR_UNPAREN(CAM)>, wf_trace<CR_UNPAREN(CL)>, wf_trace<CR_UNPAREN(SH)>, __VA_ARGS__}
+#define CR_WFK(CAMK, CL, SH, ...) {CR_UNPAREN(CAMK), wf_trace<CR_UNPAREN(CL)>, wf_trace<CR_UNPAREN(SH)>, __VA_ARGS__}
+#ifdef CR_ALL_VARIANTS
 #define CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, PL)                                                     \
-    {wf_trace<false, false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU>,                                      \
-     wf_trace<false, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>,                                  \
-     wf_trace<true, false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL>, R, W, TL, CU, 0, 0}
+    CR_WF3((tc::Cfg<false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU, 0, 0>),                                 \
+           (tc::Cfg<false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL, 0>),                                \
+           (tc::Cfg<true, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL, 0>), R, W, TL, CU, 0, 0)
 #define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU) CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, 0)
 #define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, 0)
 #define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
 #define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
 #define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
 #define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
-// The trace builds, by index (cr_set_option "variant").  The default compile holds the
-// plain reference build 0, build 15 (the packet camera trace's fallback for an eye on a
-// split plane), builds 18 and 26 (round 2's and round 3's defaults), 40 / 42 (26 / 18 with the exact
-// short division in the camera packet) and the defaults 43 / 44 (40 / 42 with it in the shadow trace
-// too); every measured
-// and superseded build -- each is described below and in DESIGN.md §3 / §6 -- compiles
-// with `make ALL_VARIANTS=1` and is an empty entry (rejected at render) otherwise.
-#define CR_WF_NONE {nullptr, nullptr, nullptr, 8, 8, 0, 0, 0, 0}
-#ifdef CR_ALL_VARIANTS
-#define CR_WF_OPT(...) __VA_ARGS__
-#else
-#define CR_WF_OPT(...) CR_WF_NONE
+// 17-25: packet camera traces with the secondary / shadow builds of the round-2 / round-3 experiments
+#define CR_WF_LC(S, LCV, W, PROF)                                                                              \
+    CR_WFK(S, (tc::Cfg<false, 8, W, true, false, true, 1, false, true, 0, false, 0, 0, LCV, PROF>),              \
+           (tc::Cfg<true, 8, W, true, false, true, 1, false, true, 0, false, 0, 0, LCV, PROF>), 8, W, 0, 2, 1, 0)
 #endif
-static const WfVariant kWf[] = {
-    CR_WF(4, 8, false, false, false), CR_WF_OPT(CR_WF(8, 8, false, false, false)),
-    CR_WF_OPT(CR_WF(8, 8, true, false, false)), CR_WF_OPT(CR_WF(8, 6, false, false, false)),
-    CR_WF_OPT(CR_WF(8, 6, true, false, false)), CR_WF_OPT(CR_WF(8, 8, true, true, false)),
-    CR_WF_OPT(CR_WF(8, 8, true, false, true)), CR_WF_OPT(CR_WF(8, 8, false, false, true)),
-    CR_WF_OPT(CR_WF_PF(8, 8, true, false, false, 2)),
-    CR_WF_OPT(CR_WF_BF(8, 8, true, false, true, 1, true)),
-    // 10-12: build 9 with the top of the tree in LDS (TILE nodes, 32 B each, after the
-    // stack ring: 8 blocks x (R x 2 KiB + TILE x 32 B) within the CU's 160 KiB)
-    CR_WF_OPT(CR_WF_T(8, 8, true, false, true, 1, true, 128)), CR_WF_OPT(CR_WF_T(4, 8, true, false, true, 1, true, 384)),
-    CR_WF_OPT(CR_WF_T(4, 8, true, false, true, 1, true, 0)),
-    // 13: build 9 with a uniform leaf's records two per scalar-load wait
-    CR_WF_OPT(CR_WF_U(8, 8, true, false, true, 1, true, 0, true)),
-    // 14: build 9 whose camera trace skips triangle tests and leaves by the screen-space cull boxes
-    CR_WF_OPT(CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 1)),
-    // 15: 14 that also skips the subtrees whose box excludes the sample (checked at each fat-record fetch)
-    CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 2),
-    // 16: 15 whose secondary closest and shadow traces skip the tests their segment cannot
-    // pass by the triangle's plane (planecull.hpp)
-    CR_WF_OPT(CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1)),
-    // 17: 15 whose camera rays traverse as one packet per wave (wf_trace_packet)
-    CR_WF_OPT({wf_trace_packet<8, 1>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
-               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1, 0}),
-    // 18: 17 with two camera rays per lane (packets of 128 rays: the scalar control per node
-    // shared by twice the rays)
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0>, 8, 8, 0, 2, 1, 0},
-    // 19: 18 whose secondary closest and shadow traces skip the references a leaf's cull record
-    // (leafcull.hpp: two normal groups, each a box and a normal cone) excludes for the ray
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
-               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 8, 0, 2, 1, 0}),
-    // 20: 19 whose lanes pass a leaf with every reference excluded and descend to the next one
-    // in the same traversal round
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
-               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 8, 0, 2, 1, 0}),
-    // 21 / 22: 19 / 20 at 6 waves per SIMD (80 VGPRs: no spills)
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>,
-               wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 1>, 8, 6, 0, 2, 1, 0}),
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>,
-               wf_trace<true, false, 8, 6, true, false, true, 1, false, true, 0, false, 0, 0, 2>, 8, 6, 0, 2, 1, 0}),
-    // 23 / 24: 18 / 19 with the phase clock of the secondary and shadow traces (measurement only)
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>,
-               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, true>, 8, 8, 0, 2, 1, 0}),
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>,
-               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 1, true>, 8, 8, 0, 2, 1, 0}),
-    // 25: 19 with the fixed-pad records (one dot product and a slab test per group)
-    CR_WF_OPT({wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 3>,
-               wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 3>, 8, 8, 0, 2, 1, 0}),
-    // 26: 25 with the packed records (six float4 per leaf, leaves of up to 16 references);
-    // the tail kernel culls the same way
-    {wf_trace_packet<8, 2>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
-    // 27-39: measured on top of 26 in round 3 and rejected (DESIGN.md §3.7 keeps their numbers): the
-    //     exact short division by RN(1/d) kept in LDS (27) or in VGPRs (29), far-side-first shadow
-    //     traversal (28), the secondary closest trace at 7 waves (30) or without the leaf cull (31), dealt
-    //     shadow-leaf tests (32), cull records loaded one group at a time (33, 34), the shadow trace at 7
-    //     waves (35, 36), lanes passing up to 1 / 3 fully culled leaves per round (37-39)
-    CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE,
-    CR_WF_NONE, CR_WF_NONE, CR_WF_NONE, CR_WF_NONE,
-    // 40: 26 whose camera packet divides by the rays' RN(1/d) kept in VGPRs (FD; the packet's
-    //     spills are outside its loops): camera trace 41.0 -> 37.7 ms, 363.1 -> 360.0 ms per pass
-    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
-    // 41: 40 with packets of 64 rays (one per lane: no spills): camera 49.6 ms (rejected)
-    CR_WF_NONE,
+
+// The trace builds by number (cr_set_option "variant").  The default compile holds the plain reference
+// build 0, build 15 (the packet camera trace's fallback for an eye on a split plane), 18 and 26 (round 2's
+// and round 3's defaults), 40 / 42 (26 / 18 with the exact short division in the camera packet) and the
+// defaults 43 / 44 (40 / 42 with it in the shadow trace too).  The measured and superseded builds -- each
+// described below and in DESIGN.md §3 / §6 -- compile with `make ALL_VARIANTS=1`; the rejected builds
+// 27-39, 41 and 45 are gone (DESIGN.md keeps their numbers).
+struct WfBuild {
+    int id;
+    WfVariant v;
+};
+static const WfBuild kWf[] = {
+    {0, CR_WF3((tc::CameraRef), (tc::ClosestRef), (tc::ShadowRef), 4, 8, 0, 0, 0, 0)},
+    // 15: fat records, scalar loads, branch-light steps; the camera trace skips the tests, leaves and
+    // subtrees whose screen-space cull box excludes the sample
+    {15, CR_WF3((tc::CameraCull), (tc::ClosestFat), (tc::ShadowFat), 8, 8, 0, 2, 0, 0)},
+    // 18: 15 whose camera rays traverse as one packet of 128 per wave (two per lane; wf_trace_packet)
+    {18, {wf_trace_packet<8, 2>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFat>, 8, 8, 0, 2, 1, 0}},
+    // 26: 18 whose secondary closest and shadow traces skip the references a leaf's packed cull record
+    // (leafcull.hpp: two normal groups, each a box and a normal cone) excludes for the ray; the tail
+    // kernel culls the same way
+    {26, {wf_trace_packet<8, 2>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLc>, 8, 8, 0, 2, 1, 4}},
+    // 40: 26 whose camera packet divides by the rays' RN(1/d) kept in VGPRs (FD; the packet's spills are
+    //     outside its loops): camera trace 41.0 -> 37.7 ms, 363.1 -> 360.0 ms per pass
+    {40, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLc>, 8, 8, 0, 2, 1, 4}},
     // 42: 18 with 40's camera packet (the default below LEAF_CULL_MIN_TRIS triangles)
-    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
-     wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0},
+    {42, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFat>, 8, 8, 0, 2, 1, 0}},
     // 43 / 44 (the defaults): 40 / 42 whose shadow trace divides by the ray's RN(1/d) in VGPRs too (FD;
     //     no spills at 8 waves once the stack-overflow pointer and the query count stopped occupying
     //     VGPRs): 357.5 / 355.3 vs 358.4 / 358.1 ms per pass, nanobox 162.4 vs 163.7 ms (shadow 30.7 -> 29.9)
-    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4>,
-     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 4>, 8, 8, 0, 2, 1, 4},
-    {wf_trace_packet<8, 2, false, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0>,
-     wf_trace<true, false, 8, 8, true, true, true, 1, false, true, 0, false, 0, 0, 0>, 8, 8, 0, 2, 1, 0},
-    // 45: 43 with FD in the secondary closest trace too (3 loop-invariant lane values spilled; rejected)
-    CR_WF_NONE};
+    {43, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
+    {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 0, 2, 1, 0}},
+#ifdef CR_ALL_VARIANTS
+    {1, CR_WF(8, 8, false, false, false)}, {2, CR_WF(8, 8, true, false, false)}, {3, CR_WF(8, 6, false, false, false)},
+    {4, CR_WF(8, 6, true, false, false)}, {5, CR_WF(8, 8, true, true, false)}, {6, CR_WF(8, 8, true, false, true)},
+    {7, CR_WF(8, 8, false, false, true)}, {8, CR_WF_PF(8, 8, true, false, false, 2)},
+    {9, CR_WF_BF(8, 8, true, false, true, 1, true)},
+    // 10-12: build 9 with the top of the tree in LDS (TILE nodes, 32 B each, after the stack ring:
+    // 8 blocks x (R x 2 KiB + TILE x 32 B) within the CU's 160 KiB)
+    {10, CR_WF_T(8, 8, true, false, true, 1, true, 128)}, {11, CR_WF_T(4, 8, true, false, true, 1, true, 384)},
+    {12, CR_WF_T(4, 8, true, false, true, 1, true, 0)},
+    // 13: build 9 with a uniform leaf's records two per scalar-load wait
+    {13, CR_WF_U(8, 8, true, false, true, 1, true, 0, true)},
+    // 14: build 9 whose camera trace skips triangle tests and leaves by the screen-space cull boxes
+    {14, CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 1)},
+    // 16: 15 whose secondary closest and shadow traces skip the tests their segment cannot pass by the
+    // triangle's plane (planecull.hpp)
+    {16, CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1)},
+    // 17: 15 whose camera rays traverse as one packet per wave, one ray per lane
+    {17, CR_WF_LC((wf_trace_packet<8, 1>), 0, 8, false)},
+    // 19: 18 with the per-ray-bound leaf cull records; 20: 19 whose lanes pass a leaf with every reference
+    // excluded and descend to the next one in the same round; 21 / 22: 19 / 20 at 6 waves per SIMD
+    {19, CR_WF_LC((wf_trace_packet<8, 2>), 1, 8, false)}, {20, CR_WF_LC((wf_trace_packet<8, 2>), 2, 8, false)},
+    {21, CR_WF_LC((wf_trace_packet<8, 2>), 1, 6, false)}, {22, CR_WF_LC((wf_trace_packet<8, 2>), 2, 6, false)},
+    // 23 / 24: 18 / 19 with the phase clock of the secondary and shadow traces (measurement only)
+    {23, CR_WF_LC((wf_trace_packet<8, 2>), 0, 8, true)}, {24, CR_WF_LC((wf_trace_packet<8, 2>), 1, 8, true)},
+    // 25: 19 with the fixed-pad records (one dot product and a slab test per group)
+    {25, CR_WF_LC((wf_trace_packet<8, 2>), 3, 8, false)},
+#endif
+};
+static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
+// the build numbered `variant`, or null when it is not compiled in
+static const WfVariant *wf_build(int variant) {
+    for (int i = 0; i < kNumWf; i++)
+        if (kWf[i].id == variant) return &kWf[i].v;
+    return nullptr;
+}
+static const WfVariant &wf_build_or_ref(int variant) {
+    const WfVariant *v = wf_build(variant);
+    return v ? *v : kWf[0].v;
+}
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
-static const WfVariant kWfPerf26 = {
-    wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
-    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>, 8, 8, 0, 2, 1, 4};
-static const WfVariant kWfPerf18 = {
-    wf_trace_packet<8, 2, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>,
-    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>, 8, 8, 0, 2, 1, 0};
+static const WfVariant kWfPerf26 = {wf_trace_packet<8, 2, true>, wf_trace<tc::ClosestFatLcPerf>,
+                                    wf_trace<tc::ShadowFatLcPerf>, 8, 8, 0, 2, 1, 4};
+static const WfVariant kWfPerf18 = {wf_trace_packet<8, 2, true>, wf_trace<tc::ClosestFatPerf>,
+                                    wf_trace<tc::ShadowFatPerf>, 8, 8, 0, 2, 1, 0};
 // ... and builds 40 / 42 (26 / 18 with the FD camera packet: the same work, the division shortened)
-static const WfVariant kWfPerf40 = {
-    wf_trace_packet<8, 2, true, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>,
-    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 4, false, true>, 8, 8, 0, 2, 1, 4};
-static const WfVariant kWfPerf42 = {
-    wf_trace_packet<8, 2, true, true>, wf_trace<false, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>,
-    wf_trace<true, false, 8, 8, true, false, true, 1, false, true, 0, false, 0, 0, 0, false, true>, 8, 8, 0, 2, 1, 0};
+static const WfVariant kWfPerf40 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLcPerf>,
+                                    wf_trace<tc::ShadowFatLcPerf>, 8, 8, 0, 2, 1, 4};
+static const WfVariant kWfPerf42 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatPerf>,
+                                    wf_trace<tc::ShadowFatPerf>, 8, 8, 0, 2, 1, 0};
 // (43 / 44 count through 40 / 42's instances: their shadow trace's short division does the same work)
 bool wf_perf_available(int variant) {
     return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44;
@@ -1356,15 +1392,18 @@ static const WfVariant &perf_variant(int variant) {
            : (variant == 42 || variant == 44) ? kWfPerf42
                                               : kWfPerf26;
 }
-static const WfVariant kWfCount = {wf_trace<false, true, 8, 1, false, false, false, 1, true>,
-                                   wf_trace<false, true, 8, 1, false>, wf_trace<true, true, 8, 1, false>, 8, 4, 0,
-                                   0, 0, 0};
-static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
-int num_wf_variants() { return kNumWf; }
-// The camera-ray trace of a variant; the packet trace (build 17) needs a near child common
-// to all camera rays, which an eye lying exactly on a split plane breaks: build 15's then.
+static const WfVariant kWfCount = {wf_trace<tc::CameraCount>, wf_trace<tc::ClosestCount>, wf_trace<tc::ShadowCount>,
+                                   8, 4, 0, 0, 0, 0};
+// one past the largest build number (option validation)
+int num_wf_variants() {
+    int m = 0;
+    for (int i = 0; i < kNumWf; i++) m = kWf[i].id + 1 > m ? kWf[i].id + 1 : m;
+    return m;
+}
+// The camera-ray trace of a variant; the packet trace (build 17) needs a near child common to all
+// camera rays, which an eye lying exactly on a split plane breaks: build 15's then.
 static void (*camera_kernel(const WfVariant &v, const RenderArgs &A))(RenderArgs, WfArgs, uint32_t) {
-    return (v.packet && A.eye_on_split) ? kWf[15].camera : v.camera;
+    return (v.packet && A.eye_on_split) ? wf_build(15)->camera : v.camera;
 }
 // The chunk's camera rays come from the packet trace itself (WfArgs::cam_fused) when the ctx asks for it
 // (W.cam_fused on entry), the camera kernel is the packet trace, generation 1 runs as its own launches
@@ -1372,8 +1411,8 @@ static void (*camera_kernel(const WfVariant &v, const RenderArgs &A))(RenderArgs
 static bool camera_fuses(const WfVariant &v, const RenderArgs &A, const WfArgs &W) {
     return W.cam_fused && v.packet && !A.eye_on_split && camera_state_lean(W);
 }
-bool wf_variant_culls(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].cull; }
-bool wf_variant_available(int variant) { return variant >= 0 && variant < kNumWf && kWf[variant].closest; }
+bool wf_variant_culls(int variant) { return wf_build(variant) && wf_build(variant)->cull; }
+bool wf_variant_available(int variant) { return wf_build(variant) != nullptr; }
 
 // One thread per leaf reference: its cull box for this render's camera (camcull.hpp),
 // from the record's A, e1, e2 -- the floats the triangle test uses.  Boxes
@@ -1438,7 +1477,7 @@ int launch_cam_cull(const RenderArgs &A, uint32_t nrefs, float4 *boxes, float4 *
 }
 
 void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &blocks) {
-    const WfVariant &v = kWf[(variant >= 0 && variant < kNumWf) ? variant : 0];
+    const WfVariant &v = wf_build_or_ref(variant);
     block = 256;
     blocks = (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)v.waves_per_simd; // 4 SIMDs, 4 waves/block
 }
@@ -1533,7 +1572,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     WfArgs W = W0;
     const WfVariant &v = A.full_counters ? kWfCount
                          : A.perf_counters ? perf_variant(A.variant)
-                                           : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
+                                           : wf_build_or_ref(A.variant);
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     const uint32_t cblocks = blocks, sblocks = blocks;
@@ -1630,7 +1669,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
 int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hipStream_t st, TraceEvents *te) {
     const WfVariant &v = A.full_counters ? kWfCount
                          : A.perf_counters ? perf_variant(A.variant)
-                                           : kWf[(A.variant >= 0 && A.variant < kNumWf) ? A.variant : 0];
+                                           : wf_build_or_ref(A.variant);
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
     const uint32_t cblocks = blocks, sblocks = blocks;

@@ -10,6 +10,10 @@ import csv
 import json
 import re
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from kernel_names import trace_info  # noqa: E402
 
 
 def main():
@@ -29,16 +33,17 @@ def main():
             n = r["Kernel_Name"]
             ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
             tot += ms
-            if "wf_trace<false" in n or "wf_trace_packet" in n:  # the packet build's camera trace
+            info = trace_info(n)
+            if info and info[0] in ("camera", "closest"):
                 g += 1
                 k = "g%d closest" % g
-                counting |= re.search(r"wf_trace<false, true,", n) is not None
-            elif "wf_trace<true" in n:
+                counting |= info[1] != "lean"
+            elif info and info[0] == "shadow":
                 gs += 1
                 k = "g%d shadow" % gs
-            elif "wf_tail" in n:
+            elif info and info[0] == "tail":
                 k = "tail (g%d..)" % (gs + 1)
-                counting |= "wf_tail<true" in n
+                counting |= info[1] != "lean"
             elif "rocprim" in n or "rs_upsweep" in n or "rs_downsweep" in n or "rs_scan" in n:
                 k = "sort"
             elif "wf_shade" in n or "wf_bounce" in n or "wf_resolve" in n:

@@ -14,6 +14,10 @@ import csv
 import json
 import re
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from kernel_names import trace_info  # noqa: E402
 
 
 def main(src, dst, spp=128):
@@ -50,18 +54,10 @@ def main(src, dst, spp=128):
     # per lean trace kind (bench.py roofline.issue): SHADOW, FULL, ..., CAM[, BF] template args
     kinds = {}
     for k, v in out.items():
-        m = re.search(r"wf_trace<([^>]*)>", k)
-        if re.search(r"wf_trace_packet<\d+, \d+, true", k) or re.search(r"wf_trace<[^>]*, true>", k):
-            continue  # the performed-work counting instances (bench.py's perf pass)
-        if "wf_trace_packet" in k:  # the packet build's camera-ray trace (lean)
-            kind = "camera"
-        elif not m:
-            continue
-        else:
-            a = [x.strip() for x in m.group(1).split(",")]
-            if a[1] != "false":
-                continue
-            kind = "shadow" if a[0] == "true" else ("camera" if len(a) > 8 and a[8] == "true" else "closest")
+        info = trace_info(k)
+        if not info or info[0] == "tail" or info[1] != "lean":
+            continue  # the counting and performed-work instances, the tail kernel
+        kind = info[0]
         d = v["dispatches"]
         kinds[kind] = {"kernel": k, "valu_issue_busy": v["valu_issue_busy"], "salu_issue_busy": v["salu_issue_busy"],
                        "ta_busy": v.get("ta_busy"), "shader_clock_ghz": v["shader_clock_ghz"],

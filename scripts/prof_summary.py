@@ -24,16 +24,10 @@ import shutil
 import sys
 from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from kernel_names import is_counting, trace_info  # noqa: E402
+
 ROOT = Path(__file__).resolve().parents[1]
-
-
-def is_counting(name: str) -> bool:
-    # FULL is the second template argument of both trace kernels
-    # (and the performed-work counting instances of bench.py's perf pass: last template argument
-    # PC; profile runs pass --no-perf-pass, so these are not expected)
-    return (re.search(r"(wf_trace|render_dynamic)<\w+, true,", name) is not None or "wf_tail<true" in name or
-            re.search(r"(wf_trace|wf_tail)<[^()]*, true>\(", name) is not None or
-            re.search(r"wf_trace_packet<\d+, \d+, true", name) is not None)  # packet: PC is the third argument
 
 
 def main():
@@ -92,15 +86,11 @@ def main():
     # the trace kernel's lean instantiations (bench.py roofline): fabric bytes per launch
     trace = {}
     for n, e in summary.items():
-        m = re.search(r"wf_trace<([^>]*)>", n)
-        packet = "wf_trace_packet" in n  # the packet build's camera-ray trace (lean)
-        if not (m or packet) or "fabric_bytes_total" not in e:
+        info = trace_info(n)
+        if not info or info[0] == "tail" or "fabric_bytes_total" not in e:
             continue
-        # SHADOW, FULL, R, MINW, SC, FD, FAT, PF, CAM[, BF]
-        targs = ["false", "false"] if packet else [a.strip() for a in m.group(1).split(",")]
-        if targs[1] == "false":  # lean builds (the timed ones)
-            cam = packet or (len(targs) > 8 and targs[8] == "true")
-            kind = "shadow" if targs[0] == "true" else ("camera" if cam else "closest")
+        kind, mode = info
+        if mode == "lean":  # the timed builds
             trace[kind] = {
                 "kernel": n, "calls": e["calls"], "avg_ns": e["avg_ns"],
                 "fabric_bytes_per_launch": e["fabric_bytes_total"] / e["calls"]}

@@ -3,14 +3,10 @@
 One line per kernel: start offset and duration (ms), queue id, short name."""
 import csv
 import sys
+from pathlib import Path
 
-
-def short(n):
-    n = n.replace("(anonymous namespace)::", "").split("(")[0]
-    for k in ("wf_trace<false, false", "wf_trace<true, false", "wf_trace<false, true", "wf_trace<true, true"):
-        if n.startswith("void cr::" + k) or n.startswith("cr::" + k):
-            return ("closest" if "<false" in k else "shadow") + ("(count)" if k.endswith("true") else "") + n[n.find("<"):][:60]
-    return n.replace("void ", "").replace("cr::", "")[:70]
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from kernel_names import short  # noqa: E402
 
 
 def main():
