@@ -4,6 +4,7 @@
 // kernels.hip header), the progressive accumulator, the counters and the
 // per-launch HIP events.  No C++ exception or hipError_t crosses the ABI.
 #include "ctx.hpp"
+#include "quadnodes.hpp"
 #include "leafcull.hpp"
 #include "planecull.hpp"
 
@@ -205,6 +206,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     if (c->kernel == 2 && !c->full_counters && !cr::wf_variant_available(A.variant))
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
                                          " is not compiled in (make ALL_VARIANTS=1)");
+    if (c->kernel == 2 && !c->full_counters && cr::wf_variant_quad(A.variant) && !c->S.quad)
+        return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
+                                         " needs the two-level node records, which this scene's leaves do not fit");
     if (c->perf_counters && (c->kernel != 2 || c->full_counters || !cr::wf_perf_available(A.variant)))
         return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18 and 26 only, "
                                      "without the counting build");
@@ -694,6 +698,29 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         cr::leaf_cull_pack((const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
                            (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u,
                            (cr::LcFloat4 *)(lcullp.data() + (size_t)cr::LC_RECP * i));
+    // two-level node records (quadnodes.hpp) and the packed cull records by first reference, for trace builds
+    // 46 / 47 (make ALL_VARIANTS=1: measured slower, wavefront.hip kWf); a scene whose leaves do not fit the
+    // records' words, or whose per-reference cull table would pass 4 GiB, keeps the fat-record builds only
+    // (S.quad null)
+    cr::QuadLayout ql;
+    std::string qerr;
+#ifdef CR_ALL_VARIANTS
+    const bool quad_ok = (uint64_t)16 * cr::LC_RECP * ((uint64_t)d->n_refs + 1) <= 0xFFFFFFFFull &&
+                         cr::quad_build((const cr::QuadNode *)nodes.data(), NN, d->n_refs, ql, qerr);
+#else
+    const bool quad_ok = false;
+#endif
+    std::vector<uint4> quad;
+    std::vector<float4> lcullq;
+    if (quad_ok) {
+        quad.resize(ql.slots);
+        std::memcpy(quad.data(), ql.rec.data(), 16 * (size_t)ql.slots);
+        lcullq.assign((size_t)cr::LC_RECP * ((size_t)d->n_refs + 1), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (uint32_t i = 0; i < NN; i++)
+            if ((nodes[i].y & 3u) == 3u && (nodes[i].y >> 2))
+                std::memcpy(lcullq.data() + (size_t)cr::LC_RECP * nodes[i].x, lcullp.data() + (size_t)cr::LC_RECP * i,
+                            16 * cr::LC_RECP);
+    }
     std::vector<float4> tri((size_t)3 * nt), mn(nt), mkd(nt), mke(nt);
     std::vector<float2> muv((size_t)3 * nt);
     for (uint32_t t = 0; t < nt; t++) {
@@ -775,10 +802,12 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, lcullf, &c->S.lcullf)) || (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
-        (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels))) {
+        (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels)) ||
+        (quad_ok && ((rc = upload(c, quad, &c->S.quad)) || (rc = upload(c, lcullq, &c->S.lcullq))))) {
         free_scene(c);
         return rc;
     }
+    c->S.qfbits = quad_ok ? ql.fbits : 0u;
     c->S.nlights = d->n_lights;
     c->S.n_nodes = d->n_nodes;
     c->S.bmin = make_float3(d->box_min[0], d->box_min[1], d->box_min[2]);

@@ -93,6 +93,13 @@ struct DevScene {
     const float4 *lcull;
     const float4 *lcullf; // the same records in the fixed-pad form (leaf_cull_fixed, trace builds with LC 3)
     const float4 *lcullp; // ... packed (LC_RECP float4 per node, leaf_cull_pack, LC 4)
+    // two-level node records (quadnodes.hpp: {w_n, w_c0, w_c1, meta} per slot; null when the scene's
+    // leaves do not fit their words) and the packed leaf cull records indexed by a leaf's FIRST
+    // reference (LC_RECP float4 per reference, only leaves' firsts filled: the QUAD traces' leaves carry
+    // their first reference, not a node id); a quad leaf word is first | count << qfbits
+    const uint4 *quad;
+    const float4 *lcullq;
+    uint32_t qfbits;
     float db;             // bound on |coordinate| of any origin or vertex (padded box + 1)
     const float4 *tri;    // 3 per triangle: A, B, C
     const float4 *mat_n;  // normal, w = emissive flag bits
@@ -287,6 +294,7 @@ int num_wf_variants();
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
 bool wf_variant_available(int variant); // compiled in (the default compile holds builds 0, 15, 18, 26)
+bool wf_variant_quad(int variant);      // its secondary / shadow traces read DevScene::quad
 bool wf_perf_available(int variant);    // a performed-work instance of this trace build exists (18, 26)
 // cull boxes of this render's camera for the nrefs leaf references (+ 4 padding boxes)
 // and their unions per subtree (node_boxes[n_nodes]): leaves first, then the inner

@@ -144,6 +144,7 @@ typedef unsigned int cr_v2u __attribute__((ext_vector_type(2)));
 typedef float cr_v4f __attribute__((ext_vector_type(4)));
 typedef float cr_v8f __attribute__((ext_vector_type(8)));
 typedef unsigned int cr_v8u __attribute__((ext_vector_type(8)));
+typedef unsigned int cr_v4u __attribute__((ext_vector_type(4)));
 typedef float cr_v16f __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ uint2 sload_node(const uint2 *p) {
     cr_v2u r;
@@ -224,7 +225,8 @@ __device__ __forceinline__ void sload_lcull(const float4 *p, LcFloat4 (&r)[LC_RE
 }
 // The references of the leaf at `node` that the lane's ray (o, d: unit, segment [0, tmax])
 // must test (leafcull.hpp); bits < count.
-// FORM 0: per-ray bound records (S.lcull), 1: fixed-pad (S.lcullf), 2: packed fixed-pad (S.lcullp)
+// FORM 0: per-ray bound records (S.lcull), 1: fixed-pad (S.lcullf), 2: packed fixed-pad (S.lcullp),
+// 3: packed fixed-pad by first reference (S.lcullq)
 __device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_REC]) {
     cr_v16f a;
     cr_v8f b;
@@ -240,7 +242,8 @@ template <bool SC, int FORM = 0>
 __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
     LcFloat4 rec[LC_REC];
     constexpr int NR = FORM >= 2 ? LC_RECP : LC_REC;
-    const float4 *recs = FORM >= 2 ? S.lcullp : (FORM == 1 ? S.lcullf : S.lcull);
+    // FORM 3: the packed records indexed by the leaf's first reference (QUAD traces: `node` is that)
+    const float4 *recs = FORM == 3 ? S.lcullq : FORM == 2 ? S.lcullp : (FORM == 1 ? S.lcullf : S.lcull);
     if (SC && wave_uniform(node)) {
         if (FORM >= 2) sload_lcullp(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
         else sload_lcull(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
@@ -267,6 +270,18 @@ template <bool SC> __device__ __forceinline__ float4 load_box(const float4 *b, u
 template <bool SC> __device__ __forceinline__ uint2 load_node(const DevScene &S, uint32_t node) {
     if (SC && wave_uniform(node)) return sload_node(S.nodes + __builtin_amdgcn_readfirstlane(node));
     return S.nodes[node];
+}
+
+// Two-level node records (DevScene::quad, quadnodes.hpp): 16 B per record root, one dwordx4 (or one
+// s_load_dwordx4 when the wave is uniform) per two descent levels.
+__device__ __forceinline__ uint4 sload_quad(const uint4 *p) {
+    cr_v4u r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+template <bool SC> __device__ __forceinline__ uint4 load_quad(const DevScene &S, uint32_t slot) {
+    if (SC && wave_uniform(slot)) return sload_quad(S.quad + __builtin_amdgcn_readfirstlane(slot));
+    return *(const uint4 *)((const char *)S.quad + slot * 16u);
 }
 
 // Fat node records (DevScene::fat): 32 B per node, {self, child 0, child 1}, so
@@ -329,6 +344,7 @@ struct TraceDefaults {
     static constexpr int LC = 0;          // leaf cull records (1 per-ray, 2 passing culled leaves, 3 fixed, 4 packed)
     static constexpr bool PROF = false;   // phase clock (measurement only)
     static constexpr bool PC = false;     // performed-work counters (measurement only)
+    static constexpr bool QUAD = false;   // two-level 16-B node records (quadnodes.hpp) instead of fat ones
 };
 
 template <class C>
@@ -340,6 +356,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                                                Prof *pf = nullptr, Pc *pc = nullptr, uint32_t quorum = 0) {
     static constexpr int R = C::R, PF = C::PF, TILE = C::TILE, CULL = C::CULL, PLANE = C::PLANE, LC = C::LC;
     static constexpr bool FULL = C::FULL, FD = C::FD, SC = C::SC, FAT = C::FAT, BF = C::BF, UL2 = C::UL2;
+    static constexpr bool QUAD = C::QUAD;
     uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
     // quorum (lean FAT builds without the camera cull): the wave's descent stops at a fetch once at most
     // quorum / 64 of the lanes that entered the round still descend; those keep T.node (the node to fetch)
@@ -363,10 +380,13 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
     static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
+    static_assert(!QUAD || (BF && SC && !CULL && !PLANE && !TILE && !UL2 && LC != 2 && !FULL), "quad records: lean BF + SC builds");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
-    auto step = [&](uint2 nd) -> uint32_t {
+    // (sh: the children's positions are child + (side << sh) -- 0 for node ids and a record root's middle
+    // children, 2 for a middle node's child records in QUAD codes)
+    auto step = [&](uint2 nd, uint32_t sh = 0) -> uint32_t {
         if (pc) pc->steps++;
         if (FULL) {
             c.inner++;
@@ -394,7 +414,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                 const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
                 if (pc && T.nl == R) pc->vb += 8;
                 if (T.nl == R) gstack_at(gstk, T.sp - R, gstride, gid) = ring[slot]; // spill the oldest
-                ring[slot] = make_uint2(child + below, __float_as_uint(T.tmax));
+                ring[slot] = make_uint2(child + (below << sh), __float_as_uint(T.tmax));
             }
             T.nl = push && T.nl < R ? T.nl + 1 : T.nl;
             T.sp += push ? 1u : 0u;
@@ -413,7 +433,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             T.tmax = tsplit;
             k = 1u - below;
         }
-        T.node = child + k;
+        T.node = child + (k << sh);
         return k;
     };
     uint2 nd;
@@ -442,7 +462,45 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     // pops and descends to its next leaf in the same round, so the round's tests run on every lane
     for (;;) {
     culled = false;
-    if (FAT) { // two levels per dependent load: a node's record carries its children's
+    if (QUAD) { // two levels per 16-B record (quadnodes.hpp); T.node is a position code slot << 2 | sel
+        uint4 q;
+        auto fetchq = [&](uint32_t code) {
+            const uint32_t slot = code >> 2;
+            pc_load(pc, SC && wave_uniform(slot), 16);
+            q = load_quad<SC>(S, slot);
+        };
+        // the record root at `code` (sel 0): its word and axis; its children are the record's middle nodes
+        auto root_view = [&](uint32_t code) { return make_uint2(q.x, (q.w & 3u) | ((code + 1u) << 2)); };
+        // middle node k: its word and axis; its children are the records at gb_k, gb_k + 1 (codes stride 4)
+        auto mid_view = [&](uint32_t k) {
+            const uint32_t gb = (q.w >> 6) + (((k != 0u) & (((q.w >> 2) & 3u) != 3u)) ? 2u : 0u);
+            return make_uint2(k ? q.z : q.y, ((q.w >> (2u + 2u * k)) & 3u) | (gb << 4));
+        };
+        fetchq(T.node);
+        const uint32_t sel = T.node & 3u;
+        nd = sel ? mid_view(sel - 1u) : root_view(T.node);
+        if (sel && (nd.y & 3u) != 3u) { // a popped middle node: its own step, then its child's record
+            step(nd, 2);
+            fetchq(T.node);
+            nd = root_view(T.node);
+        }
+        while ((nd.y & 3u) != 3u) {
+            const uint32_t k = step(nd);
+            nd = mid_view(k);
+            if ((nd.y & 3u) != 3u) {
+                step(nd, 2);
+                if (quorum && (uint32_t)__popcll(__ballot(1)) * 64u <= nbusy * quorum) {
+                    nd = make_uint2(PENDING_LEAF, 3u); // (no leaf word has `first` 0xfffffffe's bits and count)
+                } else {
+                    fetchq(T.node);
+                    nd = root_view(T.node);
+                }
+            }
+        }
+        pending = quorum && nd.x == PENDING_LEAF;
+        // the leaf's word -> {first, 3 | count << 2}, the fat records' leaf form
+        if (!pending) nd = make_uint2(nd.x & ((1u << S.qfbits) - 1u), 3u | ((nd.x >> S.qfbits) << 2));
+    } else if (FAT) { // two levels per dependent load: a node's record carries its children's
         uint4 f0, f1;
         auto fetch = [&](uint32_t node) {
             if (TILE && node < (uint32_t)TILE) {
@@ -523,11 +581,13 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     lmask = 0u;
     if (LC && count && count <= (uint32_t)LC_MAXREFS) {
         // LC 3: the fixed-pad records; leaves below lc_min: every reference, no check
+        // (QUAD: the records are indexed by the leaf's first reference)
+        const uint32_t lcid = QUAD ? first : T.node;
         if (pc && count >= lc_min) {
             pc->masks++;
-            pc_load(pc, SC && wave_uniform(T.node), 16u * (LC >= 4 ? LC_RECP : LC_REC));
+            pc_load(pc, SC && wave_uniform(lcid), 16u * (LC >= 4 ? LC_RECP : LC_REC));
         }
-        lmask = count >= lc_min ? leaf_mask<SC, LC == 4 ? 2 : (LC == 3 ? 1 : 0)>(S, T.node, count, o, d, T.tmax)
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 4 ? (QUAD ? 3 : 2) : (LC == 3 ? 1 : 0)>(S, lcid, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }

@@ -386,8 +386,9 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
             if (r != busy_st) {
                 if (PC) pc.vb += SHADOW ? 4u : 16u;
                 if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
+                // w: the hit's leaf + 1 (QUAD: its record slot + 1), the queue sort's key region
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
-                                                           __float_as_uint(d.y), T.node + 1u) // w: the hit's leaf + 1
+                                                           __float_as_uint(d.y), (C::QUAD ? T.node >> 2 : T.node) + 1u)
                                               : make_uint4(0u, 0u, 0u, 0u);
                 state = ST_NEED_WORK;
             }
@@ -1239,6 +1240,7 @@ struct WfVariant {
     int cull; // the camera trace reads the cull boxes (1: references and leaves, 2: also subtrees)
     int packet; // the camera trace is a packet trace (needs a near child common to all camera rays)
     int lc;     // the tail kernel's leaf cull form (trav_round's LC; 0: none)
+    int quad = 0; // the secondary / shadow traces read the two-level records (DevScene::quad)
 };
 
 // The trace configurations of the builds (traverse.hpp TraceDefaults), by what they restate.
@@ -1259,11 +1261,21 @@ struct ShadowFatLc : ClosestFatLc { static constexpr bool SHADOW = true; };
 // + the exact short split division by the ray's RN(1/d) in the shadow trace (43; 44 without the leaf cull)
 struct ShadowFatLcFd : ShadowFatLc { static constexpr bool FD = true; };
 struct ShadowFatFd : ShadowFat { static constexpr bool FD = true; };
+// + two-level 16-B node records (quadnodes.hpp: one dwordx4 per two descent levels instead of the fat
+// records' dwordx4 + dwordx2; 46, 47)
+struct ClosestQuadLc : ClosestFatLc { static constexpr bool QUAD = true; };
+struct ShadowQuadLcFd : ShadowFatLcFd { static constexpr bool QUAD = true; };
+struct ClosestQuad : ClosestFat { static constexpr bool QUAD = true; };
+struct ShadowQuadFd : ShadowFatFd { static constexpr bool QUAD = true; };
 // the performed-work counting instances (RenderArgs::perf_counters; measurement only)
 struct ClosestFatLcPerf : ClosestFatLc { static constexpr bool PC = true; };
 struct ShadowFatLcPerf : ShadowFatLc { static constexpr bool PC = true; };
 struct ClosestFatPerf : ClosestFat { static constexpr bool PC = true; };
 struct ShadowFatPerf : ShadowFat { static constexpr bool PC = true; };
+struct ClosestQuadLcPerf : ClosestQuadLc { static constexpr bool PC = true; };
+struct ShadowQuadLcPerf : ShadowFatLcPerf { static constexpr bool QUAD = true; };
+struct ClosestQuadPerf : ClosestQuad { static constexpr bool PC = true; };
+struct ShadowQuadPerf : ShadowFatPerf { static constexpr bool QUAD = true; };
 // the counting build (SURVEY §8d work counters, diagnostics: RenderArgs::full_counters), 1 wave per SIMD
 struct Count : TraceDefaults { static constexpr bool FULL = true; static constexpr int MINW = 1; };
 struct CameraCount : Count { static constexpr bool CAM = true; };
@@ -1334,6 +1346,16 @@ static const WfBuild kWf[] = {
     {43, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
     {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 0, 2, 1, 0}},
 #ifdef CR_ALL_VARIANTS
+    // 46 / 47: 43 / 44 whose secondary closest and shadow traces descend over the two-level 16-B records
+    //     (quadnodes.hpp; the same decisions at the same nodes with the same intervals, one dwordx4 per
+    //     two levels instead of a dwordx4 + dwordx2: 46% fewer descent fetch instructions on the sponza
+    //     stand-in, scripts/quad_census.py).  Round 5, two interleaved rounds at the driver's command:
+    //     2183.1 / 2182.1 (43) vs 2134.7 / 2138.5 Mray/s (46); shadow 41.6 -> 42.8 ms, closest beside it
+    //     73.2 -> 75.2 ms -- the traces are not bound by their count of vector loads (the L1 is at 0.82 of
+    //     its tag rate, profiles/r05_pmc_mem_sponza.json) but by instruction issue, and the quad records'
+    //     middle-node views and the resumption of a popped middle child add VALU and SALU per level
+    {46, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestQuadLc>, wf_trace<tc::ShadowQuadLcFd>, 8, 8, 0, 2, 1, 4, 1}},
+    {47, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestQuad>, wf_trace<tc::ShadowQuadFd>, 8, 8, 0, 2, 1, 0, 1}},
     {1, CR_WF(8, 8, false, false, false)}, {2, CR_WF(8, 8, true, false, false)}, {3, CR_WF(8, 6, false, false, false)},
     {4, CR_WF(8, 6, true, false, false)}, {5, CR_WF(8, 8, true, true, false)}, {6, CR_WF(8, 8, true, false, true)},
     {7, CR_WF(8, 8, false, false, true)}, {8, CR_WF_PF(8, 8, true, false, false, 2)},
@@ -1382,11 +1404,23 @@ static const WfVariant kWfPerf40 = {wf_trace_packet<8, 2, true, true>, wf_trace<
                                     wf_trace<tc::ShadowFatLcPerf>, 8, 8, 0, 2, 1, 4};
 static const WfVariant kWfPerf42 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatPerf>,
                                     wf_trace<tc::ShadowFatPerf>, 8, 8, 0, 2, 1, 0};
+#ifdef CR_ALL_VARIANTS
+// ... and builds 46 / 47 (the quad-record descent: fewer, smaller node loads, the same steps)
+static const WfVariant kWfPerf46 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestQuadLcPerf>,
+                                    wf_trace<tc::ShadowQuadLcPerf>, 8, 8, 0, 2, 1, 4, 1};
+static const WfVariant kWfPerf47 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestQuadPerf>,
+                                    wf_trace<tc::ShadowQuadPerf>, 8, 8, 0, 2, 1, 0, 1};
+#endif
 // (43 / 44 count through 40 / 42's instances: their shadow trace's short division does the same work)
 bool wf_perf_available(int variant) {
-    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44;
+    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 ||
+           (wf_variant_available(variant) && (variant == 46 || variant == 47));
 }
 static const WfVariant &perf_variant(int variant) {
+#ifdef CR_ALL_VARIANTS
+    if (variant == 46) return kWfPerf46;
+    if (variant == 47) return kWfPerf47;
+#endif
     return variant == 18 ? kWfPerf18
            : (variant == 40 || variant == 43) ? kWfPerf40
            : (variant == 42 || variant == 44) ? kWfPerf42
@@ -1413,6 +1447,7 @@ static bool camera_fuses(const WfVariant &v, const RenderArgs &A, const WfArgs &
 }
 bool wf_variant_culls(int variant) { return wf_build(variant) && wf_build(variant)->cull; }
 bool wf_variant_available(int variant) { return wf_build(variant) != nullptr; }
+bool wf_variant_quad(int variant) { return wf_build(variant) && wf_build(variant)->quad; }
 
 // One thread per leaf reference: its cull box for this render's camera (camcull.hpp),
 // from the record's A, e1, e2 -- the floats the triangle test uses.  Boxes

@@ -20,7 +20,8 @@ ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit",
 # trace's fallback), round 2's default 18, 26 (leaf cull records), 40 / 42 (26 / 18 with the exact
 # short division in the camera packet) and the defaults 43 / 44 (40 / 42 with it in the shadow trace)
 TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
-# builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="37 38"
+# builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="46 47" (the
+# two-level quad node records, csrc/quadnodes.hpp; their perf instances too)
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
@@ -830,7 +831,7 @@ def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
     assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2
 
 
-@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44])
+@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44] + [b for b in TRACE_BUILDS if b in (46, 47)])
 @pytest.mark.parametrize("tail_min", [0, 3000])
 def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
     """The performed-work builds (option perf_counters: builds 18 / 26 / 40 / 42 with counters, cr_get_perf)
@@ -868,7 +869,7 @@ def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
             assert pk["leaves"] <= rk["leaf"] and pk["steps"] <= rk["inner"], (kind, pk, rk)
             if kind != "camera" and tail_min == 0:
                 assert (pk["steps"], pk["leaves"]) == (rk["inner"], rk["leaf"]), (kind, pk, rk)
-                if variant in (18, 42, 44):
+                if variant in (18, 42, 44, 47):
                     assert pk["masks"] == 0 and pk["tests"] == rk["tritest"], (kind, pk, rk)
                 else:
                     assert pk["masks"] <= pk["leaves"]
