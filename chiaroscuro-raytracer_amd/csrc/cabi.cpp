@@ -357,6 +357,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cam_fused = c->wf_cam_fuse;
                 W.ctl_ray = c->wf_ctl_ray;
                 W.vis_dw = c->wf_vis_dw;
+                W.vis_mark = c->wf_vis_mark && !c->wf_fold && !c->wf_tail_overlap && p->k <= 63 ? 1 : 0;
                 W.nee_skip = c->wf_nee_skip;
                 W.tail_waves = c->wf_tail_waves;
                 if (sort) {
@@ -1210,6 +1211,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_cam_fuse") && (v == 0 || v == 1)) c->wf_cam_fuse = (int)v;
     else if (!std::strcmp(key, "wf_ctl_ray") && (v == 0 || v == 1)) c->wf_ctl_ray = (int)v;
     else if (!std::strcmp(key, "wf_vis_dw") && (v == 0 || v == 1)) c->wf_vis_dw = (int)v;
+    else if (!std::strcmp(key, "wf_vis_mark") && (v == 0 || v == 1)) c->wf_vis_mark = (int)v;
     else if (!std::strcmp(key, "sum_lds") && v >= 0 && v <= 65536) c->sum_lds = (uint32_t)v;
     else if (!std::strcmp(key, "wf_nee_skip") && (v == 0 || v == 1)) c->wf_nee_skip = (int)v;
     else if (!std::strcmp(key, "sum_staged") && (v == 0 || v == 1)) c->sum_staged = (int)v;

@@ -106,6 +106,8 @@ struct cr_ctx {
     // WfArgs::vis_dw; round 4, two interleaved rounds: sponza 318.1 / 317.9 -> 318.0 / 318.3 ms per layer,
     // cornell_box 105.7 / 106.1 -> 105.1 / 105.1 ms per pass
     int wf_vis_dw = 1;
+    // WfArgs::vis_mark (round 5)
+    int wf_vis_mark = 1;
     // WfArgs::nee_skip; round 4, two interleaved rounds: sponza 316.6 / 317.0 -> 293.7 / 293.1 ms per
     // layer, cornell_box 103.2 / 102.3 -> 95.1 / 95.3 ms per pass, nanobox 144.6 / 145.0 -> 142.9 / 143.0
     int wf_nee_skip = 1;

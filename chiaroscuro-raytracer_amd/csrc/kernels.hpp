@@ -277,6 +277,12 @@ struct WfArgs {
     // that bounce (SHADOW_VIS / SHADOW_OCC) instead of occ[slot] -- wf_resolve then reads no occ entries,
     // which a sorted shadow queue scatters over the paths (option "wf_vis_dw")
     int vis_dw;
+    // 1 (option "wf_vis_mark", needs fold 0, no overlapped tail, K <= 63): the resolve marks are
+    // (k << 2) | visible << 1 | ended; wf_shade writes PS3 = direct + contrib (the reference's add for a
+    // visible NEE ray, done there) and a mark with visible 0, the shadow trace sets visible for an
+    // unoccluded answer (one byte, nothing for an occluded one), and wf_resolve touches only the paths
+    // whose bounce is visible (copy PS3 over dw) or ended (fold) -- no dw read / write for the rest
+    int vis_mark;
     // 1: an NEE query whose contribution is exactly zero is answered without a trace (wavefront.hip
     // nee_zero; lean builds only -- the counting and performed-work builds trace every query) and
     // counted as a shadow query (option "wf_nee_skip")

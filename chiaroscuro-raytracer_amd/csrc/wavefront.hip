@@ -240,9 +240,17 @@ __global__ void __launch_bounds__(256) wf_camera(RenderArgs A, WfArgs W) {
 // dw record of bounce g (idx is then the path), which held the query's slot (SHADOW_VIS / SHADOW_OCC
 // replace it; NO_SLOT -- no NEE ray -- is never written here).
 enum : uint32_t { SHADOW_VIS = 0u, SHADOW_OCC = 1u };
+// With WfArgs::vis_mark idx is the path | ENDED_BIT when it ends at this bounce: a visible answer sets the
+// visible bit of the path's resolve mark (one byte), an occluded one writes nothing.
+enum : uint32_t { ENDED_BIT = 0x80000000u };
 __device__ __forceinline__ void shadow_store(const WfArgs &W, uint32_t g, uint32_t idx, bool occluded) {
-    if (W.vis_dw) ((uint32_t *)(W.dw + (size_t)(2 * (g - 1)) * W.P + idx))[3] = occluded ? SHADOW_OCC : SHADOW_VIS;
-    else W.occ[idx] = occluded ? 1u : 0u;
+    if (W.vis_mark) {
+        if (!occluded) W.mark[idx & ~ENDED_BIT] = (uint8_t)((g << 2) | 2u | (idx >> 31));
+    } else if (W.vis_dw) {
+        ((uint32_t *)(W.dw + (size_t)(2 * (g - 1)) * W.P + idx))[3] = occluded ? SHADOW_OCC : SHADOW_VIS;
+    } else {
+        W.occ[idx] = occluded ? 1u : 0u;
+    }
 }
 // WfArgs::nee_skip: an NEE term of exactly (+0, +0, +0) -- the reference's geometric factor max(0, ...)
 // is 0 (the surface or the light faces away), or the product underflows -- adds nothing whatever the
@@ -346,8 +354,12 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
                         if (!(SHADOW && W.ended_only && (W.sexcl[idx] & SEXCL_CONT))) {
                         o = ld3(r0);
                         d = ld3(r1);
-                        if (SHADOW) exclude = W.sexcl[idx] & ~SEXCL_CONT;
-                        if (SHADOW && W.vis_dw) idx = __float_as_uint(r0.w); // the result goes to path idx's dw
+                        const uint32_t sx = SHADOW ? W.sexcl[idx] : 0u;
+                        if (SHADOW) exclude = sx & ~SEXCL_CONT;
+                        // the result goes to path idx's dw record (vis_dw) or resolve mark (vis_mark: its
+                        // ended bit rides in idx)
+                        if (SHADOW && W.vis_mark) idx = __float_as_uint(r0.w) | ((sx & SEXCL_CONT) ? 0u : ENDED_BIT);
+                        else if (SHADOW && W.vis_dw) idx = __float_as_uint(r0.w);
                         if (CULL) { // ray idx of generation 1 is path idx's camera ray
                             const float2 q = W.cxy[idx];
                             csx = q.x;
@@ -359,7 +371,7 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
                             state = busy_st;
                             if (FULL) diag_begin(&dg);
                         } else if (SHADOW) {
-                            if (PC) pc.vb += 4;
+                            if (PC) pc.vb += W.vis_mark ? 1u : 4u;
                             shadow_store(W, g, idx, false); // culled: visible (kdtree.cpp:285-287)
                         } else {
                             if (PC) pc.vb += 16;
@@ -384,7 +396,7 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
                 A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr, A.desc_quorum);
             if (r != busy_st) {
-                if (PC) pc.vb += SHADOW ? 4u : 16u;
+                if (PC) pc.vb += SHADOW ? (W.vis_mark ? (r == ST_OCCLUDED ? 0u : 1u) : 4u) : 16u;
                 if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
                 // w: the hit's leaf + 1 (QUAD: its record slot + 1), the queue sort's key region
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
@@ -555,8 +567,9 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
         }
     }
     direct = hs.direct;
-    PS(W, 3, p) = pk(contrib, 0u);
-    W.mark[p] = (uint8_t)((k << 1) | (cont ? 0u : 1u));
+    // vis_mark: the visible case's D_k = direct + contrib, the reference's add (rayTracer.cpp:96-99) done here
+    PS(W, 3, p) = pk(W.vis_mark ? add(hs.direct, contrib) : contrib, 0u);
+    W.mark[p] = (uint8_t)(W.vis_mark ? (k << 2) | (cont ? 0u : 1u) : (k << 1) | (cont ? 0u : 1u));
     return nee;
 }
 
@@ -666,8 +679,20 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
 // D_k = direct + (visible ? contrib : 0) (rayTracer.cpp:96-99), and the
 // back-to-front fold of every path that ended at this bounce (ended: bit 0 of its mark).
 // The contribution (PS3) is read only for a visible NEE ray.
-__device__ __forceinline__ void resolve_path(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t g, bool ended) {
+// m: the path's resolve mark (a hit of generation g)
+__device__ __forceinline__ void resolve_path(const RenderArgs &A, const WfArgs &W, uint32_t p, uint32_t g, uint32_t m) {
+    const bool ended = m & 1u;
     float4 &dk = W.dw[(size_t)(2 * (g - 1)) * W.P + p];
+    if (W.vis_mark) { // dw holds direct; PS3 direct + contrib, the D_k of a visible NEE ray
+        if (m & 2u) {
+            const float4 s3 = PS(W, 3, p);
+            if (ended) finish_path(A, W, p, g, ld3(s3));
+            else dk = s3;
+        } else if (ended) {
+            finish_path(A, W, p, g, ld3(dk));
+        }
+        return;
+    }
     const float4 d4 = dk;
     const uint32_t slot = __float_as_uint(d4.w);
     f3 direct = ld3(d4);
@@ -684,9 +709,10 @@ __device__ __forceinline__ void resolve_path(const RenderArgs &A, const WfArgs &
 __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32_t g) {
     const uint32_t n = *cnt_closest(W, g);
     if (W.resolve_paths && (uint64_t)n * W.resolve_paths >= (uint64_t)W.P) {
+        const uint32_t sh = W.vis_mark ? 2u : 1u;
         for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < W.P; p += gridDim.x * blockDim.x) {
             const uint32_t m = W.mark[p];
-            if ((m >> 1) == g && (!W.ended_only || (m & 1u))) resolve_path(A, W, p, g, m & 1u);
+            if ((m >> sh) == g && (!W.ended_only || (m & 1u))) resolve_path(A, W, p, g, m);
         }
         return;
     }
@@ -698,7 +724,7 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
         const uint32_t m = W.mark[p]; // (2g | ended: a hit of this queue)
         // (overlapped tail: a continuing path is the tail's, which resolves this bounce itself)
         if (W.ended_only && !(m & 1u)) continue;
-        resolve_path(A, W, p, g, m & 1u);
+        resolve_path(A, W, p, g, m);
     }
 }
 
@@ -708,8 +734,8 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
 __global__ void __launch_bounds__(256) wf_fold(RenderArgs A, WfArgs W, uint32_t g) {
     const uint32_t n = *cnt_ended(W, g);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        // (overlapped tail: only the ended paths are here, which the tail never takes)
-        resolve_path(A, W, W.ended[i], g, true);
+        // (overlapped tail: only the ended paths are here, which the tail never takes; fold: no vis_mark)
+        resolve_path(A, W, W.ended[i], g, 1u);
     }
     // fold 2: the paths that go on -- closest queue g + 1 -- have their bounce g resolved here too (beside
     // the closest trace of g + 1, off the critical path), unless an overlapped tail resolves them itself

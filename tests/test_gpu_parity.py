@@ -89,9 +89,11 @@ def test_wavefront_sort_choice_bitexact(ca, cornell_mm, sponza, sort):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("fold,resolve_paths,vis", [(1, 16, 0), (2, 16, 0), (0, 0, 0), (0, 1, 0), (0, 4, 0), (0, 64, 0),
-                                                   (0, 16, 1), (0, 0, 1), (1, 16, 1), (2, 16, 1)])
-def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_paths, vis):
+@pytest.mark.parametrize("fold,resolve_paths,vis,mark", [(1, 16, 0, 1), (2, 16, 0, 1), (0, 0, 0, 1), (0, 1, 0, 1),
+                                                        (0, 4, 0, 1), (0, 64, 0, 1), (0, 16, 1, 1), (0, 0, 1, 1),
+                                                        (1, 16, 1, 1), (2, 16, 1, 1), (0, 16, 1, 0), (0, 0, 1, 0),
+                                                        (0, 64, 0, 0)])
+def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_paths, vis, mark):
     """The NEE term of a bounce and the fold of an ended path: by default (wf_fold 0) wf_resolve's
     sweep after each shadow trace, in queue order (resolve_paths 0) or, for queues of at least
     P / resolve_paths rays, in path order by the PS3 bounce mark (default 16; 64: nearly every
@@ -100,11 +102,14 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
     generation, wf_tail at pickup) or beside the next closest trace from its queue (2).  The same bits and
     counters over progressive layers 1..3 on the same buffers (a mark left by an earlier layer or chunk
     must not resolve a path twice), sorted queues, one chunk and wf_paths 4096 chunks.  wf_vis_dw 1: the
-    shadow trace writes each result over the slot in the path's dw record instead of occ[slot]."""
+    shadow trace writes each result over the slot in the path's dw record instead of occ[slot].  wf_vis_mark 1
+    (the default; wf_fold 0 only): wf_shade stores the visible case's D_k = direct + contrib, the shadow trace
+    sets the visible bit of the path's mark, and wf_resolve touches only visible or ended bounces."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_fold", fold)
         pair.dev.set_option("wf_vis_dw", vis)
+        pair.dev.set_option("wf_vis_mark", mark)
         pair.dev.set_option("wf_resolve_paths", resolve_paths)
         pair.dev.set_option("wf_sort_min", 0)
         cam = pair.camera(ca, x, y)
@@ -122,6 +127,7 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
         finally:
             pair.dev.set_option("wf_fold", 0)
             pair.dev.set_option("wf_vis_dw", VIS_DEFAULT)
+            pair.dev.set_option("wf_vis_mark", 1)
             pair.dev.set_option("wf_resolve_paths", 16)
             pair.dev.set_option("wf_sort_min", 1 << 20)
             pair.dev.set_option("wf_paths", 256 << 20)
