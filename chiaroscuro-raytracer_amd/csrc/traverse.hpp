@@ -140,6 +140,11 @@ __device__ __forceinline__ bool trav_begin(const DevScene &S, f3 o, f3 d, bool s
 // lane wants the same node / leaf, one s_load serves the wave and the vector
 // memory address path -- the measured bottleneck -- is not used at all.  The
 // data is read-only for the whole launch, so the scalar cache is coherent.
+// Every block that issues more than one load marks its outputs early-clobber
+// ("=&s"): without it the register allocator may give a later load's base the
+// registers an earlier load of the same block is filling, and a scalar load
+// that returns before the next one issues then rewrites that base (the
+// full-size-only illegal address of the grandchild-prefetch builds).
 typedef unsigned int cr_v2u __attribute__((ext_vector_type(2)));
 typedef float cr_v4f __attribute__((ext_vector_type(4)));
 typedef float cr_v8f __attribute__((ext_vector_type(8)));
@@ -155,7 +160,7 @@ __device__ __forceinline__ TriRec sload_rec(const float4 *p) {
     cr_v8f a;
     cr_v4f b;
     asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(a), "=s"(b)
+                 : "=&s"(a), "=&s"(b)
                  : "s"(p));
     return TriRec{make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]),
                   make_float4(b[0], b[1], b[2], b[3])};
@@ -166,7 +171,7 @@ __device__ __forceinline__ void sload_rec2(const float4 *p, TriRec &r0, TriRec &
     cr_v16f a;
     cr_v8f b;
     asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx8 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(a), "=s"(b)
+                 : "=&s"(a), "=&s"(b)
                  : "s"(p));
     r0 = TriRec{make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]),
                 make_float4(a[8], a[9], a[10], a[11])};
@@ -189,7 +194,7 @@ __device__ __forceinline__ void sload_fat_box(const uint4 *p, const float4 *q, u
     cr_v8u r;
     cr_v4f x;
     asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(r), "=s"(x)
+                 : "=&s"(r), "=&s"(x)
                  : "s"(p), "s"(q));
     a = make_uint4(r[0], r[1], r[2], r[3]);
     b = make_uint4(r[4], r[5], r[6], r[7]);
@@ -202,7 +207,7 @@ __device__ __forceinline__ void sload_fat_box_n(const uint4 *fat, const float4 *
     cr_v8u r;
     cr_v4f x;
     asm volatile("s_load_dwordx8 %0, %2, %4\n\ts_load_dwordx4 %1, %3, %5\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(r), "=s"(x)
+                 : "=&s"(r), "=&s"(x)
                  : "s"(fat), "s"(boxes), "s"(n * 32u), "s"(n * 16u));
     a = make_uint4(r[0], r[1], r[2], r[3]);
     b = make_uint4(r[4], r[5], r[6], r[7]);
@@ -215,7 +220,7 @@ __device__ __forceinline__ void sload_lcull(const float4 *p, LcFloat4 (&r)[LC_RE
     cr_v4f c;
     asm volatile("s_load_dwordx16 %0, %3, 0x0\n\ts_load_dwordx8 %1, %3, 0x40\n\ts_load_dwordx4 %2, %3, 0x60\n\t"
                  "s_waitcnt lgkmcnt(0)"
-                 : "=s"(a), "=s"(b), "=s"(c)
+                 : "=&s"(a), "=&s"(b), "=&s"(c)
                  : "s"(p));
 #pragma unroll
     for (int i = 0; i < 4; i++) r[i] = LcFloat4{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]};
@@ -231,7 +236,7 @@ __device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_R
     cr_v16f a;
     cr_v8f b;
     asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx8 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(a), "=s"(b)
+                 : "=&s"(a), "=&s"(b)
                  : "s"(p));
 #pragma unroll
     for (int i = 0; i < 4; i++) r[i] = LcFloat4{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]};

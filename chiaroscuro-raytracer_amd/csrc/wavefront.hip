@@ -937,7 +937,12 @@ enum : uint32_t { PACKET_DEPTH = 256 }; // >= the deepest tree cr_upload_scene a
 // entry it owns.
 // FD: the split distance by the exact short division from the ray's RN(1/d) per axis, kept in
 // VGPRs (div_by_rcp: Markstein's correction, the full division outside its checked range).
-template <int R, int S, bool PC = false, bool FD = false>
+// SPEC: the fat record and subtree box of the node the packet reaches if both of a fetch's levels go to
+// the near child (the eye's side: the packet's common near child) are loaded right after the fetch, while
+// the two levels' lane work runs -- only when that node's parent record is inner and its index is inside
+// the tree (a leaf's words hold a reference range, not a child index), and used when it is the next fetch.
+typedef const __attribute__((address_space(4))) cr_v4u k_v4u;
+template <int R, int S, bool PC = false, bool FD = false, bool SPEC = false>
 __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint32_t pring_lds[]; // [R][blockDim][S] per-ray tmax bits at push
     __shared__ uint32_t pnode[4][PACKET_DEPTH];
@@ -1155,6 +1160,9 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             }
         };
         bool go = any_active();
+        uint32_t spec = 0xffffffffu; // SPEC: the node whose records sf0, sf1, sb were loaded ahead
+        uint4 sf0 = make_uint4(0u, 0u, 0u, 0u), sf1 = sf0;
+        float4 sb = make_float4(0.f, 0.f, 0.f, 0.f);
         while (go) {
             // fetch node cn: its record, both children's records and its subtree box
             uint4 f0, f1;
@@ -1164,7 +1172,37 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                 pc.sb += 48;
                 pc.waves++;
             }
-            sload_fat_box_n(Sc.fat, cnode, cn, f0, f1, b);
+            if (SPEC && cn == spec) {
+                f0 = sf0;
+                f1 = sf1;
+                b = sb;
+            } else {
+                sload_fat_box_n(Sc.fat, cnode, cn, f0, f1, b);
+            }
+            if (SPEC) { // the near-near grandchild (all uniform: the eye, the records)
+                spec = 0xffffffffu;
+                if ((f0.y & 3u) != 3u) {
+                    const uint32_t a0 = f0.y & 3u;
+                    const float e0 = a0 == 0u ? eye_s[0] : (a0 == 1u ? eye_s[1] : eye_s[2]);
+                    const bool below0 = e0 < __uint_as_float(f0.x);
+                    const uint32_t rx = below0 ? f0.z : f1.x, ry = below0 ? f0.w : f1.y; // the near child's record
+                    if ((ry & 3u) != 3u) { // inner: ry >> 2 is a child index (a leaf's is a reference count)
+                        const uint32_t a1 = ry & 3u;
+                        const float e1 = a1 == 0u ? eye_s[0] : (a1 == 1u ? eye_s[1] : eye_s[2]);
+                        const uint32_t gc = (ry >> 2) + (e1 < __uint_as_float(rx) ? 0u : 1u);
+                        if (gc < Sc.n_nodes) {
+                            spec = __builtin_amdgcn_readfirstlane(gc);
+                            // (compiler-visible scalar loads: it places the wait before the first use)
+                            const k_v4u *kf = (const k_v4u *)Sc.fat, *kb = (const k_v4u *)cnode;
+                            const cr_v4u x0 = kf[2u * spec], x1 = kf[2u * spec + 1u], xb = kb[spec];
+                            sf0 = make_uint4(x0[0], x0[1], x0[2], x0[3]);
+                            sf1 = make_uint4(x1[0], x1[1], x1[2], x1[3]);
+                            sb = make_float4(__uint_as_float(xb[0]), __uint_as_float(xb[1]), __uint_as_float(xb[2]),
+                                             __uint_as_float(xb[3]));
+                        }
+                    }
+                }
+            }
 #pragma unroll
             for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, b);
             uint2 nd = make_uint2(f0.x, f0.y);
@@ -1372,6 +1410,14 @@ static const WfBuild kWf[] = {
     {43, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
     {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 0, 2, 1, 0}},
 #ifdef CR_ALL_VARIANTS
+    // 48: 43 whose camera packet loads the near-near grandchild's records ahead (SPEC), issued before the
+    //     current node's box test so the next fetch finds them in SGPRs.  Bit-exact; two interleaved
+    //     rounds at the driver's command 2187.0 / 2191.7 (43) vs 2114.9 / 2114.3 Mray/s: camera trace
+    //     34.9 -> 44.5 ms -- the loads that miss (the packet goes elsewhere 28% of the time,
+    //     tests/native/packet_check.cpp) and the 12 SGPRs they hold cost more than the wait they hide.
+    //     (Its first runs faulted at full size: traverse.hpp's two-load asm blocks lacked early-clobber
+    //     outputs; scripts/smem_hazard.py now checks every built object for that.)
+    {48, {wf_trace_packet<8, 2, false, true, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
     // 46 / 47: 43 / 44 whose secondary closest and shadow traces descend over the two-level 16-B records
     //     (quadnodes.hpp; the same decisions at the same nodes with the same intervals, one dwordx4 per
     //     two levels instead of a dwordx4 + dwordx2: 46% fewer descent fetch instructions on the sponza

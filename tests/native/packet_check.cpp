@@ -13,9 +13,17 @@
 // pop from the ray's current tmax (the kd stack invariant), far-only rays parked with
 // tmax = tmin.  For every ray the sequence of (leaf, tmin, tmax) tests and the answer
 // must equal the recursion's.
-//   packet_check <seed> <cases> [mutant]   prints "violations N rays M leaf_tests L"
+//   packet_check <seed> <cases> [mutant]   prints "violations N rays M leaf_tests L spec S spec_used U spec_bad B"
 // mutant 1: far-only rays not parked (tmax kept); 2: every ray's tmax set at a push, active
 // or not -- both must be caught (the check has teeth).
+// The speculative load of build 48 (wf_trace_packet SPEC): at every fetch the kernel computes, from the
+// fetched fat record alone, the near-near grandchild whose records it loads ahead.  The model encodes
+// every node as the kernel's words (inner: split bits, axis | child << 2; leaf: first reference,
+// 3 | count << 2 -- a leaf's `first` runs far past the node count) and checks each speculative index: it
+// must come from an inner record and lie inside the tree (spec_bad counts the others; the run fails).
+// mutant 3: the near child's record not checked for a leaf, its child index read from the word a leaf
+// keeps its first reference in (the unguarded form) -- must be caught.  (An index from an inner record is
+// a child of the tree, always inside it: the kernel's bound check only backs that up.)
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -39,6 +47,7 @@ struct Node {
     float split = 0;
     int child = -1; // children at child, child + 1
     std::vector<float> hits; // leaf: hit distances
+    uint32_t first = 0, count = 0; // leaf: its reference range (the kernel's leaf words)
 };
 std::vector<Node> tree;
 
@@ -48,6 +57,7 @@ int build(int depth, float lo[3], float hi[3]) {
     if (depth == 0 || rnd() < 0.06) {
         const int nh = rnd() < 0.7 ? 0 : 1 + (int)(rnd() * 3);
         for (int i = 0; i < nh; i++) tree[id].hits.push_back((float)(rnd() * 40.0 - 5.0));
+        tree[id].count = 1 + (uint32_t)(rnd() * 12); // (first is numbered after the build, in node order)
         return id;
     }
     const int a = (int)(rnd() * 3);
@@ -112,6 +122,45 @@ bool ref(int ray, int node, const float d[3], float tmin, float tmax, std::vecto
     return ref(ray, farc, d, tsplit, tmax, log, best);
 }
 
+// the kernel's two words of node n (cr_upload_scene's encoding)
+void words(int n, uint32_t &x, uint32_t &y) {
+    const Node &t = tree[n];
+    if (t.axis < 0) {
+        x = t.first;
+        y = 3u | t.count << 2;
+    } else {
+        memcpy(&x, &t.split, 4);
+        y = (uint32_t)t.axis | (uint32_t)t.child << 2;
+    }
+}
+long long spec_n = 0, spec_used = 0, spec_bad = 0;
+// build 48's speculative index after fetching node cn (0xffffffff: none), from the fat record's words
+uint32_t speculate(int cn) {
+    uint32_t x0, y0;
+    words(cn, x0, y0);
+    if ((y0 & 3u) == 3u) return 0xffffffffu;
+    float s0;
+    memcpy(&s0, &x0, 4);
+    const uint32_t a0 = y0 & 3u, c0 = y0 >> 2;
+    const bool below0 = eye[a0] < s0;
+    uint32_t rx, ry;
+    words((int)(below0 ? c0 : c0 + 1), rx, ry); // the near child's record, in the fat record
+    uint32_t gc;
+    if (mutant == 3) { // unguarded: a leaf's record taken for an inner one, its first word as the index
+        gc = ((ry & 3u) == 3u) ? rx : (ry >> 2);
+    } else {
+        if ((ry & 3u) == 3u) return 0xffffffffu;
+        float s1;
+        memcpy(&s1, &rx, 4);
+        gc = (ry >> 2) + (eye[ry & 3u] < s1 ? 0u : 1u);
+    }
+    if (mutant != 3 && gc >= tree.size()) return 0xffffffffu;
+    spec_n++;
+    const bool inner_src = (ry & 3u) != 3u;
+    if (gc >= tree.size() || !inner_src) spec_bad++;
+    return gc;
+}
+
 // The packet traversal of wf_trace_packet<R, S> (S rays per lane x 64 lanes = the packet).
 void packet(int nr, const std::vector<std::vector<float>> &dir, std::vector<float> tmin, std::vector<float> tmax,
             std::vector<std::vector<Rec>> &log, std::vector<int> &found, std::vector<float> &best) {
@@ -139,8 +188,14 @@ void packet(int nr, const std::vector<std::vector<float>> &dir, std::vector<floa
     };
     int cn = 0;
     bool go = any();
+    uint32_t spec = 0xffffffffu;
+    int lvl_fetch = 0; // levels since the last fetch (the kernel fetches every two levels)
     while (go) {
         bool popit = true;
+        if (lvl_fetch == 0) { // a fetch: the speculative index of its record (SPEC)
+            if ((uint32_t)cn == spec) spec_used++;
+            spec = speculate(cn);
+        }
         for (;;) {
             for (int r = 0; r < nr; r++) active[r] = active[r] && !culled(cn, r); // the node's box
             if (!any()) break;
@@ -192,9 +247,11 @@ void packet(int nr, const std::vector<std::vector<float>> &dir, std::vector<floa
             break; // fetch cn (the kernel's two-level fat step is the same sequence of decisions)
         }
         if (!popit) {
+            lvl_fetch = (lvl_fetch + 1) & 1; // (two levels per fetched fat record)
             go = true;
             continue;
         }
+        lvl_fetch = 0; // a pop fetches its node
         go = false;
         while (!stack.empty()) {
             Entry e = stack.back();
@@ -229,6 +286,12 @@ int main(int argc, char **argv) {
         tree.clear();
         float lo[3] = {-10, -10, -10}, hi[3] = {10, 10, 10};
         build(6 + (int)(rnd() * 11), lo, hi);
+        uint32_t refs = 0;
+        for (Node &n : tree)
+            if (n.axis < 0) {
+                n.first = refs; // leaves' reference ranges in node order: past the node count soon
+                refs += n.count;
+            }
         cull_seed = (uint32_t)next();
         for (int i = 0; i < 3; i++) eye[i] = (float)(rnd() * 16.0 - 8.0);
         // an eye exactly on a split plane breaks the common near child: the host then uses
@@ -269,6 +332,7 @@ int main(int argc, char **argv) {
             }
         }
     }
-    printf("violations %lld rays %lld leaf_tests %lld\n", viol, rays, tests);
-    return viol ? 1 : 0;
+    printf("violations %lld rays %lld leaf_tests %lld spec %lld spec_used %lld spec_bad %lld\n", viol, rays, tests,
+           spec_n, spec_used, spec_bad);
+    return viol || spec_bad ? 1 : 0;
 }

@@ -45,3 +45,29 @@ def test_packet_model_has_teeth(exe, mutant):
     """Without parking far-only rays (1), or with inactive rays' tmax changed at a push
     (2), the restored intervals differ from the recursion's."""
     assert _run(exe, 1, 200, mutant)[0] > 0
+
+
+def _spec(exe, seed, cases, mutant=0):
+    r = subprocess.run([str(exe), str(seed), str(cases), str(mutant)], capture_output=True, text=True, timeout=300)
+    m = re.search(r"spec (\d+) spec_used (\d+) spec_bad (\d+)", r.stdout)
+    assert m, r.stdout + r.stderr
+    return [int(v) for v in m.groups()]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_speculative_grandchild_index_guarded(exe, seed):
+    """Build 48's camera packet loads the near-near grandchild's records ahead of the fetch that needs
+    them (wf_trace_packet SPEC).  Its index comes from the fetched fat record alone: taken only when the
+    near child's record is inner (a leaf's words hold its reference range, which runs past the node count)
+    and inside the tree.  Every speculative index of the model's packets obeys that, and most of them are
+    the next fetch."""
+    spec, used, bad = _spec(exe, seed, 600)
+    assert bad == 0 and spec > 20_000 and used > 0.5 * spec
+
+
+def test_speculative_index_model_has_teeth(exe):
+    """The unguarded form -- the near child's record read as inner even when it is a leaf, so a reference
+    offset becomes a node index -- is caught.  (That was the first suspect for the full-size fault of the
+    prefetch builds; with the index guarded they still faulted, and the cause was the asm blocks'
+    missing early-clobber outputs, tests/test_smem_hazard.py.)"""
+    assert _spec(exe, 1, 300, 3)[2] > 0
