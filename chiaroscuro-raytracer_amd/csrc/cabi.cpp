@@ -160,9 +160,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // round 3): camera trace 41.1 -> 37.1 ms on the sponza stand-in, 24.1 -> 22.1 on nanobox,
     // 3.54 -> 3.55 on cornell_box (short packets: the reciprocals cost what they save);
     // 43 / 44 = 40 / 42 with the short division in the shadow trace too: 358.2 -> 356.4 ms, nanobox
-    // 163.7 -> 162.4 ms
+    // 163.7 -> 162.4 ms; 49 = 43 with the compressed leaf cull records (round 5: 48 B per leaf, three
+    // loads instead of six): 2179 -> 2252 Mray/s at the driver's command, shadow 41.7 -> 40.0 ms
     A.variant = c->variant >= 0 ? c->variant
-                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 43 : 44)
+                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 49 : 44)
                                  : 0;
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
@@ -683,8 +684,9 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     }
     // ... and in the fixed-pad form: origins and vertices inside the padded box (+1: the 0.001 n offsets)
     std::vector<float4> lcullf((size_t)cr::LC_REC * NN, make_float4(0.f, 0.f, 0.f, 0.f));
+    double lc_db = 1.0;
     {
-        double db = 1.0, smax = 0.0;
+        double &db = lc_db, smax = 0.0;
         for (int i = 0; i < 3; i++) {
             db = std::max(db, std::max(std::fabs((double)d->box_min[i]), std::fabs((double)d->box_max[i])) + 1.0);
             smax = std::max(smax, (double)d->box_max[i] - (double)d->box_min[i] + 2.0);
@@ -699,6 +701,14 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         cr::leaf_cull_pack((const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
                            (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u,
                            (cr::LcFloat4 *)(lcullp.data() + (size_t)cr::LC_RECP * i));
+    // ... and compressed on the scene's grid (48 B per node, LC 5)
+    const cr::LcGrid lcg = cr::lc_grid_make((const cr::LcFloat4 *)lcullf.data(), NN, lc_db);
+    std::vector<uint4> lcullc((size_t)cr::LC_RECC * NN, make_uint4(0u, 0u, 0u, 0u));
+    for (uint32_t i = 0; i < NN; i++)
+        cr::leaf_cull_compress((const cr::LcFloat4 *)(lcull.data() + (size_t)cr::LC_REC * i),
+                               (const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
+                               (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u, lcg,
+                               (uint32_t *)(lcullc.data() + (size_t)cr::LC_RECC * i));
     // two-level node records (quadnodes.hpp) and the packed cull records by first reference, for trace builds
     // 46 / 47 (make ALL_VARIANTS=1: measured slower, wavefront.hip kWf); a scene whose leaves do not fit the
     // records' words, or whose per-reference cull table would pass 4 GiB, keeps the fat-record builds only
@@ -800,7 +810,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         free_scene(c);
         return rc;
     }
-    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, lcullf, &c->S.lcullf)) || (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, tri, &c->S.tri)) ||
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, lcullf, &c->S.lcullf)) || (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, lcullc, &c->S.lcullc)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
         (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels)) ||
@@ -809,6 +819,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         return rc;
     }
     c->S.qfbits = quad_ok ? ql.fbits : 0u;
+    c->S.lcg = lcg;
     c->S.nlights = d->n_lights;
     c->S.n_nodes = d->n_nodes;
     c->S.bmin = make_float3(d->box_min[0], d->box_min[1], d->box_min[2]);

@@ -161,6 +161,82 @@ CR_LC_HD inline uint32_t leaf_cull_mask_packed(const float o[3], const float d[3
     return keep & all;
 }
 
+// Compressed fixed-pad records (LC_RECC uint4 = 48 B per node, leaves of up to 16 references):
+// the packed record's six 16-B loads per leaf were the secondary and shadow traces' largest
+// load-instruction cost.  Twelve words:
+//   {box0 x, y, z} {ax0.x | ax0.y << 16} {ax0.z | kappa0 << 16} {dt0 | dt1 << 16}
+//   {box1 x, y, z} {ax1.x | ax1.y << 16} {ax1.z | kappa1 << 16} {mask0 | mask1 << 16}
+// box word: lo | hi << 16 on the scene's grid (LcGrid: base + q * step), lo rounded down and hi up
+// past the fixed-pad box by the rounding of the kernels' fused evaluation (below); the normal
+// cone's axis as three IEEE halves (any vector: kappa is recomputed for the decoded one), kappa
+// and dt as halves rounded up; tk is one bound for the whole scene (LcGrid::tk).  A reference in
+// neither mask is tested always.  Every change against the fixed-pad record only enlarges a bound,
+// so the skip stays exact (tests/native/leafcull_check.cpp, form 3).
+// The slab parameter of a grid plane q is RN(RN(fma(q, step, RN(base - o))) * inv): the plane
+// moves by |RN(base - o) - (base - o)| <= u |base - o| <= u (|base| + db), which the host pads;
+// the relative rounding is that of the fixed form's RN(RN(lo - o) * inv).
+enum { LC_RECC = 3 };
+struct LcGrid {
+    float base[3], step[3], tk;
+    float pad; // (host: the margin every box got past its fixed-pad bounds)
+};
+// an IEEE half (low 16 bits of h) as float: exact
+CR_LC_HD inline float lc_half(uint32_t h) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)h);
+#else
+    const uint32_t e = (h >> 10) & 31u, m = h & 1023u;
+    const float v = e == 0 ? ldexpf((float)m, -24) : e == 31 ? (m ? NAN : INFINITY) : ldexpf((float)(m | 1024u), (int)e - 25);
+    return (h & 0x8000u) ? -v : v;
+#endif
+}
+// lc_group_skip_fixed on a compressed group (bo[i] = RN(base[i] - o[i])).  FINITE: every inv[i] is
+// finite, so no slab parameter is NaN (0 * inf) -- entry and exit are then plain min / max, the
+// values the NaN-aware selects give (up to the sign of a zero, which no comparison below sees)
+template <bool FINITE = false>
+CR_LC_HD inline bool lc_group_skip_c(const float d[3], const float inv[3], const float bo[3], float tmax,
+                                     const uint32_t box[3], uint32_t axw, uint32_t azk, float dt, const LcGrid &G) {
+    const float u = 0x1p-24f;
+    const float dn = fabsf((d[0] * lc_half(axw & 0xffffu) + d[1] * lc_half(axw >> 16)) + d[2] * lc_half(azk & 0xffffu));
+    if (!(dn >= lc_half(azk >> 16))) return false; // possibly grazing (or NaN): never skipped
+    const float t_hi = (tmax * G.tk) * (1.f + 2.f * u) + dt, t_lo = -dt;
+    float tn = -INFINITY, tf = INFINITY;
+    for (int i = 0; i < 3; i++) {
+        const float t0 = fmaf((float)(box[i] & 0xffffu), G.step[i], bo[i]) * inv[i];
+        const float t1 = fmaf((float)(box[i] >> 16), G.step[i], bo[i]) * inv[i];
+        if (FINITE) {
+            tn = i ? fmaxf(tn, fminf(t0, t1)) : fminf(t0, t1);
+            tf = i ? fminf(tf, fmaxf(t0, t1)) : fmaxf(t0, t1);
+        } else {
+            const bool nan = !(t0 == t0) || !(t1 == t1);
+            const float a = nan ? -INFINITY : (t0 < t1 ? t0 : t1), b = nan ? INFINITY : (t0 < t1 ? t1 : t0);
+            tn = a > tn ? a : tn;
+            tf = b < tf ? b : tf;
+        }
+    }
+    // the slab parameters carry 4u of relative rounding (4u |t| is exact: the fma rounds once)
+    tn = fmaf(-4.f * u, fabsf(tn), tn);
+    tf = fmaf(4.f * u, fabsf(tf), tf);
+    return (tn > tf) | (tn > t_hi) | (tf < t_lo);
+}
+CR_LC_HD inline uint32_t leaf_cull_mask_c(const float o[3], const float d[3], const float inv[3], bool unit, float tmax,
+                                          const uint32_t w[12], uint32_t count, const LcGrid &G) {
+    const uint32_t all = count >= 32 ? 0xffffffffu : ((1u << count) - 1u);
+    if (!unit || count > (uint32_t)LC_MAXREFS_P) return all;
+    const uint32_t m0 = w[11] & 0xffffu, m1 = w[11] >> 16;
+    const float bo[3] = {G.base[0] - o[0], G.base[1] - o[1], G.base[2] - o[2]};
+    const float dt0 = lc_half(w[5] & 0xffffu), dt1 = lc_half(w[5] >> 16);
+    uint32_t drop = 0u;
+    if (fabsf(inv[0]) < INFINITY && fabsf(inv[1]) < INFINITY && fabsf(inv[2]) < INFINITY) {
+        if (m0 && lc_group_skip_c<true>(d, inv, bo, tmax, w, w[3], w[4], dt0, G)) drop |= m0;
+        if (m1 && lc_group_skip_c<true>(d, inv, bo, tmax, w + 6, w[9], w[10], dt1, G)) drop |= m1;
+    } else {
+        if (m0 && lc_group_skip_c(d, inv, bo, tmax, w, w[3], w[4], dt0, G)) drop |= m0;
+        if (m1 && lc_group_skip_c(d, inv, bo, tmax, w + 6, w[9], w[10], dt1, G)) drop |= m1;
+    }
+    return all & ~drop;
+}
+
 // The references of a leaf (count of them) its tests need for this ray: bit j for
 // reference first + j.  rec: the node's LC_REC float4.  Leaves beyond LC_MAXREFS and
 // non-unit rays: every reference (the caller tests count references then).
@@ -385,6 +461,136 @@ inline void leaf_cull_pack(const LcFloat4 fx[LC_REC], uint32_t count, LcFloat4 o
         b = ((b + 0xffu) & ~0xffu) | bytes[i];
         __builtin_memcpy(w[i], &b, 4);
     }
+}
+
+// Host: the smallest IEEE half >= x (x >= 0; +inf when none is)
+inline uint32_t lc_half_up(double x) {
+    if (!(x >= 0.0)) return x < 0.0 ? 0u : 0x7c00u;
+    if (!(x <= 65504.0)) return 0x7c00u;
+    uint32_t lo = 0u, hi = 0x7bffu;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) / 2u;
+        if ((double)lc_half(mid) >= x) hi = mid;
+        else lo = mid + 1u;
+    }
+    return lo;
+}
+// Host: the nearest IEEE half to x (finite x within the half range)
+inline uint32_t lc_half_near(double x) {
+    const uint32_t sg = x < 0 ? 0x8000u : 0u;
+    const uint32_t h = lc_half_up(fabs(x));
+    if (h == 0u || h >= 0x7c00u) return sg | (h >= 0x7c00u ? 0x7bffu : 0u);
+    return sg | ((double)lc_half(h) - fabs(x) <= fabs(x) - (double)lc_half(h - 1u) ? h : h - 1u);
+}
+// Host: the scene's grid from the fixed-pad boxes of every group that has references (fx: LC_REC
+// float4 per node, n nodes), for origins with |o_i| <= db.  pad: the fused evaluation moves a plane by
+// up to u |base - o| <= u (|base| + db); the boxes get 2.5 times that bound (the rest covers the host's
+// double arithmetic); tk = the largest group tk.
+inline LcGrid lc_grid_make(const LcFloat4 *fx, size_t n, double db) {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float tk = 1.f;
+    for (size_t i = 0; i < n; i++) {
+        const LcFloat4 *r = fx + (size_t)LC_REC * i;
+        uint32_t m[2];
+        __builtin_memcpy(&m[0], &r[6].x, 4);
+        __builtin_memcpy(&m[1], &r[6].y, 4);
+        for (int k = 0; k < 2; k++) {
+            if (!m[k]) continue;
+            const float l[3] = {r[3 * k].x, r[3 * k].y, r[3 * k].z}, h[3] = {r[3 * k + 1].x, r[3 * k + 1].y, r[3 * k + 1].z};
+            bool fin = fabs(r[3 * k + 2].w) < 1e30;
+            for (int a = 0; a < 3; a++) fin = fin && fabs(l[a]) < 1e30 && fabs(h[a]) < 1e30; // (NaN: false)
+            if (!fin) continue;
+            for (int a = 0; a < 3; a++) {
+                lo[a] = fmin(lo[a], (double)l[a]);
+                hi[a] = fmax(hi[a], (double)h[a]);
+            }
+            tk = fmaxf(tk, r[3 * k + 2].w);
+        }
+    }
+    double M = db;
+    for (int a = 0; a < 3; a++)
+        if (lo[a] <= hi[a]) M = fmax(M, fmax(fabs(lo[a]), fabs(hi[a])));
+    const double pad = 2.5 * 0x1p-24 * (db + M) * (1 + 1e-6) + 1e-30;
+    LcGrid G;
+    G.pad = (float)pad;
+    if ((double)G.pad < pad) G.pad = nextafterf(G.pad, INFINITY);
+    for (int a = 0; a < 3; a++) {
+        if (lo[a] <= hi[a]) {
+            lo[a] -= 2 * (double)G.pad;
+            hi[a] += 2 * (double)G.pad;
+        }
+        if (!(lo[a] <= hi[a])) lo[a] = hi[a] = 0.0;
+        G.base[a] = (float)lo[a];
+        if ((double)G.base[a] > lo[a]) G.base[a] = nextafterf(G.base[a], -INFINITY);
+        float s = (float)((hi[a] - (double)G.base[a]) / 65535.0);
+        if (!(s > 0.f)) s = 1e-30f;
+        while ((double)G.base[a] + 65535.0 * (double)s < hi[a]) s = nextafterf(s, INFINITY);
+        G.step[a] = s;
+    }
+    G.tk = tk;
+    return G;
+}
+// Host: the fixed-pad record of a node (fx, leaf_cull_fixed of `in`) compressed to twelve words on
+// grid G (its boxes G.pad past the fixed ones); count: the leaf's references (above LC_MAXREFS_P: every
+// one tested always).  A group whose box leaves the grid, or that the fixed record never skips, gets
+// kappa = +inf (never skipped).  The planes are the exact reals base + q step (the kernels' fma).
+inline void leaf_cull_compress(const LcFloat4 in[LC_REC], const LcFloat4 fx[LC_REC], uint32_t count, const LcGrid &G,
+                               uint32_t w[12]) {
+    const double pad = G.pad;
+    for (int i = 0; i < 12; i++) w[i] = 0u;
+    uint32_t m[2];
+    __builtin_memcpy(&m[0], &fx[6].x, 4);
+    __builtin_memcpy(&m[1], &fx[6].y, 4);
+    if (count > (uint32_t)LC_MAXREFS_P) m[0] = m[1] = 0u;
+    const double u = 0x1p-24, c0 = 1.0 / LC_C0_INV;
+    uint32_t hd[2] = {0u, 0u};
+    for (int k = 0; k < 2; k++) {
+        uint32_t *box = w + 6 * k;
+        box[4] = 0x7c00u << 16; // kappa +inf: never skipped
+        if (!m[k]) continue;
+        // the axis as three halves, and the cone around the decoded vector: the fixed record's
+        // half-angle plus the axis's move
+        const double a[3] = {in[3 * k + 2].x, in[3 * k + 2].y, in[3 * k + 2].z};
+        const double an = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        if (!(an > 0)) continue;
+        uint32_t hv[3];
+        double v[3];
+        for (int i = 0; i < 3; i++) {
+            hv[i] = lc_half_near(a[i] / an);
+            v[i] = lc_half(hv[i]);
+        }
+        const double vn = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) * (1 + 1e-15);
+        if (!(vn > 0.5)) continue;
+        const double cd = fmin(1.0, fabs(a[0] * v[0] + a[1] * v[1] + a[2] * v[2]) / (an * vn));
+        const double th = acos(fmin(1.0, fmax(0.0, (double)in[3 * k + 2].w))) + acos(cd) + 1e-9;
+        const double room = acos(c0) - th, g = in[3 * k].w;
+        if (!(room > 1e-6 && c0 > 20.2 * u * g && g < 1e20) || !(fx[3 * k + 2].w <= G.tk)) continue;
+        // the box on the grid, outward past the pad (base + q step exact in double: q < 2^16)
+        bool ok = true;
+        uint32_t bw[3];
+        for (int i = 0; i < 3 && ok; i++) {
+            const double lo = (double)(&fx[3 * k].x)[i] - pad, hi = (double)(&fx[3 * k + 1].x)[i] + pad;
+            const double b = G.base[i], st = G.step[i];
+            double ql = floor((lo - b) / st), qh = ceil((hi - b) / st);
+            if (!(ql >= 0.0) || !(qh <= 65535.0)) {
+                ok = false;
+                break;
+            }
+            while (ql > 0.0 && b + ql * st > lo) ql -= 1.0;
+            while (qh < 65535.0 && b + qh * st < hi) qh += 1.0;
+            ok = b + ql * st <= lo && b + qh * st >= hi;
+            bw[i] = (uint32_t)ql | (uint32_t)qh << 16;
+        }
+        if (!ok) continue;
+        // dn >= (K + 3.01u)(1 + 8u)|v|  =>  |d^.v^| >= K (|d| <= 1 + 8u, the float dot's rounding)
+        const uint32_t hk = lc_half_up((cos(room) + 1e-12 + 3.01 * u) * (1 + 8 * u) * vn * (1 + 1e-9));
+        for (int i = 0; i < 3; i++) box[i] = bw[i];
+        box[3] = hv[0] | hv[1] << 16;
+        box[4] = hv[2] | hk << 16;
+        hd[k] = lc_half_up((double)fx[3 * k + 1].w);
+    }
+    w[5] = hd[0] | hd[1] << 16;
+    w[11] = (m[0] & 0xffffu) | (m[1] & 0xffffu) << 16;
 }
 
 } // namespace cr

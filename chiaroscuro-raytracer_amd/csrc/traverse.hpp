@@ -243,8 +243,36 @@ __device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_R
     r[4] = LcFloat4{b[0], b[1], b[2], b[3]};
     r[5] = LcFloat4{b[4], b[5], b[6], b[7]};
 }
+// FORM 4: the compressed records (S.lcullc, 48 B: three 16-B loads, or one 48-B scalar load pair)
+__device__ __forceinline__ void sload_lcullc(const uint4 *p, uint32_t (&w)[12]) {
+    cr_v8u a;
+    cr_v4u b;
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b)
+                 : "s"(p));
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = a[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[8 + i] = b[i];
+}
 template <bool SC, int FORM = 0>
 __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
+    if (FORM == 4) {
+        uint32_t w[12];
+        if (SC && wave_uniform(node)) {
+            sload_lcullc(S.lcullc + (size_t)LC_RECC * __builtin_amdgcn_readfirstlane(node), w);
+        } else {
+            const uint4 *p = (const uint4 *)((const char *)S.lcullc + node * (uint32_t)(16 * LC_RECC));
+#pragma unroll
+            for (int i = 0; i < LC_RECC; i++) {
+                const uint4 v = p[i];
+                w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
+            }
+        }
+        const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
+        const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+        return leaf_cull_mask_c(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, w, count, S.lcg);
+    }
     LcFloat4 rec[LC_REC];
     constexpr int NR = FORM >= 2 ? LC_RECP : LC_REC;
     // FORM 3: the packed records indexed by the leaf's first reference (QUAD traces: `node` is that)
@@ -259,6 +287,16 @@ __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, 
             const float4 v = p[i];
             rec[i] = LcFloat4{v.x, v.y, v.z, v.w};
         }
+#ifdef CR_PAD_LC // address-path calibration only: CR_PAD_LC extra 16-B loads of the record's own lines
+        typedef const __attribute__((address_space(1))) cr_v4f g_f4;
+        g_f4 *q = (g_f4 *)p;
+        asm volatile("" : "+v"(q));
+#pragma unroll
+        for (int i = 0; i < CR_PAD_LC; i++) {
+            const cr_v4f v = q[i];
+            asm volatile("" ::"v"(v));
+        }
+#endif
     }
     const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
     // v_rcp_f32: within 1 ulp of 1/d (the check allows 2, tests/native/leafcull_check.cpp)
@@ -302,6 +340,16 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
     const uint4 *p = (const uint4 *)((const char *)S.fat + node * 32u);
     a = p[0];
     b = p[1];
+#ifdef CR_PAD_FETCH // address-path calibration only: CR_PAD_FETCH extra 16-B loads of the record's line
+    typedef const __attribute__((address_space(1))) cr_v4u g_u4;
+    g_u4 *q = (g_u4 *)p;
+    asm volatile("" : "+v"(q));
+#pragma unroll
+    for (int i = 0; i < CR_PAD_FETCH; i++) {
+        const cr_v4u v = q[i & 1];
+        asm volatile("" ::"v"(v));
+    }
+#endif
 }
 
 // PF: software-pipelined leaf loop (triangle j+1's loads issued before j is
@@ -346,7 +394,7 @@ struct TraceDefaults {
     static constexpr bool UL2 = false;    // a uniform leaf's records two per scalar-load wait
     static constexpr int CULL = 0;        // camera cull boxes: 1 references and leaves, 2 also subtrees
     static constexpr int PLANE = 0;       // plane records of secondary / shadow rays
-    static constexpr int LC = 0;          // leaf cull records (1 per-ray, 2 passing culled leaves, 3 fixed, 4 packed)
+    static constexpr int LC = 0;          // leaf cull records (1 per-ray, 2 passing culled leaves, 3 fixed, 4 packed, 5 compressed)
     static constexpr bool PROF = false;   // phase clock (measurement only)
     static constexpr bool PC = false;     // performed-work counters (measurement only)
     static constexpr bool QUAD = false;   // two-level 16-B node records (quadnodes.hpp) instead of fat ones
@@ -386,6 +434,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
     static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
     static_assert(!QUAD || (BF && SC && !CULL && !PLANE && !TILE && !UL2 && LC != 2 && !FULL), "quad records: lean BF + SC builds");
+    static_assert(LC != 5 || !QUAD, "compressed leaf cull records: indexed by node (fat-record builds)");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -393,6 +442,13 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     // children, 2 for a middle node's child records in QUAD codes)
     auto step = [&](uint2 nd, uint32_t sh = 0) -> uint32_t {
         if (pc) pc->steps++;
+#ifdef CR_PAD_STEP // issue-cost calibration only: CR_PAD_STEP extra VALU per shadow descent step
+        if (C::SHADOW) {
+            uint32_t z = nd.x;
+#pragma unroll
+            for (int i = 0; i < CR_PAD_STEP; i++) asm volatile("v_mov_b32 %0, %0" : "+v"(z));
+        }
+#endif
         if (FULL) {
             c.inner++;
             const bool uni = wave_uniform(T.node);
@@ -590,9 +646,9 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         const uint32_t lcid = QUAD ? first : T.node;
         if (pc && count >= lc_min) {
             pc->masks++;
-            pc_load(pc, SC && wave_uniform(lcid), 16u * (LC >= 4 ? LC_RECP : LC_REC));
+            pc_load(pc, SC && wave_uniform(lcid), 16u * (LC == 5 ? LC_RECC : LC == 4 ? LC_RECP : LC_REC));
         }
-        lmask = count >= lc_min ? leaf_mask<SC, LC == 4 ? (QUAD ? 3 : 2) : (LC == 3 ? 1 : 0)>(S, lcid, count, o, d, T.tmax)
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 5 ? 4 : LC == 4 ? (QUAD ? 3 : 2) : (LC == 3 ? 1 : 0)>(S, lcid, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }

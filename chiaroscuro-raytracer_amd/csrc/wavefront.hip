@@ -1325,6 +1325,11 @@ struct ShadowFatLc : ClosestFatLc { static constexpr bool SHADOW = true; };
 // + the exact short split division by the ray's RN(1/d) in the shadow trace (43; 44 without the leaf cull)
 struct ShadowFatLcFd : ShadowFatLc { static constexpr bool FD = true; };
 struct ShadowFatFd : ShadowFat { static constexpr bool FD = true; };
+// the same with the compressed leaf cull records (48 B per leaf instead of 96: three loads, not six)
+struct ClosestFatLc5 : Fat { static constexpr int LC = 5; };
+struct ShadowFatLc5Fd : ClosestFatLc5 { static constexpr bool SHADOW = true, FD = true; };
+struct ClosestFatLc5Perf : ClosestFatLc5 { static constexpr bool PC = true; };
+struct ShadowFatLc5Perf : ClosestFatLc5Perf { static constexpr bool SHADOW = true; };
 // + two-level 16-B node records (quadnodes.hpp: one dwordx4 per two descent levels instead of the fat
 // records' dwordx4 + dwordx2; 46, 47)
 struct ClosestQuadLc : ClosestFatLc { static constexpr bool QUAD = true; };
@@ -1409,6 +1414,9 @@ static const WfBuild kWf[] = {
     //     VGPRs): 357.5 / 355.3 vs 358.4 / 358.1 ms per pass, nanobox 162.4 vs 163.7 ms (shadow 30.7 -> 29.9)
     {43, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
     {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 0, 2, 1, 0}},
+    // 49: 43 whose secondary closest, shadow and tail traces read the compressed leaf cull records
+    //     (leafcull.hpp LC_RECC: boxes on the scene's 16-bit grid, octahedral axes, half constants)
+    {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 0, 2, 1, 5}},
 #ifdef CR_ALL_VARIANTS
     // 48: 43 whose camera packet loads the near-near grandchild's records ahead (SPEC), issued before the
     //     current node's box test so the next fetch finds them in SGPRs.  Bit-exact; two interleaved
@@ -1476,6 +1484,9 @@ static const WfVariant kWfPerf40 = {wf_trace_packet<8, 2, true, true>, wf_trace<
                                     wf_trace<tc::ShadowFatLcPerf>, 8, 8, 0, 2, 1, 4};
 static const WfVariant kWfPerf42 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatPerf>,
                                     wf_trace<tc::ShadowFatPerf>, 8, 8, 0, 2, 1, 0};
+// ... and build 49 (the compressed leaf cull records: the same work, half the mask bytes)
+static const WfVariant kWfPerf49 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc5Perf>,
+                                    wf_trace<tc::ShadowFatLc5Perf>, 8, 8, 0, 2, 1, 5};
 #ifdef CR_ALL_VARIANTS
 // ... and builds 46 / 47 (the quad-record descent: fewer, smaller node loads, the same steps)
 static const WfVariant kWfPerf46 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestQuadLcPerf>,
@@ -1485,7 +1496,7 @@ static const WfVariant kWfPerf47 = {wf_trace_packet<8, 2, true, true>, wf_trace<
 #endif
 // (43 / 44 count through 40 / 42's instances: their shadow trace's short division does the same work)
 bool wf_perf_available(int variant) {
-    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 ||
+    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 || variant == 49 ||
            (wf_variant_available(variant) && (variant == 46 || variant == 47));
 }
 static const WfVariant &perf_variant(int variant) {
@@ -1494,6 +1505,7 @@ static const WfVariant &perf_variant(int variant) {
     if (variant == 47) return kWfPerf47;
 #endif
     return variant == 18 ? kWfPerf18
+           : variant == 49 ? kWfPerf49
            : (variant == 40 || variant == 43) ? kWfPerf40
            : (variant == 42 || variant == 44) ? kWfPerf42
                                               : kWfPerf26;
@@ -1696,10 +1708,14 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, s, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+        else if (A.perf_counters && v.lc == 5)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+        else if (v.lc == 5)
+            launch_tail_lean<5>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
         else if (v.lc == 4)
             launch_tail_lean<4>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
         else
@@ -1799,10 +1815,14 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+        else if (A.perf_counters && v.lc == 5)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (A.perf_counters)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+        else if (v.lc == 5)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else

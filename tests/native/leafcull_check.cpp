@@ -8,9 +8,9 @@
 // huge triangles, degenerate ones.  Rays have unit directions (normalised as glm does)
 // and start anywhere in the scene box, next to the triangles, on their planes, and aim at
 // points on their edges and vertices (a few ulps off), along grazing directions (d in
-// the plane up to 1e-9 ... 1e-1), with tmax random or a few ulps around the hit distance.
+// the plane up to 1e-9 ... 1e-1), axis-parallel from a vertex's coordinate planes, with tmax random or a few ulps around the hit distance.
 // The kernels compute inv = v_rcp_f32(d) (1 ulp); the check perturbs inv by up to 2 ulp.
-//   leafcull_check <seed> <leaves> [form: 0 per-ray, 1 fixed-pad, 2 packed]   prints "violations N tested M accepted A skipped K"
+//   leafcull_check <seed> <leaves> [form: 0 per-ray, 1 fixed-pad, 2 packed, 3 compressed]   prints "violations N tested M accepted A skipped K"
 #include "leafcull.hpp"
 
 #include <cmath>
@@ -76,6 +76,13 @@ V unit() {
 float ulps(float x, int k) {
     for (int i = 0; i < (k < 0 ? -k : k); i++) x = nextafterf(x, k < 0 ? -INFINITY : INFINITY);
     return x;
+}
+
+// the compressed form's grid jitter: its own generator, so forms 2 and 3 see the same leaves and rays
+uint64_t gs = 0x2545F4914F6CDD1Dull;
+double grid_rnd() {
+    gs = gs * 6364136223846793005ull + 1442695040888963407ull;
+    return (double)(gs >> 11) * 0x1p-53;
 }
 
 struct Tri {
@@ -158,7 +165,7 @@ int main(int argc, char **argv) {
     rs ^= seed * 0x9E3779B97F4A7C15ull;
     for (int i = 0; i < 10; i++) rnd();
     uint64_t viol = 0, tested = 0, accepted = 0, skipped = 0;
-    const int form = argc > 3 ? atoi(argv[3]) : 0; // 1: fixed-pad records (leaf_cull_fixed), 2: packed
+    const int form = argc > 3 ? atoi(argv[3]) : 0; // 1: fixed-pad records (leaf_cull_fixed), 2: packed, 3: compressed
     for (int L = 0; L < leaves; L++) {
         const double scale = pow(10.0, rr(-2, 3.5));
         const std::vector<Tri> t = make_leaf(scale);
@@ -179,7 +186,7 @@ int main(int argc, char **argv) {
         for (int r = 0; r < 400; r++) {
             const Tri &T = t[(size_t)(rnd() * n)];
             V o, d;
-            const int rk = (int)(rnd() * 7);
+            const int rk = (int)(rnd() * 8);
             const V edge_pt = add(T.A, add(muls(T.e1, (float)rnd()), muls(T.e2, (float)(rnd() * 0.2))));
             const V vtx = rnd() < 0.5 ? T.A : add(T.A, rnd() < 0.5 ? T.e1 : T.e2);
             const V nrm = normalize(cross(T.e1, T.e2));
@@ -217,6 +224,16 @@ int main(int argc, char **argv) {
                 d = rnd() < 0.5 ? inpl : normalize(add(inpl, muls(nrm_ok ? nrm : unit(), (float)(rr(-1, 1) * pow(10.0, rr(-12, -5))))));
                 break;
             }
+            case 7: { // axis-parallel (a zero direction component: inv infinite) from a vertex's coordinate planes
+                o = add(target, rv(scale * 2));
+                d = normalize(sub(target, o));
+                const int z = (int)(rnd() * 3);
+                (&d.x)[z] = 0.f;
+                if (rnd() < 0.3) (&d.x)[(z + 1) % 3] = 0.f;
+                d = normalize(d);
+                (&o.x)[z] = (&vtx.x)[z];
+                break;
+            }
             default: // other triangles of the leaf behind / in front
                 o = add(T.A, rv(scale * 2));
                 d = normalize(sub(target, o));
@@ -246,7 +263,21 @@ int main(int argc, char **argv) {
                     }
                 cr::LcFloat4 fr[cr::LC_REC];
                 cr::leaf_cull_fixed(rec, db, smax, fr);
-                if (form == 2) {
+                if (form == 3) { // compressed: the leaf's boxes on a scene grid up to 1000x the leaf's scale wider
+                    cr::LcFloat4 two[2 * cr::LC_REC];
+                    for (int i = 0; i < cr::LC_REC; i++) two[i] = two[cr::LC_REC + i] = fr[i];
+                    const double ext = scale * pow(10.0, grid_rnd() * 6 - 3);
+                    for (int i = 0; i < 3; i++) {
+                        (&two[cr::LC_REC].x)[i] = (float)((&fr[0].x)[i] - ext * grid_rnd());
+                        (&two[cr::LC_REC + 1].x)[i] = (float)((&fr[1].x)[i] + ext * grid_rnd());
+                    }
+                    const uint32_t one = 1u;
+                    std::memcpy(&two[cr::LC_REC + 6].x, &one, 4);
+                    const cr::LcGrid G = cr::lc_grid_make(two, 2, db);
+                    uint32_t w[12];
+                    cr::leaf_cull_compress(rec, fr, n, G, w);
+                    keep = cr::leaf_cull_mask_c(ov, dv, inv, true, tmax, w, n, G);
+                } else if (form == 2) {
                     cr::LcFloat4 pr[cr::LC_RECP];
                     cr::leaf_cull_pack(fr, n, pr);
                     keep = cr::leaf_cull_mask_packed(ov, dv, inv, true, tmax, pr, n);

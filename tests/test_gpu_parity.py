@@ -18,8 +18,9 @@ ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit",
 # the wavefront trace builds of the default compile (wavefront.hip kWf; every measured build
 # compiles with make ALL_VARIANTS=1): the plain reference build 0, 15 (the packet camera
 # trace's fallback), round 2's default 18, 26 (leaf cull records), 40 / 42 (26 / 18 with the exact
-# short division in the camera packet) and the defaults 43 / 44 (40 / 42 with it in the shadow trace)
-TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44]
+# short division in the camera packet), 43 / 44 (40 / 42 with it in the shadow trace) and the default 49
+# (43 with the compressed leaf cull records)
+TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44, 49]
 # builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="46 47" (the
 # two-level quad node records, csrc/quadnodes.hpp; their perf instances too)
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
@@ -183,7 +184,7 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, r
                     p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=layer)
                     g = pair.dev.render(cam, p, None)
                     gc = pair.dev.counters()
-                    assert pair.dev.last_trace_build() in (43, 44)
+                    assert pair.dev.last_trace_build() in (49, 44)
                     o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
                     assert_bitwise(g, o, "cam_fuse %d ctl_ray %d fold %d wf_paths %d layer %d" % (fuse, ctl, fold, paths, layer))
                     assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
@@ -205,7 +206,7 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, fold, r
 def test_wavefront_desc_quorum_bitexact(ca, sponza, nanobox, quorum):
     """desc_quorum q: a wave's descent round stops at a node fetch once at most q / 64 of its lanes still
     descend; those lanes keep their node and interval and descend on next round (64: after every fetch).
-    The lean builds 43 / 44, sorted queues, several layers: the same bits and query counters."""
+    The lean builds 49 / 44, sorted queues, several layers: the same bits and query counters."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("desc_quorum", quorum)
@@ -219,7 +220,7 @@ def test_wavefront_desc_quorum_bitexact(ca, sponza, nanobox, quorum):
                 p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=layer)
                 g = pair.dev.render(cam, p, None)
                 gc = pair.dev.counters()
-                assert pair.dev.last_trace_build() in (43, 44)
+                assert pair.dev.last_trace_build() in (49, 44)
                 o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
                 assert_bitwise(g, o, "desc_quorum %d layer %d" % (quorum, layer))
                 assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
@@ -837,7 +838,7 @@ def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
     assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2
 
 
-@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44] + [b for b in TRACE_BUILDS if b in (46, 47)])
+@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44, 49] + [b for b in TRACE_BUILDS if b in (46, 47)])
 @pytest.mark.parametrize("tail_min", [0, 3000])
 def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
     """The performed-work builds (option perf_counters: builds 18 / 26 / 40 / 42 with counters, cr_get_perf)
@@ -903,7 +904,7 @@ def test_perf_counters_default_build_only(ca, cornell):
 
 
 def test_default_build_by_scene_size(ca, sponza, nanobox):
-    """The default trace build culls leaves (43) on the 261k-triangle sponza stand-in and not (44)
+    """The default trace build culls leaves (49) on the 261k-triangle sponza stand-in and not (44)
     on the 20k-triangle nanobox stand-in (cabi.cpp LEAF_CULL_MIN_TRIS): seen through the
     performed-work counts of the default build."""
     masks = {}
@@ -925,7 +926,7 @@ def test_default_build_by_scene_size(ca, sponza, nanobox):
         builds.append(pair.dev.last_trace_build())
         masks[name] = perf["shadow"]["masks"] + perf["closest"]["masks"] + perf["tail"]["masks"]
         # cr_last_trace_build names it: perf and lean renders the scene-size default, counting -1
-        want = 43 if name == "sponza" else 44
+        want = 49 if name == "sponza" else 44
         assert builds == [want, want, -1], (name, builds)
     assert masks["sponza"] > 0 and masks["nanobox"] == 0, masks
 

@@ -30,8 +30,8 @@ def _build(tmp_path, header_dir):
     return exe
 
 
-def _run(exe, seed, leaves):
-    r = subprocess.run([str(exe), str(seed), str(leaves)], capture_output=True, text=True, timeout=600)
+def _run(exe, seed, leaves, form=0):
+    r = subprocess.run([str(exe), str(seed), str(leaves), str(form)], capture_output=True, text=True, timeout=600)
     m = re.search(r"violations (\d+) tested (\d+) accepted (\d+) skipped (\d+)", r.stdout)
     assert m, r.stdout + r.stderr
     return [int(v) for v in m.groups()]
@@ -57,3 +57,30 @@ def test_margins_are_needed(tmp_path):
     exe = _build(tmp_path, tmp_path / "hdr")
     viol = _run(exe, 3, 6000)[0]
     assert viol > 100
+
+
+@pytest.mark.parametrize("form", [2, 3])
+def test_packed_and_compressed_records_are_conservative(tmp_path, form):
+    """The records the kernels read: packed (LC 4, builds 26 / 40 / 43) and compressed (LC 5, build 49:
+    boxes on a 16-bit scene grid up to 1000x wider than the leaf, octahedral axis with kappa recomputed
+    for it, half constants).  No accepted test dropped; the compressed form skips nearly as much."""
+    exe = _build(tmp_path, HDR.parent)
+    viol, tested, accepted, skipped = _run(exe, 4, 6000, form)
+    assert viol == 0 and tested > 30_000_000 and accepted > 500_000
+    if form == 3:
+        skipped_packed = _run(exe, 4, 6000, 2)[3]
+        assert skipped >= 0.95 * skipped_packed
+
+
+def test_compressed_record_margins_are_needed(tmp_path):
+    """With the grid box rounded inward instead of outward, the compressed records drop accepted
+    tests: the checker sees it.  (The quantised axis's move, ~3e-5 rad, sits far inside the half
+    rounding of kappa, so leaving its widening out is not visible to this check.)"""
+    src = HDR.read_text()
+    old = "while (ql > 0.0 && b + ql * st > lo) ql -= 1.0;"
+    src = src.replace(old, "ql += 2.0;").replace("ok = b + ql * st <= lo && b + qh * st >= hi;", "ok = true;")
+    assert old in HDR.read_text() and old not in src
+    (tmp_path / "hdr").mkdir()
+    (tmp_path / "hdr" / "leafcull.hpp").write_text(src)
+    exe = _build(tmp_path, tmp_path / "hdr")
+    assert _run(exe, 5, 6000, 3)[0] > 0
