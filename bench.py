@@ -117,8 +117,9 @@ def cpu_baseline(osc, cam, xres, yres, spp, k, seed, budget_s):
     sample = "%d of %d rows (every %d-th) x %d px x %d spp, %d rays" % (nr, yres, ystep, xres, s_spp, rays)
     return {"value": round(v_all, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
             "build": "oracle/liboracle_lean.so: oracle.c at the reference's -O3 (Makefile:5), -ffp-contract=off, "
-                     "the checker's work counters compiled out of the traversal (OR_LEAN); the same bits as the "
-                     "counting liboracle.so that checks the parity rows",
+                     "the checker's work counters compiled out of the traversal (OR_LEAN), libm sinf / cosf as the "
+                     "reference's std::sin / std::cos (brdf.cpp:53); the same bits as the counting liboracle.so "
+                     "that checks the parity rows",
             "value_1t": round(v_1t, 4), "threads_all": threads, "physical_cores": phys,
             "parallel_efficiency": round(v_all / (v_1t * threads), 3) if v_1t > 0 else None,
             # linear in cores from the 1-thread rate: an upper bound for the whole host (the pool

@@ -90,8 +90,14 @@ static inline uint32_t rng_index(rng_t *r, uint32_t n) {
  * cosine polynomial, which is exact).  The kernels run the same op sequence
  * (csrc/device_math.hpp cr_sincosf).  or_sincos_check sweeps it against the
  * host libm: equal on every float with |x| < 120 (2.25e9 values).
- * or_set_trig_mode(1) calls libm sinf / cosf instead. */
+ * or_set_trig_mode(1) calls libm sinf / cosf instead -- what the reference's std::sin / std::cos do
+ * (brdf.cpp:53); the restatement's fma() is a software call without -mfma, so the timed CPU baseline
+ * (OR_LEAN) starts in mode 1: the same bits (or_sincos_check), 2.70 -> 3.20 Mray/s on one thread (C1). */
+#ifdef OR_LEAN
+static int g_trig_mode = 1;
+#else
 static int g_trig_mode = 0;
+#endif
 void or_set_trig_mode(int mode) { g_trig_mode = mode; }
 static uint32_t abstop12(float x) { uint32_t u; memcpy(&u, &x, 4); return (u >> 20) & 0x7ffu; }
 static const double GS_HPI_INV = 0x1.45f306dc9c883p+23, GS_HPI = 0x1.921fb54442d18p+0;

@@ -129,8 +129,9 @@ def test_preview_camera_matches_reference(ca):
 
 def test_lean_oracle_is_the_same_render(po, ca):
     """bench.py's timed cpu_baseline leg runs liboracle_lean.so (oracle.c at -O3, the hot recursion's work
-    counters compiled out): its pixels are the counting liboracle.so's bit for bit, and its query and path
-    counts -- the baseline's ray count -- are the same; the hot counters read 0."""
+    counters compiled out, libm sinf / cosf as the reference calls them): its pixels are the counting
+    liboracle.so's bit for bit (which restates glibc's sinf / cosf), and its query and path counts -- the
+    baseline's ray count -- are the same; the hot counters read 0."""
     from chiaroscuro_amd import scenes
     sc = ca.Scene(scenes.config_rtc("cornell"), "xres", "48", "yres", "40")
     i = sc.info
