@@ -702,13 +702,26 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
                            (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u,
                            (cr::LcFloat4 *)(lcullp.data() + (size_t)cr::LC_RECP * i));
     // ... and compressed on the scene's grid (48 B per node, LC 5)
-    const cr::LcGrid lcg = cr::lc_grid_make((const cr::LcFloat4 *)lcullf.data(), NN, lc_db);
+    cr::LcGrid lcg = cr::lc_grid_make((const cr::LcFloat4 *)lcullf.data(), NN, lc_db);
+    cr::lc_grid_dt(lcg, (const cr::LcFloat4 *)lcullf.data(), NN);
     std::vector<uint4> lcullc((size_t)cr::LC_RECC * NN, make_uint4(0u, 0u, 0u, 0u));
     for (uint32_t i = 0; i < NN; i++)
         cr::leaf_cull_compress((const cr::LcFloat4 *)(lcull.data() + (size_t)cr::LC_REC * i),
                                (const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
                                (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u, lcg,
                                (uint32_t *)(lcullc.data() + (size_t)cr::LC_RECC * i));
+    // ... and in 32 B per node (LC 6, build 51 of make ALL_VARIANTS=1: the same grid and boxes, the cone and
+    // dt constants in 13 bits a group)
+#ifdef CR_ALL_VARIANTS
+    std::vector<uint4> lculls((size_t)cr::LC_RECS * NN, make_uint4(0u, 0u, 0u, 0u));
+#else
+    std::vector<uint4> lculls;
+#endif
+    for (uint32_t i = 0; i < (uint32_t)(lculls.size() / cr::LC_RECS); i++)
+        cr::leaf_cull_compress_s((const cr::LcFloat4 *)(lcull.data() + (size_t)cr::LC_REC * i),
+                                 (const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
+                                 (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u, lcg,
+                                 (uint32_t *)(lculls.data() + (size_t)cr::LC_RECS * i));
     // two-level node records (quadnodes.hpp) and the packed cull records by first reference, for trace builds
     // 46 / 47 (make ALL_VARIANTS=1: measured slower, wavefront.hip kWf); a scene whose leaves do not fit the
     // records' words, or whose per-reference cull table would pass 4 GiB, keeps the fat-record builds only
@@ -810,7 +823,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         free_scene(c);
         return rc;
     }
-    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, lcullf, &c->S.lcullf)) || (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, lcullc, &c->S.lcullc)) || (rc = upload(c, tri, &c->S.tri)) ||
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, lcullf, &c->S.lcullf)) || (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, lcullc, &c->S.lcullc)) || (rc = upload(c, lculls, &c->S.lculls)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
         (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels)) ||

@@ -96,6 +96,7 @@ struct DevScene {
     const float4 *lcullf; // the same records in the fixed-pad form (leaf_cull_fixed, trace builds with LC 3)
     const float4 *lcullp; // ... packed (LC_RECP float4 per node, leaf_cull_pack, LC 4)
     const uint4 *lcullc;  // ... compressed (LC_RECC uint4 per node on grid lcg, leaf_cull_compress, LC 5)
+    const uint4 *lculls;  // ... short compressed (LC_RECS uint4 per node on grid lcg, leaf_cull_compress_s, LC 6)
     LcGrid lcg;
     // two-level node records (quadnodes.hpp: {w_n, w_c0, w_c1, meta} per slot; null when the scene's
     // leaves do not fit their words) and the packed leaf cull records indexed by a leaf's FIRST

@@ -179,6 +179,7 @@ enum { LC_RECC = 3 };
 struct LcGrid {
     float base[3], step[3], tk;
     float pad; // (host: the margin every box got past its fixed-pad bounds)
+    float dt0; // the short records' dt unit (LC_RECS: dt = dt0 2^e; lc_grid_dt)
 };
 // an IEEE half (low 16 bits of h) as float: exact
 CR_LC_HD inline float lc_half(uint32_t h) {
@@ -234,6 +235,75 @@ CR_LC_HD inline uint32_t leaf_cull_mask_c(const float o[3], const float d[3], co
         if (m0 && lc_group_skip_c(d, inv, bo, tmax, w, w[3], w[4], dt0, G)) drop |= m0;
         if (m1 && lc_group_skip_c(d, inv, bo, tmax, w + 6, w[9], w[10], dt1, G)) drop |= m1;
     }
+    return all & ~drop;
+}
+
+// Short compressed records (LC_RECS uint4 = 32 B per node, leaves of up to 16 references): the
+// compressed record in two 16-B loads, or one 32-B scalar load -- the secondary and shadow traces'
+// cost follows their load instructions.  Eight words:
+//   {box0 x, y, z} {box1 x, y, z}                        as LC_RECC's (lo | hi << 16 on grid G)
+//   {ax0.p | ax0.q << 7 | ax1.p << 14 | ax1.q << 21 | e0 << 28}
+//   {mask0 | kappa0 << 16 | kappa1 << 22 | e1 << 28}
+// Group 0 is mask0's references, group 1 the leaf's others (a leaf whose references include ones
+// tested always puts them in group 1, and never skips it).  Axis k: the normal LINE's octahedral
+// coordinates on the upper hemisphere, x = RN(fma(p, RN(1/63), -1)), y the same of q, z =
+// RN(RN(1 - |x|) - |y|) -- any vector: kappa is computed for the decoded one; kappa = RN(c RN(1/62))
+// (c = 63 with the axis (0, 0, 1) is above any |d.v|: never skipped); dt = G.dt0 2^e.  Every field only enlarges a bound of
+// the fixed-pad record, so the skip stays exact (tests/native/leafcull_check.cpp, form 4).
+enum { LC_RECS = 2 };
+CR_LC_HD inline float lc_axis_s(uint32_t c) { return fmaf((float)c, 1.f / 63.f, -1.f); }
+CR_LC_HD inline float lc_kappa_s(uint32_t c) { return (float)c * (1.f / 62.f); }
+// the slab part of lc_group_skip_c for the segment [t_lo, t_hi]
+template <bool FINITE>
+CR_LC_HD inline bool lc_slab_skip(const float inv[3], const float bo[3], const uint32_t box[3], float t_lo, float t_hi,
+                                  const LcGrid &G) {
+    const float u = 0x1p-24f;
+    float tn = -INFINITY, tf = INFINITY;
+    for (int i = 0; i < 3; i++) {
+        const float t0 = fmaf((float)(box[i] & 0xffffu), G.step[i], bo[i]) * inv[i];
+        const float t1 = fmaf((float)(box[i] >> 16), G.step[i], bo[i]) * inv[i];
+        if (FINITE) {
+            tn = i ? fmaxf(tn, fminf(t0, t1)) : fminf(t0, t1);
+            tf = i ? fminf(tf, fmaxf(t0, t1)) : fmaxf(t0, t1);
+        } else {
+            const bool nan = !(t0 == t0) || !(t1 == t1);
+            const float a = nan ? -INFINITY : (t0 < t1 ? t0 : t1), b = nan ? INFINITY : (t0 < t1 ? t1 : t0);
+            tn = a > tn ? a : tn;
+            tf = b < tf ? b : tf;
+        }
+    }
+    tn = fmaf(-4.f * u, fabsf(tn), tn);
+    tf = fmaf(4.f * u, fabsf(tf), tf);
+    return (tn > tf) | (tn > t_hi) | (tf < t_lo);
+}
+template <bool FINITE>
+CR_LC_HD inline uint32_t leaf_cull_drop_s(const float d[3], const float inv[3], const float bo[3], float th,
+                                          const uint32_t w[8], uint32_t m0, uint32_t m1, const LcGrid &G) {
+    uint32_t drop = 0u;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t m = k ? m1 : m0;
+        if (!m) continue;
+        const uint32_t a = w[6] >> (14 * k);
+        const float x = lc_axis_s(a & 127u), y = lc_axis_s((a >> 7) & 127u);
+        const float z = (1.f - fabsf(x)) - fabsf(y);
+        const float dn = fabsf((d[0] * x + d[1] * y) + d[2] * z);
+        if (!(dn >= lc_kappa_s((w[7] >> (16 + 6 * k)) & 63u))) continue; // possibly grazing (or NaN)
+        const float dt = ldexpf(G.dt0, (int)(w[6 + k] >> 28));
+        if (lc_slab_skip<FINITE>(inv, bo, w + 3 * k, -dt, th + dt, G)) drop |= m;
+    }
+    return drop;
+}
+CR_LC_HD inline uint32_t leaf_cull_mask_s(const float o[3], const float d[3], const float inv[3], bool unit, float tmax,
+                                          const uint32_t w[8], uint32_t count, const LcGrid &G) {
+    const uint32_t all = count >= 32 ? 0xffffffffu : ((1u << count) - 1u);
+    if (!unit || count > (uint32_t)LC_MAXREFS_P) return all;
+    const uint32_t m0 = w[7] & 0xffffu & all, m1 = all & ~m0;
+    const float bo[3] = {G.base[0] - o[0], G.base[1] - o[1], G.base[2] - o[2]};
+    const float th = (tmax * G.tk) * (1.f + 2.f * 0x1p-24f);
+    const uint32_t drop = fabsf(inv[0]) < INFINITY && fabsf(inv[1]) < INFINITY && fabsf(inv[2]) < INFINITY
+                              ? leaf_cull_drop_s<true>(d, inv, bo, th, w, m0, m1, G)
+                              : leaf_cull_drop_s<false>(d, inv, bo, th, w, m0, m1, G);
     return all & ~drop;
 }
 
@@ -530,6 +600,21 @@ inline LcGrid lc_grid_make(const LcFloat4 *fx, size_t n, double db) {
     G.tk = tk;
     return G;
 }
+// Host: group k's fixed-pad box (fx) on grid G, outward past `pad` (base + q step exact in double:
+// q < 2^16): three words lo | hi << 16; false when it leaves the grid
+inline bool lc_grid_box(const LcFloat4 fx[LC_REC], int k, const LcGrid &G, double pad, uint32_t bw[3]) {
+    for (int i = 0; i < 3; i++) {
+        const double lo = (double)(&fx[3 * k].x)[i] - pad, hi = (double)(&fx[3 * k + 1].x)[i] + pad;
+        const double b = G.base[i], st = G.step[i];
+        double ql = floor((lo - b) / st), qh = ceil((hi - b) / st);
+        if (!(ql >= 0.0) || !(qh <= 65535.0)) return false;
+        while (ql > 0.0 && b + ql * st > lo) ql -= 1.0;
+        while (qh < 65535.0 && b + qh * st < hi) qh += 1.0;
+        if (!(b + ql * st <= lo && b + qh * st >= hi)) return false;
+        bw[i] = (uint32_t)ql | (uint32_t)qh << 16;
+    }
+    return true;
+}
 // Host: the fixed-pad record of a node (fx, leaf_cull_fixed of `in`) compressed to twelve words on
 // grid G (its boxes G.pad past the fixed ones); count: the leaf's references (above LC_MAXREFS_P: every
 // one tested always).  A group whose box leaves the grid, or that the fixed record never skips, gets
@@ -565,23 +650,8 @@ inline void leaf_cull_compress(const LcFloat4 in[LC_REC], const LcFloat4 fx[LC_R
         const double th = acos(fmin(1.0, fmax(0.0, (double)in[3 * k + 2].w))) + acos(cd) + 1e-9;
         const double room = acos(c0) - th, g = in[3 * k].w;
         if (!(room > 1e-6 && c0 > 20.2 * u * g && g < 1e20) || !(fx[3 * k + 2].w <= G.tk)) continue;
-        // the box on the grid, outward past the pad (base + q step exact in double: q < 2^16)
-        bool ok = true;
         uint32_t bw[3];
-        for (int i = 0; i < 3 && ok; i++) {
-            const double lo = (double)(&fx[3 * k].x)[i] - pad, hi = (double)(&fx[3 * k + 1].x)[i] + pad;
-            const double b = G.base[i], st = G.step[i];
-            double ql = floor((lo - b) / st), qh = ceil((hi - b) / st);
-            if (!(ql >= 0.0) || !(qh <= 65535.0)) {
-                ok = false;
-                break;
-            }
-            while (ql > 0.0 && b + ql * st > lo) ql -= 1.0;
-            while (qh < 65535.0 && b + qh * st < hi) qh += 1.0;
-            ok = b + ql * st <= lo && b + qh * st >= hi;
-            bw[i] = (uint32_t)ql | (uint32_t)qh << 16;
-        }
-        if (!ok) continue;
+        if (!lc_grid_box(fx, k, G, pad, bw)) continue;
         // dn >= (K + 3.01u)(1 + 8u)|v|  =>  |d^.v^| >= K (|d| <= 1 + 8u, the float dot's rounding)
         const uint32_t hk = lc_half_up((cos(room) + 1e-12 + 3.01 * u) * (1 + 8 * u) * vn * (1 + 1e-9));
         for (int i = 0; i < 3; i++) box[i] = bw[i];
@@ -591,6 +661,82 @@ inline void leaf_cull_compress(const LcFloat4 in[LC_REC], const LcFloat4 fx[LC_R
     }
     w[5] = hd[0] | hd[1] << 16;
     w[11] = (m[0] & 0xffffu) | (m[1] & 0xffffu) << 16;
+}
+
+// Host: G.dt0 for the short records -- the smallest dt of a group with references (fx: LC_REC float4
+// per node, n nodes); 1 when there is none
+inline void lc_grid_dt(LcGrid &G, const LcFloat4 *fx, size_t n) {
+    float m = INFINITY;
+    for (size_t i = 0; i < n; i++) {
+        const LcFloat4 *r = fx + (size_t)LC_REC * i;
+        uint32_t mk[2];
+        __builtin_memcpy(&mk[0], &r[6].x, 4);
+        __builtin_memcpy(&mk[1], &r[6].y, 4);
+        for (int k = 0; k < 2; k++)
+            if (mk[k] && r[3 * k + 1].w > 0.f) m = fminf(m, r[3 * k + 1].w);
+    }
+    G.dt0 = m < 1e30f ? m : 1.f;
+}
+// Host: the fixed-pad record of a node compressed to the eight words of LC_RECS on grid G (G.dt0 set
+// by lc_grid_dt); count above LC_MAXREFS_P: every reference tested (both groups never skipped).
+inline void leaf_cull_compress_s(const LcFloat4 in[LC_REC], const LcFloat4 fx[LC_REC], uint32_t count, const LcGrid &G,
+                                 uint32_t w[8]) {
+    for (int i = 0; i < 8; i++) w[i] = 0u;
+    uint32_t m[3];
+    __builtin_memcpy(&m[0], &fx[6].x, 4);
+    __builtin_memcpy(&m[1], &fx[6].y, 4);
+    __builtin_memcpy(&m[2], &fx[6].z, 4);
+    // a group never skipped: kappa code 63 with the axis (0, 0, 1), so |d.v| <= |d| < 63 / 62
+    const uint32_t pole = 63u | 63u << 7;
+    uint32_t kc[2] = {63u, 63u}, ec[2] = {0u, 0u}, ac[2] = {pole, pole};
+    if (count > (uint32_t)LC_MAXREFS_P || count == 0) {
+        w[6] = ac[0] | ac[1] << 14;
+        w[7] = kc[0] << 16 | kc[1] << 22;
+        return;
+    }
+    const uint32_t all = (1u << count) - 1u;
+    // slot 0: a group of the record; slot 1: the rest.  With references tested always, slot 1 holds
+    // them and is never skipped, so slot 0 gets the group with more references
+    int src[2] = {0, 1};
+    const bool always = (m[2] & all) != 0u;
+    if (always && __builtin_popcount(m[1]) > __builtin_popcount(m[0])) src[0] = 1, src[1] = 0;
+    const uint32_t mask0 = m[src[0]] & all;
+    const double u = 0x1p-24, c0 = 1.0 / LC_C0_INV;
+    for (int s = 0; s < 2; s++) {
+        const int k = src[s];
+        if (s == 1 && always) break;
+        if (!m[k]) continue;
+        if (!lc_grid_box(fx, k, G, G.pad, w + 3 * s)) continue;
+        // the axis line on the upper hemisphere, octahedral, and the cone around the decoded vector
+        double a[3] = {in[3 * k + 2].x, in[3 * k + 2].y, in[3 * k + 2].z};
+        const double an = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        if (!(an > 0)) continue;
+        if (a[2] < 0) a[0] = -a[0], a[1] = -a[1], a[2] = -a[2];
+        const double l1 = fabs(a[0]) + fabs(a[1]) + fabs(a[2]);
+        const double pq[2] = {fmin(126.0, fmax(0.0, nearbyint((a[0] / l1 + 1.0) * 63.0))),
+                              fmin(126.0, fmax(0.0, nearbyint((a[1] / l1 + 1.0) * 63.0)))};
+        const uint32_t p = (uint32_t)pq[0], q = (uint32_t)pq[1];
+        const float vx = lc_axis_s(p), vy = lc_axis_s(q), vz = (1.f - fabsf(vx)) - fabsf(vy);
+        const double v[3] = {vx, vy, vz};
+        const double vn = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) * (1 + 1e-15);
+        if (!(vn > 0.5)) continue;
+        const double cd = fmin(1.0, fabs(a[0] * v[0] + a[1] * v[1] + a[2] * v[2]) / (an * vn));
+        const double th = acos(fmin(1.0, fmax(0.0, (double)in[3 * k + 2].w))) + acos(cd) + 1e-9;
+        const double room = acos(c0) - th, g = in[3 * k].w;
+        if (!(room > 1e-6 && c0 > 20.2 * u * g && g < 1e20) || !(fx[3 * k + 2].w <= G.tk)) continue;
+        // dn >= (K + 3.01u)(1 + 8u)|v|  =>  |d^.v^| >= K (|d| <= 1 + 8u, the float dot's rounding)
+        const double K = (cos(room) + 1e-12 + 3.01 * u) * (1 + 8 * u) * vn * (1 + 1e-9);
+        uint32_t c = 0;
+        while (c < 63u && !((double)lc_kappa_s(c) >= K)) c++;
+        uint32_t e = 0;
+        while (e < 16u && !((double)ldexpf(G.dt0, (int)e) >= (double)fx[3 * k + 1].w)) e++;
+        if (c >= 63u || e >= 16u) continue;
+        kc[s] = c;
+        ec[s] = e;
+        ac[s] = p | q << 7;
+    }
+    w[6] = ac[0] | ac[1] << 14 | ec[0] << 28;
+    w[7] = (mask0 & 0xffffu) | kc[0] << 16 | kc[1] << 22 | ec[1] << 28;
 }
 
 } // namespace cr

@@ -255,8 +255,31 @@ __device__ __forceinline__ void sload_lcullc(const uint4 *p, uint32_t (&w)[12]) 
 #pragma unroll
     for (int i = 0; i < 4; i++) w[8 + i] = b[i];
 }
+// FORM 5: the short compressed records (S.lculls, 32 B: two 16-B loads, or one scalar load)
+__device__ __forceinline__ void sload_lculls(const uint4 *p, uint32_t (&w)[8]) {
+    cr_v8u a;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = a[i];
+}
 template <bool SC, int FORM = 0>
 __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
+    if (FORM == 5) {
+        uint32_t w[8];
+        if (SC && wave_uniform(node)) {
+            sload_lculls(S.lculls + (size_t)LC_RECS * __builtin_amdgcn_readfirstlane(node), w);
+        } else {
+            const uint4 *p = (const uint4 *)((const char *)S.lculls + node * (uint32_t)(16 * LC_RECS));
+#pragma unroll
+            for (int i = 0; i < LC_RECS; i++) {
+                const uint4 v = p[i];
+                w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
+            }
+        }
+        const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
+        const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
+        return leaf_cull_mask_s(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, w, count, S.lcg);
+    }
     if (FORM == 4) {
         uint32_t w[12];
         if (SC && wave_uniform(node)) {
@@ -394,7 +417,7 @@ struct TraceDefaults {
     static constexpr bool UL2 = false;    // a uniform leaf's records two per scalar-load wait
     static constexpr int CULL = 0;        // camera cull boxes: 1 references and leaves, 2 also subtrees
     static constexpr int PLANE = 0;       // plane records of secondary / shadow rays
-    static constexpr int LC = 0;          // leaf cull records (1 per-ray, 2 passing culled leaves, 3 fixed, 4 packed, 5 compressed)
+    static constexpr int LC = 0;          // leaf cull records (1 per-ray, 2 passing culled leaves, 3 fixed, 4 packed, 5 compressed, 6 short)
     static constexpr bool PROF = false;   // phase clock (measurement only)
     static constexpr bool PC = false;     // performed-work counters (measurement only)
     static constexpr bool QUAD = false;   // two-level 16-B node records (quadnodes.hpp) instead of fat ones
@@ -434,7 +457,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
     static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
     static_assert(!QUAD || (BF && SC && !CULL && !PLANE && !TILE && !UL2 && LC != 2 && !FULL), "quad records: lean BF + SC builds");
-    static_assert(LC != 5 || !QUAD, "compressed leaf cull records: indexed by node (fat-record builds)");
+    static_assert(LC < 5 || !QUAD, "compressed leaf cull records: indexed by node (fat-record builds)");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -646,9 +669,9 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         const uint32_t lcid = QUAD ? first : T.node;
         if (pc && count >= lc_min) {
             pc->masks++;
-            pc_load(pc, SC && wave_uniform(lcid), 16u * (LC == 5 ? LC_RECC : LC == 4 ? LC_RECP : LC_REC));
+            pc_load(pc, SC && wave_uniform(lcid), 16u * (LC == 6 ? LC_RECS : LC == 5 ? LC_RECC : LC == 4 ? LC_RECP : LC_REC));
         }
-        lmask = count >= lc_min ? leaf_mask<SC, LC == 5 ? 4 : LC == 4 ? (QUAD ? 3 : 2) : (LC == 3 ? 1 : 0)>(S, lcid, count, o, d, T.tmax)
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 6 ? 5 : LC == 5 ? 4 : LC == 4 ? (QUAD ? 3 : 2) : (LC == 3 ? 1 : 0)>(S, lcid, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }

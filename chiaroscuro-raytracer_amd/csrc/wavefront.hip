@@ -1330,6 +1330,11 @@ struct ClosestFatLc5 : Fat { static constexpr int LC = 5; };
 struct ShadowFatLc5Fd : ClosestFatLc5 { static constexpr bool SHADOW = true, FD = true; };
 struct ClosestFatLc5Perf : ClosestFatLc5 { static constexpr bool PC = true; };
 struct ShadowFatLc5Perf : ClosestFatLc5Perf { static constexpr bool SHADOW = true; };
+// ... and with the short compressed records (32 B per leaf: two loads, or one scalar load)
+struct ClosestFatLc6 : Fat { static constexpr int LC = 6; };
+struct ShadowFatLc6Fd : ClosestFatLc6 { static constexpr bool SHADOW = true, FD = true; };
+struct ClosestFatLc6Perf : ClosestFatLc6 { static constexpr bool PC = true; };
+struct ShadowFatLc6Perf : ClosestFatLc6Perf { static constexpr bool SHADOW = true; };
 // + two-level 16-B node records (quadnodes.hpp: one dwordx4 per two descent levels instead of the fat
 // records' dwordx4 + dwordx2; 46, 47)
 struct ClosestQuadLc : ClosestFatLc { static constexpr bool QUAD = true; };
@@ -1418,6 +1423,13 @@ static const WfBuild kWf[] = {
     //     (leafcull.hpp LC_RECC: boxes on the scene's 16-bit grid, octahedral axes, half constants)
     {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 0, 2, 1, 5}},
 #ifdef CR_ALL_VARIANTS
+    // 51: 49 with the short compressed records (leafcull.hpp LC_RECS: 32 B per leaf, the boxes of 49, each
+    //     group's octahedral axis, kappa and dt in 13 bits: two loads per leaf record instead of three, one
+    //     scalar load for a uniform leaf).  Bit-exact; two interleaved rounds at the driver's command: 2266.4 /
+    //     2261.0 (49) vs 2257.0 / 2255.1 Mray/s, shadow 39.8 / 40.0 -> 40.1 / 40.2 ms per launch -- the coarser
+    //     cones and constants leave 4.9% more triangle tests per shadow launch (2.924 -> 3.068 G), which cost
+    //     what the leaf records' third load did
+    {51, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc6>, wf_trace<tc::ShadowFatLc6Fd>, 8, 8, 0, 2, 1, 6}},
     // 48: 43 whose camera packet loads the near-near grandchild's records ahead (SPEC), issued before the
     //     current node's box test so the next fetch finds them in SGPRs.  Bit-exact; two interleaved
     //     rounds at the driver's command 2187.0 / 2191.7 (43) vs 2114.9 / 2114.3 Mray/s: camera trace
@@ -1488,6 +1500,9 @@ static const WfVariant kWfPerf42 = {wf_trace_packet<8, 2, true, true>, wf_trace<
 static const WfVariant kWfPerf49 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc5Perf>,
                                     wf_trace<tc::ShadowFatLc5Perf>, 8, 8, 0, 2, 1, 5};
 #ifdef CR_ALL_VARIANTS
+// ... and build 51 (the short leaf cull records)
+static const WfVariant kWfPerf51 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc6Perf>,
+                                    wf_trace<tc::ShadowFatLc6Perf>, 8, 8, 0, 2, 1, 6};
 // ... and builds 46 / 47 (the quad-record descent: fewer, smaller node loads, the same steps)
 static const WfVariant kWfPerf46 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestQuadLcPerf>,
                                     wf_trace<tc::ShadowQuadLcPerf>, 8, 8, 0, 2, 1, 4, 1};
@@ -1497,12 +1512,13 @@ static const WfVariant kWfPerf47 = {wf_trace_packet<8, 2, true, true>, wf_trace<
 // (43 / 44 count through 40 / 42's instances: their shadow trace's short division does the same work)
 bool wf_perf_available(int variant) {
     return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 || variant == 49 ||
-           (wf_variant_available(variant) && (variant == 46 || variant == 47));
+           (wf_variant_available(variant) && (variant == 46 || variant == 47 || variant == 51));
 }
 static const WfVariant &perf_variant(int variant) {
 #ifdef CR_ALL_VARIANTS
     if (variant == 46) return kWfPerf46;
     if (variant == 47) return kWfPerf47;
+    if (variant == 51) return kWfPerf51;
 #endif
     return variant == 18 ? kWfPerf18
            : variant == 49 ? kWfPerf49
@@ -1708,12 +1724,20 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, s, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+#ifdef CR_ALL_VARIANTS
+        else if (A.perf_counters && v.lc == 6)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 6, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+#endif
         else if (A.perf_counters && v.lc == 5)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
+#ifdef CR_ALL_VARIANTS
+        else if (v.lc == 6)
+            launch_tail_lean<6>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
+#endif
         else if (v.lc == 5)
             launch_tail_lean<5>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
         else if (v.lc == 4)
@@ -1815,12 +1839,20 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+#ifdef CR_ALL_VARIANTS
+        else if (A.perf_counters && v.lc == 6)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 6, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+#endif
         else if (A.perf_counters && v.lc == 5)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (A.perf_counters)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+#ifdef CR_ALL_VARIANTS
+        else if (v.lc == 6)
+            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 6>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
+#endif
         else if (v.lc == 5)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (v.lc == 4)

@@ -10,7 +10,7 @@
 // points on their edges and vertices (a few ulps off), along grazing directions (d in
 // the plane up to 1e-9 ... 1e-1), axis-parallel from a vertex's coordinate planes, with tmax random or a few ulps around the hit distance.
 // The kernels compute inv = v_rcp_f32(d) (1 ulp); the check perturbs inv by up to 2 ulp.
-//   leafcull_check <seed> <leaves> [form: 0 per-ray, 1 fixed-pad, 2 packed, 3 compressed]   prints "violations N tested M accepted A skipped K"
+//   leafcull_check <seed> <leaves> [form: 0 per-ray, 1 fixed-pad, 2 packed, 3 compressed, 4 short]   prints "violations N tested M accepted A skipped K"
 #include "leafcull.hpp"
 
 #include <cmath>
@@ -165,7 +165,7 @@ int main(int argc, char **argv) {
     rs ^= seed * 0x9E3779B97F4A7C15ull;
     for (int i = 0; i < 10; i++) rnd();
     uint64_t viol = 0, tested = 0, accepted = 0, skipped = 0;
-    const int form = argc > 3 ? atoi(argv[3]) : 0; // 1: fixed-pad records (leaf_cull_fixed), 2: packed, 3: compressed
+    const int form = argc > 3 ? atoi(argv[3]) : 0; // 1: fixed-pad records (leaf_cull_fixed), 2: packed, 3: compressed, 4: short
     for (int L = 0; L < leaves; L++) {
         const double scale = pow(10.0, rr(-2, 3.5));
         const std::vector<Tri> t = make_leaf(scale);
@@ -263,7 +263,7 @@ int main(int argc, char **argv) {
                     }
                 cr::LcFloat4 fr[cr::LC_REC];
                 cr::leaf_cull_fixed(rec, db, smax, fr);
-                if (form == 3) { // compressed: the leaf's boxes on a scene grid up to 1000x the leaf's scale wider
+                if (form >= 3) { // compressed: the leaf's boxes on a scene grid up to 1000x the leaf's scale wider
                     cr::LcFloat4 two[2 * cr::LC_REC];
                     for (int i = 0; i < cr::LC_REC; i++) two[i] = two[cr::LC_REC + i] = fr[i];
                     const double ext = scale * pow(10.0, grid_rnd() * 6 - 3);
@@ -273,10 +273,17 @@ int main(int argc, char **argv) {
                     }
                     const uint32_t one = 1u;
                     std::memcpy(&two[cr::LC_REC + 6].x, &one, 4);
-                    const cr::LcGrid G = cr::lc_grid_make(two, 2, db);
-                    uint32_t w[12];
-                    cr::leaf_cull_compress(rec, fr, n, G, w);
-                    keep = cr::leaf_cull_mask_c(ov, dv, inv, true, tmax, w, n, G);
+                    cr::LcGrid G = cr::lc_grid_make(two, 2, db);
+                    if (form == 4) { // short: 32 B, the dt unit from the leaf's groups
+                        cr::lc_grid_dt(G, fr, 1);
+                        uint32_t w[8];
+                        cr::leaf_cull_compress_s(rec, fr, n, G, w);
+                        keep = cr::leaf_cull_mask_s(ov, dv, inv, true, tmax, w, n, G);
+                    } else {
+                        uint32_t w[12];
+                        cr::leaf_cull_compress(rec, fr, n, G, w);
+                        keep = cr::leaf_cull_mask_c(ov, dv, inv, true, tmax, w, n, G);
+                    }
                 } else if (form == 2) {
                     cr::LcFloat4 pr[cr::LC_RECP];
                     cr::leaf_cull_pack(fr, n, pr);

@@ -21,8 +21,8 @@ ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit",
 # short division in the camera packet), 43 / 44 (40 / 42 with it in the shadow trace) and the default 49
 # (43 with the compressed leaf cull records)
 TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44, 49]
-# builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="46 47" (the
-# two-level quad node records, csrc/quadnodes.hpp; their perf instances too)
+# builds compiled only with `make ALL_VARIANTS=1`, added for an experiment: CR_TEST_BUILDS="46 47 51" (the
+# two-level quad node records, csrc/quadnodes.hpp; the short leaf cull records; their perf instances too)
 TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
@@ -838,7 +838,7 @@ def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
     assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2
 
 
-@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44, 49] + [b for b in TRACE_BUILDS if b in (46, 47)])
+@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44, 49] + [b for b in TRACE_BUILDS if b in (46, 47, 51)])
 @pytest.mark.parametrize("tail_min", [0, 3000])
 def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
     """The performed-work builds (option perf_counters: builds 18 / 26 / 40 / 42 with counters, cr_get_perf)
