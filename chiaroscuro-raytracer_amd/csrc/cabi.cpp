@@ -267,6 +267,13 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 P = std::max<uint64_t>(std::min<uint64_t>(P, cap), std::min<uint64_t>(P, 1u << 20));
             }
             const size_t f4 = 16 * (size_t)P;
+            // queue-indexed arrays hold qspare more slots: the dead entries of wf_shade's chunked appends
+            // (WfArgs::app_chunk; at most one partial chunk per block and queue)
+            // (option "wf_app_chunk" forces a chunk size: room for it on every block)
+            const uint64_t forced = c->wf_app_chunk ? (uint64_t)cr::wf_shade_blocks(c->num_cus, c->wf_shade_waves) * c->wf_app_chunk : 0;
+            auto spare_for = [&](uint64_t Pn) { return std::max<uint64_t>(std::min<uint64_t>(Pn / 8, 8u << 20), forced); };
+            const uint64_t Q = P + spare_for(P);
+            const size_t fq = 16 * (size_t)Q;
             // queue sorting: by default for scenes of at least SORT_MIN_TRIS triangles only (wf_sort -1)
             const int sort = c->wf_sort >= 0 ? c->wf_sort : (c->n_tris >= SORT_MIN_TRIS ? 1 : 0);
             // queue-sort keys: (pixel sub-tile, octahedral direction bin)
@@ -297,11 +304,13 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             if (leaf_keys) key_bits = leaf_bits;
             // bytes of the buffers of a chunk of Pn paths with kb-bit sort keys
             auto need_for = [&](uint64_t Pn, int kb) -> size_t {
-                const size_t st = sort ? cr::wf_sort_tmp_bytes((uint32_t)Pn, kb, c->wf_sort_lib != 0) : 0;
-                return (4 + 2 + 2 + cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 21 * (size_t)Pn +
-                       (sort ? 32 * (size_t)Pn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
+                const uint64_t Qn = Pn + spare_for(Pn);
+                const size_t st = sort ? cr::wf_sort_tmp_bytes((uint32_t)Qn, kb, c->wf_sort_lib != 0) : 0;
+                return (4 + 2 + 2) * 16 * (size_t)Qn + 8 * (size_t)Qn +
+                       (cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 13 * (size_t)Pn +
+                       (sort ? 32 * (size_t)Qn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
             };
-            const size_t sort_tmp = sort ? cr::wf_sort_tmp_bytes((uint32_t)P, key_bits, c->wf_sort_lib != 0) : 0;
+            const size_t sort_tmp = sort ? cr::wf_sort_tmp_bytes((uint32_t)Q, key_bits, c->wf_sort_lib != 0) : 0;
             const size_t need = need_for(P, key_bits);
             // a chunk of more than a quarter of the path cap reserves the buffers of a whole-cap chunk
             // with the widest keys, so passes of other sizes (a pass group's frame pieces, the next
@@ -321,15 +330,17 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                     b += (bytes + 255) & ~(size_t)255;
                     return r;
                 };
-                W.ray[0] = (float4 *)take(2 * f4);
-                W.ray[1] = (float4 *)take(2 * f4);
-                W.hit[0] = (uint4 *)take(f4);
-                W.hit[1] = (uint4 *)take(f4);
-                W.sray = (float4 *)take(2 * f4);
+                W.ray[0] = (float4 *)take(2 * fq);
+                W.ray[1] = (float4 *)take(2 * fq);
+                W.hit[0] = (uint4 *)take(fq);
+                W.hit[1] = (uint4 *)take(fq);
+                W.sray = (float4 *)take(2 * fq);
                 W.ps = (float4 *)take(cr::WF_STATE * f4);
                 W.dw = (float4 *)take(2 * (size_t)p->k * f4);
-                W.sexcl = (uint32_t *)take(4 * (size_t)P);
-                W.occ = (uint32_t *)take(4 * (size_t)P);
+                W.sexcl = (uint32_t *)take(4 * (size_t)Q);
+                W.occ = (uint32_t *)take(4 * (size_t)Q);
+                W.qspare = (uint32_t)(Q - P);
+                W.app_force = (uint32_t)c->wf_app_chunk;
                 W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
                 W.cxy = (float2 *)take(8 * (size_t)P);
                 W.ended = (uint32_t *)take(4 * (size_t)P);
@@ -364,8 +375,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 if (sort) {
                     for (int q = 0; q < 2; q++)
                         for (int i = 0; i < 2; i++) {
-                            W.key[q][i] = (uint32_t *)take(4 * (size_t)P);
-                            W.perm[q][i] = (uint32_t *)take(4 * (size_t)P);
+                            W.key[q][i] = (uint32_t *)take(4 * (size_t)Q);
+                            W.perm[q][i] = (uint32_t *)take(4 * (size_t)Q);
                         }
                     W.sort_tmp = take(sort_tmp);
                     W.sort_tmp_bytes = sort_tmp;
@@ -1285,6 +1296,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_resolve_paths") && v >= 0 && v <= 64) c->wf_resolve_paths = (uint32_t)v;
     else if (!std::strcmp(key, "wf_fold") && v >= 0 && v <= 2) c->wf_fold = (int)v;
     else if (!std::strcmp(key, "wf_shade_waves") && (v == 6 || v == 8)) c->wf_shade_waves = (int)v;
+    else if (!std::strcmp(key, "wf_app_chunk") && (v == 0 || (v >= 256 && v <= 65536 && !(v & (v - 1))))) c->wf_app_chunk = (int)v;
     else if (!std::strcmp(key, "wf_leaf_shift") && v >= 0 && v <= 24) c->wf_leaf_shift = (uint32_t)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;
     else if (!std::strcmp(key, "sample_buf_bytes") && v >= 1 && v <= (1ll << 40)) c->sample_buf = (uint64_t)v;

@@ -141,6 +141,9 @@ struct cr_ctx {
     // WfArgs::shade_waves (option "wf_shade_waves": 6 or 8); round 4, two interleaved rounds: sponza
     // 322.5 / 322.9 vs 322.6 / 322.2 ms per layer, cornell_box 108.4 / 108.7 vs 107.6 / 107.3 ms per pass
     int wf_shade_waves = 8;
+    // wf_shade's append chunk (WfArgs::app_force): 0 = by the queue's length (launch_wavefront_chunk), else
+    // this power of two >= 256 whenever the queue arrays have room (tests: the dead entries at small sizes)
+    int wf_app_chunk = 0;
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

@@ -267,6 +267,14 @@ struct WfArgs {
     int fold;
     uint32_t *ended;    // [P] paths that ended at the generation being folded
     int shade_waves;    // wf_shade's build: 8 waves per SIMD (64 VGPRs, spills) or else its natural 6
+    // wf_shade's queue appends in chunks (set per launch by launch_wavefront_chunk): a block reserves
+    // app_chunk slots of a queue with one atomic and fills them over its iterations; the unused end of
+    // its last chunk becomes dead entries (ray w = NO_PATH, key ~0) that the consumers skip.  0: one
+    // atomic per block iteration.  Same-address device atomics serialise (~5.7 ns each on MI355X,
+    // scripts/append_bench.hip): the per-iteration form bound wf_shade of a full chunk.
+    uint32_t app_chunk;
+    uint32_t qspare;    // queue slots past P in every queue-indexed array (the dead entries' room; 0: no chunks)
+    uint32_t app_force; // option "wf_app_chunk": this chunk size (>= 256) for every launch that has room (tests)
     // 1: no wf_camera launch -- the packet camera trace derives each path's camera ray from its
     // (pixel, sample) itself, and wf_shade(1) / wf_resolve(1) take path p = ray p and the eye as
     // its origin (set per chunk by launch_wavefront_chunk; option "wf_cam_fuse")
@@ -295,13 +303,16 @@ struct WfArgs {
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position, ended list, resolve mark
-inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4 + 1; }
+// (+ 21: the queue arrays' spare slots, P / 8 of them at 168 B -- cabi.cpp spare_for)
+inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4 + 1 + 21; }
 // Second stream and fork / join events of a render (shadow trace g beside closest trace g + 1).
 struct WfStreams {
     hipStream_t side;
     hipEvent_t fork, join;
 };
 int num_wf_variants();
+// blocks of a wf_shade launch at the ctx's wf_shade_waves (its grid-stride grid)
+uint32_t wf_shade_blocks(int num_cus, int shade_waves);
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
 bool wf_variant_available(int variant); // compiled in (the default compile holds builds 0, 15, 18, 26)

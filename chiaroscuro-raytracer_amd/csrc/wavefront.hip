@@ -105,6 +105,61 @@ __device__ __forceinline__ void block_append_n(uint32_t *const (&counter)[N], co
                   __builtin_amdgcn_mbcnt_hi((uint32_t)(m[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[q], 0u));
 }
 
+// block_append_n with the slots reserved app_chunk at a time (WfArgs::app_chunk): thread 0 keeps each
+// queue's current chunk (cb: its first slot, cu: slots used; cu = C and cb anything before the first) in its
+// registers and reserves a new chunk only when an iteration's appends do not fit the current one; the
+// appends of one call then split at most once, the first `room` of them at the end of the old chunk, the
+// rest at the start of the new one.  lds: [2][4 N + 3 N] words, alternating halves as block_append_n's.
+template <int N>
+__device__ __forceinline__ void block_append_chunk(uint32_t *const (&counter)[N], const bool (&pred)[N], uint32_t *lds,
+                                                   uint32_t buf, uint32_t C, uint32_t (&cb)[N], uint32_t (&cu)[N],
+                                                   uint32_t (&slot)[N]) {
+    uint32_t *L = lds + buf * 7u * N;
+    const uint32_t wave = threadIdx.x >> 6;
+    uint64_t m[N];
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+        m[q] = __ballot(pred[q]);
+        if ((threadIdx.x & 63u) == 0) L[4 * q + wave] = (uint32_t)__popcll(m[q]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot[N], fresh[N];
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+            uint32_t s = 0;
+            for (uint32_t w = 0; w < (blockDim.x >> 6); w++) {
+                const uint32_t c = L[4 * q + w];
+                L[4 * q + w] = s;
+                s += c;
+            }
+            tot[q] = s;
+            fresh[q] = s > C - cu[q] ? atomicAdd(counter[q], C) : 0u; // (all reservations in flight together)
+        }
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+            const uint32_t room = C - cu[q];
+            L[4 * N + 3 * q] = cb[q] + cu[q];
+            L[4 * N + 3 * q + 1] = tot[q] > room ? room : tot[q];
+            L[4 * N + 3 * q + 2] = fresh[q];
+            if (tot[q] > room) {
+                cb[q] = fresh[q];
+                cu[q] = tot[q] - room;
+            } else {
+                cu[q] += tot[q];
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+        const uint32_t i = L[4 * q + wave] +
+                           __builtin_amdgcn_mbcnt_hi((uint32_t)(m[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[q], 0u));
+        const uint32_t room = L[4 * N + 3 * q + 1];
+        slot[q] = i < room ? L[4 * N + 3 * q] + i : L[4 * N + 3 * q + 2] + (i - room);
+    }
+}
+
 __device__ __forceinline__ uint32_t *cnt_closest(const WfArgs &W, uint32_t g) { return W.cnt + g; }
 __device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + WF_G + g; }
 __device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 2 * WF_G + g; }
@@ -365,8 +420,9 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
                             csx = q.x;
                             csy = q.y;
                         }
-                        if (!SHADOW && __float_as_uint(r0.w) == NO_PATH) {
-                            W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u); // dead camera ray: no query
+                        if (__float_as_uint(r0.w) == NO_PATH) {
+                            // a dead camera ray or a dead queue entry (wf_shade's chunked appends): no query
+                            if (!SHADOW) W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u);
                         } else if (iss = true, trav_begin(S, o, d, SHADOW, r1.w, T)) {
                             state = busy_st;
                             if (FULL) diag_begin(&dg);
@@ -594,10 +650,13 @@ __device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
-    __shared__ uint32_t app[5], app2[2 * 5 * 2];
+    __shared__ uint32_t app[5], app2[2 * 7 * 2];
     if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t n = *cnt_closest(W, g);
+    // chunked appends (WfArgs::app_chunk): thread 0's current chunk per queue, none yet
+    const uint32_t C = W.app_chunk;
+    uint32_t cb[2] = {0u, 0u}, cu[2] = {C, C};
     const float4 *rays = W.ray[g & 1];
     const uint4 *hits = W.hit[g & 1];
     float4 *next_rays = W.ray[(g + 1) & 1];
@@ -606,7 +665,13 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
     // fused camera (WfArgs::cam_fused): ray i of generation 1 is path i's, from the eye; no wf_camera
     // cleared its resolve mark or counted it
     const bool fused = g == 1 && W.cam_fused;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x, it++) {
+    // chunked appends: each block takes one contiguous range of the queue (a multiple of the block), so a
+    // chunk holds the outputs of neighbouring rays -- the queue keeps the input's locality (and a sorted
+    // queue its order among equal keys); otherwise the grid-stride sweep
+    const uint32_t span = C ? ((n + gridDim.x - 1) / gridDim.x + blockDim.x - 1) / blockDim.x * blockDim.x : 0u;
+    const uint32_t b0 = C ? blockIdx.x * span : blockIdx.x * blockDim.x;
+    const uint32_t b1 = C ? min(n, b0 + span) : n, bstep = C ? blockDim.x : gridDim.x * blockDim.x;
+    for (uint32_t base = b0; base < b1; base += bstep, it++) {
         const uint32_t i = base + threadIdx.x;
         const bool in = i < n;
         uint4 h = make_uint4(0u, 0u, 0u, 0u);
@@ -639,7 +704,8 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         // shadow queue g and closest queue g + 1 in one barrier round (uniform: the whole block)
         const bool want[2] = {nee, cont};
         uint32_t slots[2];
-        block_append_n<2>(queues, want, app2, it & 1u, slots);
+        if (C) block_append_chunk<2>(queues, want, app2, it & 1u, C, cb, cu, slots);
+        else block_append_n<2>(queues, want, app2, it & 1u, slots);
         const uint32_t j = slots[0], jc = slots[1];
         if (hit) W.dw[(size_t)(2 * (g - 1)) * W.P + p] = pk(direct, nee ? j : NO_SLOT);
         if (nee) {
@@ -670,6 +736,30 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         }
         tally(tl, T_HIT, hit);
         tally(tl, T_TEXHIT, textured);
+    }
+    if (C) { // the unused end of each queue's last chunk: dead entries (no path; sorted last)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            app2[0] = cb[0] + cu[0];
+            app2[1] = cu[0] < C ? C - cu[0] : 0u;
+            app2[2] = cb[1] + cu[1];
+            app2[3] = cu[1] < C ? C - cu[1] : 0u;
+        }
+        __syncthreads();
+        for (uint32_t q = 0; q < 2; q++) {
+            const uint32_t from = app2[2 * q], len = app2[2 * q + 1];
+            float4 *rq = q ? next_rays : W.sray;
+            for (uint32_t k = threadIdx.x; k < len; k += blockDim.x) {
+                const uint32_t j = from + k;
+                rq[2 * (size_t)j] = make_float4(0.f, 0.f, 0.f, __uint_as_float(NO_PATH));
+                rq[2 * (size_t)j + 1] = make_float4(0.f, 0.f, 1.f, 0.f);
+                if (!q) W.sexcl[j] = 0u;
+                if (W.sort) {
+                    W.key[q][0][j] = 0xffffffffu;
+                    if (W.sort_lib) W.perm[q][0][j] = j;
+                }
+            }
+        }
     }
     flush_tallies(A, tl);
 }
@@ -1695,6 +1785,24 @@ static uint32_t shade_grid(int num_cus, int waves) {
     return (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)std::min(b, 8);
 }
 // wf_shade at the ctx's option "wf_shade_waves" (8, the default since round 4; or 6)
+// The append chunk of a wf_shade launch over nin rays (WfArgs::app_chunk): a power of two giving each
+// block about 16 chunks per queue, so the dead entries stay a few percent of the queue; 0 (one atomic
+// per block iteration) for queues that short, and at most what the queues' spare slots hold for every
+// block's partial last chunk.  Only for queues traced in append order (W.sort 0: scenes below
+// SORT_MIN_TRIS): round 5, two interleaved rounds, cornell_box 13,002 / 13,000 -> 14,331 / 14,298 Mray/s;
+// on sorted queues (sponza stand-in) wf_shade gains 9 % but the shadow trace loses 1.7 % -- the chunks
+// change the order among equal keys -- 2278.5 / 2278.7 -> 2274.8 / 2270.4
+static uint32_t shade_app_chunk(const WfArgs &W, uint32_t nin, int num_cus) {
+    if (W.fold || !W.qspare) return 0u;
+    const uint32_t grid = shade_grid(num_cus, W.shade_waves == 8 ? 8 : 6);
+    const uint32_t want = nin / (grid * 16u), cap = W.qspare / grid;
+    if (W.app_force) return W.app_force <= cap ? W.app_force : 0u;
+    if (W.sort) return 0u;
+    uint32_t c = 256u;
+    while (c * 2u <= want && c * 2u <= cap && c < 4096u) c *= 2u;
+    return c <= want && c <= cap ? c : 0u;
+}
+uint32_t wf_shade_blocks(int num_cus, int shade_waves) { return shade_grid(num_cus, shade_waves == 8 ? 8 : 6); }
 static void launch_shade(const RenderArgs &A, const WfArgs &W, uint32_t g, int num_cus, hipStream_t st) {
     if (W.shade_waves == 8)
         hipLaunchKernelGGL(wf_shade<8>, dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
@@ -1765,14 +1873,18 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         return err ? err : (int)hipGetLastError();
     }
     closest(1, st, nullptr, W.gstack); // camera rays: path order is already coherent
+    uint32_t nin = W.P; // rays of closest queue g (generation 1: one per path)
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
+        W.app_chunk = shade_app_chunk(W, nin, num_cus);
         launch_shade(A, W, g, num_cus, st);
+        W.app_chunk = 0u;
         uint32_t cnt[2] = {0u, 0u}; // shadow queue g, closest queue g + 1
         if ((err = (int)hipMemcpyAsync(&cnt[0], W.cnt + WF_G + g, 4, hipMemcpyDeviceToHost, st)) ||
             (err = (int)hipMemcpyAsync(&cnt[1], W.cnt + g + 1, 4, hipMemcpyDeviceToHost, st)) ||
             (err = (int)hipStreamSynchronize(st)))
             break;
         const uint32_t nc = g < (uint32_t)A.K ? cnt[1] : 0u;
+        nin = nc;
         const bool next = nc >= W.tail_min && nc > 0; // closest g + 1 as its own launch, beside shadow g
         const bool pixel = !W.leaf_keys && !(W.world_keys && g >= (uint32_t)W.world_keys); // wf_shade's key choice
         const uint32_t *order_s = (g > 1 || (W.sort_g1 & 1u)) ? order_queue(W, 0, cnt[0], st, err, pixel) : nullptr;

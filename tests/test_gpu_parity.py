@@ -134,6 +134,26 @@ def test_wavefront_resolve_order_bitexact(ca, sponza, nanobox, fold, resolve_pat
             pair.dev.set_option("wf_paths", 256 << 20)
 
 
+@pytest.mark.parametrize("chunk", [256, 1024])
+def test_wavefront_chunked_appends_bitexact(ca, sponza, cornell_mm, chunk):
+    """wf_shade's chunked queue appends (WfArgs::app_chunk; forced here by option wf_app_chunk, at full
+    size they start at 8M rays): a block reserves `chunk` slots of a queue with one atomic and fills them
+    over its iterations, and the unused end of its last chunk becomes dead entries (ray w = NO_PATH, key
+    ~0) that the sort, the traces, wf_resolve and the next wf_shade skip.  128 x 96 x 128 spp puts several
+    iterations on each shade block, so appends straddle chunks.  The same bits and query counters as the
+    oracle, with sorted (sponza) and unsorted (cornell_box) queues, lean and counting builds."""
+    x, y, s = 128, 96, 128
+    for pair in (sponza, cornell_mm):
+        pair.dev.set_option("kernel", 2)
+        pair.dev.set_option("wf_app_chunk", chunk)
+        try:
+            g, gc, o, oc = _render_both(ca, pair, x, y, s)
+        finally:
+            pair.dev.set_option("wf_app_chunk", 0)
+        assert_bitwise(g, o, "wf_app_chunk %d" % chunk)
+        assert {k: gc[k] for k in ORACLE_KEYS} == oc
+
+
 @pytest.mark.parametrize("waves", [6, 8])
 def test_wavefront_shade_waves_bitexact(ca, sponza, nanobox, waves):
     """wf_shade built for 8 waves per SIMD (the default; 64 VGPRs, spills) or its natural 6: the same
