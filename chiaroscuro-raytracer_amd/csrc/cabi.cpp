@@ -174,13 +174,19 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
 // held) when the ctx first asked after its scene upload.  Kept until the next upload: the plan of a pass group (cr_layers_per_group,
 // cr_layers_per_pass) must not change as this ctx's own buffers grow, or ranks that asked at different
 // moments would plan different groups and their per-layer gathers would not pair up
+// wf_shade may append in chunks (WfArgs::app_chunk: the queues traced in append order, or a forced chunk):
+// only then do the queue arrays carry spare slots -- a sorted scene's path cap, and with it the pieces of a
+// pass group, stays what it was
+bool wf_chunked(const cr_ctx *c) {
+    return c->wf_app_chunk || c->wf_sort == 0 || (c->wf_sort < 0 && c->n_tris < SORT_MIN_TRIS);
+}
 uint64_t wf_path_cap(cr_ctx *c, int k) {
     if (!c->wf_mem_budget) {
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) return ~0ull;
         c->wf_mem_budget = freeb + c->wf_bytes + c->wf2_bytes;
     }
-    return (uint64_t)(c->wf_mem_budget * 0.45) / cr::wf_bytes_per_path(k);
+    return (uint64_t)(c->wf_mem_budget * 0.45) / cr::wf_bytes_per_path(k, wf_chunked(c));
 }
 
 int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float *out, int mode, hipStream_t st,
@@ -271,7 +277,10 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             // (WfArgs::app_chunk; at most one partial chunk per block and queue)
             // (option "wf_app_chunk" forces a chunk size: room for it on every block)
             const uint64_t forced = c->wf_app_chunk ? (uint64_t)cr::wf_shade_blocks(c->num_cus, c->wf_shade_waves) * c->wf_app_chunk : 0;
-            auto spare_for = [&](uint64_t Pn) { return std::max<uint64_t>(std::min<uint64_t>(Pn / 8, 8u << 20), forced); };
+            const bool chunked = wf_chunked(c);
+            auto spare_for = [&](uint64_t Pn) {
+                return chunked ? std::max<uint64_t>(std::min<uint64_t>(Pn / 8, 8u << 20), forced) : (uint64_t)0;
+            };
             const uint64_t Q = P + spare_for(P);
             const size_t fq = 16 * (size_t)Q;
             // queue sorting: by default for scenes of at least SORT_MIN_TRIS triangles only (wf_sort -1)

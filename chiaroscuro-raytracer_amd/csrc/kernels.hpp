@@ -303,8 +303,10 @@ struct WfArgs {
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
 // camera sample position, ended list, resolve mark
-// (+ 21: the queue arrays' spare slots, P / 8 of them at 168 B -- cabi.cpp spare_for)
-inline size_t wf_bytes_per_path(int K) { return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4 + 1 + 21; }
+// spare: + 21 for the queue arrays' spare slots of chunked appends, P / 8 of them at 168 B (cabi.cpp spare_for)
+inline size_t wf_bytes_per_path(int K, bool spare) {
+    return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4 + 1 + (spare ? 21 : 0);
+}
 // Second stream and fork / join events of a render (shadow trace g beside closest trace g + 1).
 struct WfStreams {
     hipStream_t side;

@@ -421,6 +421,7 @@ struct TraceDefaults {
     static constexpr bool PROF = false;   // phase clock (measurement only)
     static constexpr bool PC = false;     // performed-work counters (measurement only)
     static constexpr bool QUAD = false;   // two-level 16-B node records (quadnodes.hpp) instead of fat ones
+    static constexpr bool DEAD = false;   // shadow queues with dead entries (wf_shade's chunked appends) skipped
 };
 
 template <class C>

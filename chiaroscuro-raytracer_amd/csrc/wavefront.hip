@@ -420,8 +420,9 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
                             csx = q.x;
                             csy = q.y;
                         }
-                        if (__float_as_uint(r0.w) == NO_PATH) {
-                            // a dead camera ray or a dead queue entry (wf_shade's chunked appends): no query
+                        // a dead camera ray or a dead queue entry (wf_shade's chunked appends): no query -- for
+                        // shadow queues only in the C::DEAD builds (the check costs the others registers)
+                        if ((!SHADOW || C::DEAD) && __float_as_uint(r0.w) == NO_PATH) {
                             if (!SHADOW) W.hit[g & 1][idx] = make_uint4(0u, 0u, 0u, 0u);
                         } else if (iss = true, trav_begin(S, o, d, SHADOW, r1.w, T)) {
                             state = busy_st;
@@ -647,7 +648,9 @@ __device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32
 // background; hits run shade_next and append their NEE ray to shadow queue g and
 // their next ray to closest queue g + 1.
 // MINW: waves per SIMD the build is held to (6: its 75 VGPRs, no spills; 8: 64 VGPRs, the rest spilled)
-template <int MINW>
+// CH: the chunked appends (WfArgs::app_chunk) -- a build of its own, so the per-iteration form keeps its
+// registers
+template <int MINW, bool CH = false>
 __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
     __shared__ uint32_t app[5], app2[2 * 7 * 2];
@@ -655,7 +658,7 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
     __syncthreads();
     const uint32_t n = *cnt_closest(W, g);
     // chunked appends (WfArgs::app_chunk): thread 0's current chunk per queue, none yet
-    const uint32_t C = W.app_chunk;
+    const uint32_t C = CH ? W.app_chunk : 0u;
     uint32_t cb[2] = {0u, 0u}, cu[2] = {C, C};
     const float4 *rays = W.ray[g & 1];
     const uint4 *hits = W.hit[g & 1];
@@ -668,9 +671,9 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
     // chunked appends: each block takes one contiguous range of the queue (a multiple of the block), so a
     // chunk holds the outputs of neighbouring rays -- the queue keeps the input's locality (and a sorted
     // queue its order among equal keys); otherwise the grid-stride sweep
-    const uint32_t span = C ? ((n + gridDim.x - 1) / gridDim.x + blockDim.x - 1) / blockDim.x * blockDim.x : 0u;
-    const uint32_t b0 = C ? blockIdx.x * span : blockIdx.x * blockDim.x;
-    const uint32_t b1 = C ? min(n, b0 + span) : n, bstep = C ? blockDim.x : gridDim.x * blockDim.x;
+    const uint32_t span = CH ? ((n + gridDim.x - 1) / gridDim.x + blockDim.x - 1) / blockDim.x * blockDim.x : 0u;
+    const uint32_t b0 = CH ? blockIdx.x * span : blockIdx.x * blockDim.x;
+    const uint32_t b1 = CH ? min(n, b0 + span) : n, bstep = CH ? blockDim.x : gridDim.x * blockDim.x;
     for (uint32_t base = b0; base < b1; base += bstep, it++) {
         const uint32_t i = base + threadIdx.x;
         const bool in = i < n;
@@ -704,7 +707,7 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         // shadow queue g and closest queue g + 1 in one barrier round (uniform: the whole block)
         const bool want[2] = {nee, cont};
         uint32_t slots[2];
-        if (C) block_append_chunk<2>(queues, want, app2, it & 1u, C, cb, cu, slots);
+        if (CH) block_append_chunk<2>(queues, want, app2, it & 1u, C, cb, cu, slots);
         else block_append_n<2>(queues, want, app2, it & 1u, slots);
         const uint32_t j = slots[0], jc = slots[1];
         if (hit) W.dw[(size_t)(2 * (g - 1)) * W.P + p] = pk(direct, nee ? j : NO_SLOT);
@@ -737,7 +740,7 @@ __global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, ui
         tally(tl, T_HIT, hit);
         tally(tl, T_TEXHIT, textured);
     }
-    if (C) { // the unused end of each queue's last chunk: dead entries (no path; sorted last)
+    if (CH) { // the unused end of each queue's last chunk: dead entries (no path; sorted last)
         __syncthreads();
         if (threadIdx.x == 0) {
             app2[0] = cb[0] + cu[0];
@@ -1395,6 +1398,9 @@ struct WfVariant {
     int packet; // the camera trace is a packet trace (needs a near child common to all camera rays)
     int lc;     // the tail kernel's leaf cull form (trav_round's LC; 0: none)
     int quad = 0; // the secondary / shadow traces read the two-level records (DevScene::quad)
+    // the shadow trace of a queue wf_shade appended in chunks (its dead entries skipped); null: the build's
+    // wf_shade appends per iteration
+    void (*shadow_dead)(RenderArgs, WfArgs, uint32_t) = nullptr;
 };
 
 // The trace configurations of the builds (traverse.hpp TraceDefaults), by what they restate.
@@ -1415,9 +1421,11 @@ struct ShadowFatLc : ClosestFatLc { static constexpr bool SHADOW = true; };
 // + the exact short split division by the ray's RN(1/d) in the shadow trace (43; 44 without the leaf cull)
 struct ShadowFatLcFd : ShadowFatLc { static constexpr bool FD = true; };
 struct ShadowFatFd : ShadowFat { static constexpr bool FD = true; };
+struct ShadowFatFdDead : ShadowFatFd { static constexpr bool DEAD = true; };
 // the same with the compressed leaf cull records (48 B per leaf instead of 96: three loads, not six)
 struct ClosestFatLc5 : Fat { static constexpr int LC = 5; };
 struct ShadowFatLc5Fd : ClosestFatLc5 { static constexpr bool SHADOW = true, FD = true; };
+struct ShadowFatLc5FdDead : ShadowFatLc5Fd { static constexpr bool DEAD = true; };
 struct ClosestFatLc5Perf : ClosestFatLc5 { static constexpr bool PC = true; };
 struct ShadowFatLc5Perf : ClosestFatLc5Perf { static constexpr bool SHADOW = true; };
 // ... and with the short compressed records (32 B per leaf: two loads, or one scalar load)
@@ -1508,10 +1516,12 @@ static const WfBuild kWf[] = {
     //     no spills at 8 waves once the stack-overflow pointer and the query count stopped occupying
     //     VGPRs): 357.5 / 355.3 vs 358.4 / 358.1 ms per pass, nanobox 162.4 vs 163.7 ms (shadow 30.7 -> 29.9)
     {43, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
-    {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 0, 2, 1, 0}},
+    {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 0, 2, 1, 0, 0,
+          wf_trace<tc::ShadowFatFdDead>}},
     // 49: 43 whose secondary closest, shadow and tail traces read the compressed leaf cull records
     //     (leafcull.hpp LC_RECC: boxes on the scene's 16-bit grid, octahedral axes, half constants)
-    {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 0, 2, 1, 5}},
+    {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 0, 2, 1, 5, 0,
+          wf_trace<tc::ShadowFatLc5FdDead>}},
 #ifdef CR_ALL_VARIANTS
     // 51: 49 with the short compressed records (leafcull.hpp LC_RECS: 32 B per leaf, the boxes of 49, each
     //     group's octahedral axis, kappa and dt in 13 bits: two loads per leaf record instead of three, one
@@ -1804,7 +1814,11 @@ static uint32_t shade_app_chunk(const WfArgs &W, uint32_t nin, int num_cus) {
 }
 uint32_t wf_shade_blocks(int num_cus, int shade_waves) { return shade_grid(num_cus, shade_waves == 8 ? 8 : 6); }
 static void launch_shade(const RenderArgs &A, const WfArgs &W, uint32_t g, int num_cus, hipStream_t st) {
-    if (W.shade_waves == 8)
+    if (W.app_chunk && W.shade_waves == 8)
+        hipLaunchKernelGGL((wf_shade<8, true>), dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
+    else if (W.app_chunk)
+        hipLaunchKernelGGL((wf_shade<1, true>), dim3(shade_grid(num_cus, 6)), dim3(256), 0, st, A, W, g);
+    else if (W.shade_waves == 8)
         hipLaunchKernelGGL(wf_shade<8>, dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
     else
         hipLaunchKernelGGL(wf_shade<1>, dim3(shade_grid(num_cus, 6)), dim3(256), 0, st, A, W, g);
@@ -1875,8 +1889,9 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     closest(1, st, nullptr, W.gstack); // camera rays: path order is already coherent
     uint32_t nin = W.P; // rays of closest queue g (generation 1: one per path)
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
-        W.app_chunk = shade_app_chunk(W, nin, num_cus);
+        W.app_chunk = v.shadow_dead ? shade_app_chunk(W, nin, num_cus) : 0u;
         launch_shade(A, W, g, num_cus, st);
+        const bool dead = W.app_chunk != 0u; // shadow queue g may hold dead entries
         W.app_chunk = 0u;
         uint32_t cnt[2] = {0u, 0u}; // shadow queue g, closest queue g + 1
         if ((err = (int)hipMemcpyAsync(&cnt[0], W.cnt + WF_G + g, 4, hipMemcpyDeviceToHost, st)) ||
@@ -1910,7 +1925,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         W.order = order_s;
         W.ended_only = overlap ? 1u : 0u;
         if ((err = trace_event(te, st, TK_SHADOW, true))) break;
-        hipLaunchKernelGGL(v.shadow, dim3(sblocks), dim3(blk), lds, st, A, W, g);
+        hipLaunchKernelGGL(dead ? v.shadow_dead : v.shadow, dim3(sblocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, TK_SHADOW, false))) break;
         hipLaunchKernelGGL(W.fold ? wf_fold : wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
         W.ended_only = 0u;
