@@ -350,6 +350,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.occ = (uint32_t *)take(4 * (size_t)Q);
                 W.qspare = (uint32_t)(Q - P);
                 W.app_force = (uint32_t)c->wf_app_chunk;
+                W.shade_block = (uint32_t)c->wf_shade_block;
                 W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
                 W.cxy = (float2 *)take(8 * (size_t)P);
                 W.ended = (uint32_t *)take(4 * (size_t)P);
@@ -1305,6 +1306,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_resolve_paths") && v >= 0 && v <= 64) c->wf_resolve_paths = (uint32_t)v;
     else if (!std::strcmp(key, "wf_fold") && v >= 0 && v <= 2) c->wf_fold = (int)v;
     else if (!std::strcmp(key, "wf_shade_waves") && (v == 6 || v == 8)) c->wf_shade_waves = (int)v;
+    else if (!std::strcmp(key, "wf_shade_block") && (v == 256 || v == 512 || v == 1024)) c->wf_shade_block = (int)v;
     else if (!std::strcmp(key, "wf_app_chunk") && (v == 0 || (v >= 256 && v <= 65536 && !(v & (v - 1))))) c->wf_app_chunk = (int)v;
     else if (!std::strcmp(key, "wf_leaf_shift") && v >= 0 && v <= 24) c->wf_leaf_shift = (uint32_t)v;
     else if (!std::strcmp(key, "node_bfs") && v >= 1 && v <= (1ll << 30)) c->node_bfs = (uint32_t)v;

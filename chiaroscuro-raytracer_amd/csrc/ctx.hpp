@@ -144,6 +144,10 @@ struct cr_ctx {
     // wf_shade's append chunk (WfArgs::app_force): 0 = by the queue's length (launch_wavefront_chunk), else
     // this power of two >= 256 whenever the queue arrays have room (tests: the dead entries at small sizes)
     int wf_app_chunk = 0;
+    // WfArgs::shade_block (option "wf_shade_block"): threads per wf_shade block, i.e. rays per queue append on
+    // sorted queues (round 5, sponza stand-in, two interleaved rounds: 256 -> 2270.9 / 2276.0, 512 -> 2313.8 /
+    // 2314.6, 1024 -> 2318.1 / 2314.2 Mray/s -- the same-address append atomics, scripts/append_bench.hip)
+    int wf_shade_block = 1024;
     uint32_t node_bfs = cr::NODE_BFS; // nodes numbered breadth-first at the next cr_upload_scene
     // multi-process frame split (cr_comm_init / cr_render_dist_device): one RCCL
     // communicator per process, this rank's compact tile buffer, the root's gather area

@@ -275,6 +275,7 @@ struct WfArgs {
     uint32_t app_chunk;
     uint32_t qspare;    // queue slots past P in every queue-indexed array (the dead entries' room; 0: no chunks)
     uint32_t app_force; // option "wf_app_chunk": this chunk size (>= 256) for every launch that has room (tests)
+    uint32_t shade_block; // wf_shade's threads per block for the per-iteration appends (256, 512, 1024)
     // 1: no wf_camera launch -- the packet camera trace derives each path's camera ray from its
     // (pixel, sample) itself, and wf_shade(1) / wf_resolve(1) take path p = ray p and the eye as
     // its origin (set per chunk by launch_wavefront_chunk; option "wf_cam_fuse")

@@ -43,7 +43,9 @@ enum : uint32_t { SEXCL_CONT = 0x80000000u };
 // atomicAdd per block instead of one per wave -- same-address atomics from
 // every wave of the grid serialise in one L2 slice.  Slots keep lane order
 // within a wave and wave order within the block.
-__device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, uint32_t *lds /* [5] */) {
+// (lds: one word per wave of the block, up to 16, then the base)
+enum : uint32_t { APP_W = 16 };
+__device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, uint32_t *lds /* [APP_W + 1] */) {
     const uint64_t m = __ballot(pred);
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     if (lane == 0) lds[wave] = (uint32_t)__popcll(m);
@@ -55,10 +57,10 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, u
             lds[w] = s;
             s += c;
         }
-        lds[4] = s ? atomicAdd(counter, s) : 0u;
+        lds[APP_W] = s ? atomicAdd(counter, s) : 0u;
     }
     __syncthreads();
-    const uint32_t slot = lds[4] + lds[wave] +
+    const uint32_t slot = lds[APP_W] + lds[wave] +
                           __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     __syncthreads(); // lds reused by the next call
     return slot;
@@ -71,13 +73,13 @@ __device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, u
 template <int N>
 __device__ __forceinline__ void block_append_n(uint32_t *const (&counter)[N], const bool (&pred)[N], uint32_t *lds,
                                                uint32_t buf, uint32_t (&slot)[N]) {
-    uint32_t *L = lds + buf * 5u * N;
+    uint32_t *L = lds + buf * (APP_W + 1u) * N;
     const uint32_t wave = threadIdx.x >> 6;
     uint64_t m[N];
 #pragma unroll
     for (int q = 0; q < N; q++) {
         m[q] = __ballot(pred[q]);
-        if ((threadIdx.x & 63u) == 0) L[4 * q + wave] = (uint32_t)__popcll(m[q]);
+        if ((threadIdx.x & 63u) == 0) L[APP_W * q + wave] = (uint32_t)__popcll(m[q]);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -86,8 +88,8 @@ __device__ __forceinline__ void block_append_n(uint32_t *const (&counter)[N], co
         for (int q = 0; q < N; q++) {
             uint32_t s = 0;
             for (uint32_t w = 0; w < (blockDim.x >> 6); w++) {
-                const uint32_t c = L[4 * q + w];
-                L[4 * q + w] = s;
+                const uint32_t c = L[APP_W * q + w];
+                L[APP_W * q + w] = s;
                 s += c;
             }
             tot[q] = s;
@@ -96,12 +98,12 @@ __device__ __forceinline__ void block_append_n(uint32_t *const (&counter)[N], co
 #pragma unroll
         for (int q = 0; q < N; q++) base[q] = tot[q] ? atomicAdd(counter[q], tot[q]) : 0u;
 #pragma unroll
-        for (int q = 0; q < N; q++) L[4 * N + q] = base[q];
+        for (int q = 0; q < N; q++) L[APP_W * N + q] = base[q];
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < N; q++)
-        slot[q] = L[4 * N + q] + L[4 * q + wave] +
+        slot[q] = L[APP_W * N + q] + L[APP_W * q + wave] +
                   __builtin_amdgcn_mbcnt_hi((uint32_t)(m[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[q], 0u));
 }
 
@@ -114,13 +116,13 @@ template <int N>
 __device__ __forceinline__ void block_append_chunk(uint32_t *const (&counter)[N], const bool (&pred)[N], uint32_t *lds,
                                                    uint32_t buf, uint32_t C, uint32_t (&cb)[N], uint32_t (&cu)[N],
                                                    uint32_t (&slot)[N]) {
-    uint32_t *L = lds + buf * 7u * N;
+    uint32_t *L = lds + buf * (APP_W + 3u) * N;
     const uint32_t wave = threadIdx.x >> 6;
     uint64_t m[N];
 #pragma unroll
     for (int q = 0; q < N; q++) {
         m[q] = __ballot(pred[q]);
-        if ((threadIdx.x & 63u) == 0) L[4 * q + wave] = (uint32_t)__popcll(m[q]);
+        if ((threadIdx.x & 63u) == 0) L[APP_W * q + wave] = (uint32_t)__popcll(m[q]);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -129,8 +131,8 @@ __device__ __forceinline__ void block_append_chunk(uint32_t *const (&counter)[N]
         for (int q = 0; q < N; q++) {
             uint32_t s = 0;
             for (uint32_t w = 0; w < (blockDim.x >> 6); w++) {
-                const uint32_t c = L[4 * q + w];
-                L[4 * q + w] = s;
+                const uint32_t c = L[APP_W * q + w];
+                L[APP_W * q + w] = s;
                 s += c;
             }
             tot[q] = s;
@@ -139,9 +141,9 @@ __device__ __forceinline__ void block_append_chunk(uint32_t *const (&counter)[N]
 #pragma unroll
         for (int q = 0; q < N; q++) {
             const uint32_t room = C - cu[q];
-            L[4 * N + 3 * q] = cb[q] + cu[q];
-            L[4 * N + 3 * q + 1] = tot[q] > room ? room : tot[q];
-            L[4 * N + 3 * q + 2] = fresh[q];
+            L[APP_W * N + 3 * q] = cb[q] + cu[q];
+            L[APP_W * N + 3 * q + 1] = tot[q] > room ? room : tot[q];
+            L[APP_W * N + 3 * q + 2] = fresh[q];
             if (tot[q] > room) {
                 cb[q] = fresh[q];
                 cu[q] = tot[q] - room;
@@ -153,10 +155,10 @@ __device__ __forceinline__ void block_append_chunk(uint32_t *const (&counter)[N]
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < N; q++) {
-        const uint32_t i = L[4 * q + wave] +
+        const uint32_t i = L[APP_W * q + wave] +
                            __builtin_amdgcn_mbcnt_hi((uint32_t)(m[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[q], 0u));
-        const uint32_t room = L[4 * N + 3 * q + 1];
-        slot[q] = i < room ? L[4 * N + 3 * q] + i : L[4 * N + 3 * q + 2] + (i - room);
+        const uint32_t room = L[APP_W * N + 3 * q + 1];
+        slot[q] = i < room ? L[APP_W * N + 3 * q] + i : L[APP_W * N + 3 * q + 2] + (i - room);
     }
 }
 
@@ -649,11 +651,11 @@ __device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32
 // their next ray to closest queue g + 1.
 // MINW: waves per SIMD the build is held to (6: its 75 VGPRs, no spills; 8: 64 VGPRs, the rest spilled)
 // CH: the chunked appends (WfArgs::app_chunk) -- a build of its own, so the per-iteration form keeps its
-// registers
-template <int MINW, bool CH = false>
-__global__ void __launch_bounds__(256, MINW) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
+// registers.  BS: threads per block (a block-aggregated append serves BS rays)
+template <int MINW, bool CH = false, int BS = 256>
+__global__ void __launch_bounds__(BS, MINW) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
-    __shared__ uint32_t app[5], app2[2 * 7 * 2];
+    __shared__ uint32_t app[APP_W + 1], app2[2 * (APP_W + 3) * 2];
     if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t n = *cnt_closest(W, g);
@@ -1783,16 +1785,19 @@ void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks) {
 // Grid of the grid-stride wf_shade: every block resident at once.  wf_shade needs 71 VGPRs,
 // so a SIMD holds 7 of its waves, not 8: with 8 blocks per CU the eighth started only when
 // another had finished its whole share (the grid-stride loop gives every block the same).
-static uint32_t shade_grid(int num_cus, int waves) {
-    static std::atomic<int> per_cu[2] = {0, 0};
-    const int i = waves == 8 ? 1 : 0;
-    int b = per_cu[i].load();
+static uint32_t shade_grid(int num_cus, int waves, int bs = 256) {
+    static std::atomic<int> per_cu[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    const int i = waves == 8 ? 1 : 0, j = bs == 1024 ? 2 : bs == 512 ? 1 : 0;
+    int b = per_cu[i][j].load();
     if (!b) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8> : wf_shade<1>, 256, 0) != hipSuccess || b <= 0)
-            b = 8;
-        per_cu[i].store(b);
+        hipError_t e;
+        if (j == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8, false, 1024> : wf_shade<1, false, 1024>, 1024, 0);
+        else if (j == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8, false, 512> : wf_shade<1, false, 512>, 512, 0);
+        else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8> : wf_shade<1>, 256, 0);
+        if (e != hipSuccess || b <= 0) b = 8 * 256 / bs;
+        per_cu[i][j].store(b);
     }
-    return (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)std::min(b, 8);
+    return (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)std::min(b, 8 * 256 / bs);
 }
 // wf_shade at the ctx's option "wf_shade_waves" (8, the default since round 4; or 6)
 // The append chunk of a wf_shade launch over nin rays (WfArgs::app_chunk): a power of two giving each
@@ -1818,6 +1823,10 @@ static void launch_shade(const RenderArgs &A, const WfArgs &W, uint32_t g, int n
         hipLaunchKernelGGL((wf_shade<8, true>), dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
     else if (W.app_chunk)
         hipLaunchKernelGGL((wf_shade<1, true>), dim3(shade_grid(num_cus, 6)), dim3(256), 0, st, A, W, g);
+    else if (W.shade_block == 1024)
+        hipLaunchKernelGGL((wf_shade<8, false, 1024>), dim3(shade_grid(num_cus, 8, 1024)), dim3(1024), 0, st, A, W, g);
+    else if (W.shade_block == 512)
+        hipLaunchKernelGGL((wf_shade<8, false, 512>), dim3(shade_grid(num_cus, 8, 512)), dim3(512), 0, st, A, W, g);
     else if (W.shade_waves == 8)
         hipLaunchKernelGGL(wf_shade<8>, dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
     else

@@ -154,13 +154,17 @@ def test_wavefront_chunked_appends_bitexact(ca, sponza, cornell_mm, chunk):
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("waves", [6, 8])
+@pytest.mark.parametrize("waves", [6, 8, 512, 1024])
 def test_wavefront_shade_waves_bitexact(ca, sponza, nanobox, waves):
-    """wf_shade built for 8 waves per SIMD (the default; 64 VGPRs, spills) or its natural 6: the same
-    bits and counters, counting and lean builds."""
+    """wf_shade built for 8 waves per SIMD (the default; 64 VGPRs, spills) or its natural 6, or with
+    blocks of 512 / 1024 threads (option wf_shade_block: one append per that many rays): the same bits
+    and counters, counting and lean builds."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
-        pair.dev.set_option("wf_shade_waves", waves)
+        if waves in (512, 1024):
+            pair.dev.set_option("wf_shade_block", waves)
+        else:
+            pair.dev.set_option("wf_shade_waves", waves)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
             pair.dev.set_option("counters", 0)
@@ -168,6 +172,7 @@ def test_wavefront_shade_waves_bitexact(ca, sponza, nanobox, waves):
         finally:
             pair.dev.set_option("counters", 1)
             pair.dev.set_option("wf_shade_waves", 8)
+            pair.dev.set_option("wf_shade_block", 256)
         assert_bitwise(g, o, "wf_shade_waves %d" % waves)
         assert_bitwise(g_lean, o, "wf_shade_waves %d lean" % waves)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
