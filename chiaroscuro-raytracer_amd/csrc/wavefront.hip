@@ -1809,6 +1809,7 @@ static uint32_t shade_grid(int num_cus, int waves, int bs = 256) {
 // change the order among equal keys -- 2278.5 / 2278.7 -> 2274.8 / 2270.4
 static uint32_t shade_app_chunk(const WfArgs &W, uint32_t nin, int num_cus) {
     if (W.fold || !W.qspare) return 0u;
+    // (the grid of the 256-thread build bounds the blocks of any build: a 1024-thread grid has fewer)
     const uint32_t grid = shade_grid(num_cus, W.shade_waves == 8 ? 8 : 6);
     const uint32_t want = nin / (grid * 16u), cap = W.qspare / grid;
     if (W.app_force) return W.app_force <= cap ? W.app_force : 0u;
@@ -1819,7 +1820,10 @@ static uint32_t shade_app_chunk(const WfArgs &W, uint32_t nin, int num_cus) {
 }
 uint32_t wf_shade_blocks(int num_cus, int shade_waves) { return shade_grid(num_cus, shade_waves == 8 ? 8 : 6); }
 static void launch_shade(const RenderArgs &A, const WfArgs &W, uint32_t g, int num_cus, hipStream_t st) {
-    if (W.app_chunk && W.shade_waves == 8)
+    // (a chunk holds at least one iteration's appends: 1024-thread blocks need chunks of 1024 or more)
+    if (W.app_chunk >= 1024 && W.shade_block == 1024 && W.shade_waves == 8)
+        hipLaunchKernelGGL((wf_shade<8, true, 1024>), dim3(shade_grid(num_cus, 8, 1024)), dim3(1024), 0, st, A, W, g);
+    else if (W.app_chunk && W.shade_waves == 8)
         hipLaunchKernelGGL((wf_shade<8, true>), dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
     else if (W.app_chunk)
         hipLaunchKernelGGL((wf_shade<1, true>), dim3(shade_grid(num_cus, 6)), dim3(256), 0, st, A, W, g);
