@@ -357,7 +357,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hi
                            TraceEvents *te = nullptr);
 // raysort.hip: stable radix sort of (key, value) pairs; lib: hipcub's instead
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
-               hipStream_t st, bool lib = false, bool iota = false);
+               hipStream_t st, bool lib = false, bool iota = false, bool keep_keys = true);
 size_t wf_sort_tmp_bytes(uint32_t n, int key_bits, bool lib = false);
 // Persistent grid geometry chosen by launch_render (block threads, blocks).
 void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);

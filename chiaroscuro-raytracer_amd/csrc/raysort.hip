@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(RS_THREADS) rs_downsweep(const uint32_t *keys_
         const uint32_t k = skey[j];
         const uint32_t d = (k >> shift) & (RS_BINS - 1);
         const uint32_t o = out_base[d] + (j - digit_start[d]);
-        keys_out[o] = k;
+        if (keys_out) keys_out[o] = k; // (null: the last pass of a sort whose keys are not read again)
         vals_out[o] = sval[j];
     }
 }
@@ -224,8 +224,9 @@ static size_t rs_tmp_bytes(uint32_t n) {
 // temp size in tmp_bytes.  lib: hipcub's DeviceRadixSort instead (comparison).
 // iota: vals[0] is not read -- the first digit pass takes the identity 0..n-1 (the
 // queue's own order), so the producer need not write it (hand-written sort only).
+// keep_keys false: the last digit pass writes only the permutation (the caller reads vals only)
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
-               hipStream_t st, bool lib, bool iota) {
+               hipStream_t st, bool lib, bool iota, bool keep_keys) {
     if (iota && (lib || end_bit <= 0)) return -1;
     if (lib) {
 #ifdef CR_SORT_LIB
@@ -253,8 +254,10 @@ int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, vo
         hipLaunchKernelGGL(rs_scan_sums, dim3(nseg), dim3(RS_THREADS), 0, st, H, m, sums);
         hipLaunchKernelGGL(rs_scan_top, dim3(1), dim3(RS_THREADS), 0, st, sums, nseg);
         hipLaunchKernelGGL(rs_scan_apply, dim3(nseg), dim3(RS_THREADS), 0, st, H, m, sums);
+        const bool last = shift + (int)RS_BITS >= end_bit;
         hipLaunchKernelGGL(rs_downsweep, dim3(ntiles), dim3(RS_THREADS), 0, st, keys[sel],
-                           (iota && shift == 0) ? (const uint32_t *)nullptr : vals[sel], keys[sel ^ 1], vals[sel ^ 1], n,
+                           (iota && shift == 0) ? (const uint32_t *)nullptr : vals[sel],
+                           (last && !keep_keys) ? (uint32_t *)nullptr : keys[sel ^ 1], vals[sel ^ 1], n,
                            (uint32_t)shift, ntiles, H);
     }
     if (hipGetLastError() != hipSuccess) return -1;

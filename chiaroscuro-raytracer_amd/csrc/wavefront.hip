@@ -1729,7 +1729,8 @@ static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStre
     uint32_t *keys[2] = {W.key[set][0], W.key[set][1]}, *vals[2] = {W.perm[set][0], W.perm[set][1]};
     size_t tb = W.sort_tmp_bytes;
     const int bits = pixel ? W.key_bits_pixel : (set == 0 ? W.key_bits_s : W.key_bits);
-    const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, W.sort_lib != 0, W.sort_lib == 0);
+    // (the trace reads the permutation only: the last pass writes no keys)
+    const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, W.sort_lib != 0, W.sort_lib == 0, false);
     if (sel < 0) {
         err = (int)hipErrorUnknown;
         return nullptr;
