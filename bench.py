@@ -237,6 +237,96 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+# Exit status of a rank that a collective error or timeout ended (DistWatch); the launcher then ends its peers.
+EXIT_COLLECTIVE = 3
+
+
+class DistWatch:
+    """The multi-rank run's failure report (round-6 hardening of the first 8-GPU run).
+
+    Each rank records what it is doing: the pass group it renders (`group`) and the collective in flight
+    (`enter` / `leave`, done by WatchedDist around every torch.distributed call).  A daemon thread ends the
+    rank with EXIT_COLLECTIVE when one collective has been in flight for `timeout_s` -- before the process
+    group's own timeout (set 30 s later), so the message below is printed instead of a bare watchdog
+    abort -- and a collective that raises (a peer gone, the backend's timeout) ends it the same way.  A
+    SIGTERM (torch.distributed.run stopping the survivors after one rank failed) prints the rank's state
+    too.  The message names the rank, its device, its pass group and the collective in flight (or its
+    phase outside one), so the slow or dead rank of an 8-GPU run is found from the log alone
+    (src/rayTracer.cpp:55,64: the reference's single-process loop has no such failure mode)."""
+
+    def __init__(self, rank: int, device: str, timeout_s: float):
+        import threading
+        self.rank, self.device, self.timeout_s = rank, device, timeout_s
+        self.group = "setup"
+        self.phase = "setup"
+        self.cur = None  # (collective, monotonic start)
+        self._lock = threading.Lock()
+        if timeout_s > 0:
+            threading.Thread(target=self._run, name="dist-watch", daemon=True).start()
+        try:
+            import signal
+            signal.signal(signal.SIGTERM, self._on_term)
+        except ValueError:  # (not the main thread: no handler)
+            pass
+
+    def state(self) -> str:
+        with self._lock:
+            cur = self.cur
+        what = ("collective %s in flight for %.1f s" % (cur[0], time.monotonic() - cur[1]) if cur
+                else "no collective in flight (phase: %s)" % self.phase)
+        return "rank %d device %s pass group %s: %s" % (self.rank, self.device, self.group, what)
+
+    def fail(self, why: str) -> None:
+        log("bench: FAILED %s -- %s" % (self.state(), why))
+        os._exit(EXIT_COLLECTIVE)
+
+    def enter(self, name: str) -> None:
+        with self._lock:
+            self.cur = (name, time.monotonic())
+
+    def leave(self) -> None:
+        with self._lock:
+            self.cur = None
+
+    def _run(self) -> None:
+        while True:
+            time.sleep(min(1.0, self.timeout_s / 4))
+            with self._lock:
+                cur = self.cur
+            if cur and time.monotonic() - cur[1] > self.timeout_s:
+                self.fail("collective timeout (%.0f s, --dist-timeout)" % self.timeout_s)
+
+    def _on_term(self, signum, frame) -> None:
+        log("bench: TERMINATED %s" % self.state())
+        os._exit(EXIT_COLLECTIVE)
+
+
+class WatchedDist:
+    """torch.distributed as the bench and DistributedFrame use it, every collective bracketed by
+    DistWatch.enter / leave and an exception from one reported by DistWatch.fail."""
+
+    COLLECTIVES = ("barrier", "all_reduce", "all_gather", "gather", "broadcast", "broadcast_object_list")
+
+    def __init__(self, dist, watch: DistWatch):
+        self._dist, self._watch = dist, watch
+
+    def __getattr__(self, name):
+        attr = getattr(self._dist, name)
+        if name not in self.COLLECTIVES:
+            return attr
+        watch = self._watch
+
+        def call(*a, **kw):
+            watch.enter(name)
+            try:
+                r = attr(*a, **kw)
+            except Exception as e:  # (a peer gone, the backend's own timeout)
+                watch.fail("%s raised %s: %s" % (name, type(e).__name__, str(e).splitlines()[0][:300] if str(e) else ""))
+            watch.leave()
+            return r
+        return call
+
+
 class GpuBackend:
     """What a rank runs on: one MI355X per rank, RCCL (the nccl backend) between
     ranks, the C-ABI device (chiaroscuro_amd.Device) with the scene in HBM.
@@ -252,14 +342,27 @@ class GpuBackend:
     device = "cuda"
     dist_backend = "nccl"
 
-    def init_rank(self, world, local):
+    def init_rank(self, world, local, timeout_s=120.0):
+        import datetime
         import torch
         torch.cuda.set_device(local)
         if world > 1:
             import torch.distributed as dist
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # asynchronous error handling: a failed or timed-out RCCL collective raises (or ends the process)
+            # instead of leaving the rank blocked; DistWatch reports first (its timeout is 30 s shorter)
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=datetime.timedelta(seconds=timeout_s + 30.0))
             return dist
         return None
+
+    def collectives_version(self) -> str:
+        import torch
+        try:
+            v = torch.cuda.nccl.version()
+            return "RCCL %s" % (".".join(str(x) for x in v) if isinstance(v, tuple) else v)
+        except Exception as e:  # (reported, never fatal)
+            return "RCCL version unknown (%s)" % type(e).__name__
 
     def synchronize(self):
         import torch
@@ -315,6 +418,9 @@ def main():
     ap.add_argument("--save-frame", default="", help="rank 0 writes the final accumulated frame (.npy)")
     ap.add_argument("--single-layer-steps", type=int, default=2,
                     help="after the timed steps: this many one-layer passes (+1 warmup), reported as single_layer_ms")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="N > 1: seconds one collective may stay in flight before every rank exits non-zero with "
+                         "its rank, device, pass group and the collective (DistWatch)")
     ap.add_argument("--parity-rows", type=int, default=8,
                     help="rank 0 checks this many rows of the timed frame (every layer, full spp) bit for bit "
                          "against the oracle after the timed region (0: skip)")
@@ -340,17 +446,28 @@ def run_rank(args, world, backend):
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = backend.init_rank(world, local)
+    watch = None
+    if world > 1:
+        watch = DistWatch(rank, "%s:%d" % (backend.device, local), args.dist_timeout)
+        watch.phase = "init_process_group"
+        dist = backend.init_rank(world, local, args.dist_timeout)
+        dist = WatchedDist(dist, watch)
+        watch.phase = "scene load"
+    else:
+        dist = backend.init_rank(world, local)
     if dist is not None:
         assert dist.get_world_size() == world, (dist.get_world_size(), world)
         if rank == 0:
-            log("bench: %d ranks, backend %s" % (dist.get_world_size(), dist.get_backend()))
+            ver = backend.collectives_version() if hasattr(backend, "collectives_version") else "n/a"
+            log("bench: world size %d, backend %s, %s, collective timeout %.0f s" %
+                (dist.get_world_size(), dist.get_backend(), ver, args.dist_timeout))
 
     rtc = scenes.config_rtc(args.config)
     t0 = time.time()
     scene = ca.Scene(rtc, *(("xres", args.res.split("x")[0], "yres", args.res.split("x")[1]) if args.res else ()))
     info = scene.info
     model = ca.Model(scene)
+    tex_bytes = sum(len(a) for *_, a in model.textures())  # the scene's texels (a11: getColorAt reads them)
     kd = ca.KDTree(model, scene)
     opts = [(kv.split("=", 1)[0], int(kv.split("=", 1)[1], 0)) for kv in args.opt]
     dev = backend.make_device(local, info, model, kd, opts)
@@ -385,6 +502,12 @@ def run_rank(args, world, backend):
 
     def step(layer, n, record):
         """Layers layer .. layer + n - 1 (n <= nl_pass) as one pass group."""
+        if watch:
+            watch.group = "layers %d..%d" % (layer, layer + n - 1)
+            watch.phase = "render"
+        stall = os.environ.get("CHIARO_TEST_STALL_RANK")  # (tests: this rank stalls before its first timed group)
+        if stall is not None and int(stall) == rank and record and not groups:
+            time.sleep(float(os.environ.get("CHIARO_TEST_STALL_S", "60")))
         p = ca.render_params(xres, yres, spp, k, seed, layer=layer, rank=rank, nranks=world, tile=tile)
         tp = time.perf_counter()
         n, pieces = fr.plan_layers(p, n)  # (with several ranks: agreed by an all-reduce MIN)
@@ -437,6 +560,8 @@ def run_rank(args, world, backend):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if watch:
+        watch.group, watch.phase = "after the timed groups", "single-layer passes"
     timed_build = dev.last_trace_build() if hasattr(dev, "last_trace_build") else None
     nlayers_done = layer - 1  # the frame holds layers 1 .. nlayers_done (warmup and timed groups)
     # rows of the timed frame for the parity check (rank 0; the oracle runs after the collectives)
@@ -485,6 +610,8 @@ def run_rank(args, world, backend):
     rank_render_ms = [round(r[1], 3) for r in per_rank]
 
     # counting pass (untimed): algorithmic bytes of one launch of this rank
+    if watch:
+        watch.phase = "counting and performed-work passes"
     dev.set_option("counters", 1)
     pc = ca.render_params(xres, yres, spp, k, seed, layer=first_timed, rank=rank, nranks=world, tile=tile)
     scratch = torch.zeros((yres, xres, 3), dtype=torch.float32, device=backend.device)
@@ -497,6 +624,7 @@ def run_rank(args, world, backend):
     cts = dev.trace_stats() if wavefront else None
     totals["bytes"] = ca.algorithmic_bytes(cc, cc["pixels"])
     totals["tritest"] = cc["tritest"]
+    totals["texhit"] = cc["texhit"]
     totals["count_rays"] = cc["closest"] + cc["shadow"]
     dev.set_option("counters", 0)
     # performed-work pass (untimed): the default trace build's kernels with counters of what they
@@ -638,7 +766,7 @@ def run_rank(args, world, backend):
                         "algorithmic_bytes_per_launch": int(pass_bytes)}
         label = {"sponza": "sponza_standin (Sponza-Crytek stand-in, ~261k tris) 1920x1080",
                  "sponza_4k": "sponza_standin (Sponza-Crytek stand-in) 3840x2160",
-                 "nanobox": "nanobox_standin (textured nanosuit-in-a-box stand-in, ~20k tris) 1920x1080",
+                 "nanobox": "nanobox_standin (textured nanosuit-in-a-box stand-in, ~19k tris, the asset's 21 MB texture set) 1920x1080",
                  "cornell": "cornell_unit 256x256", "cornell_box": "cornell_box_lit 1024x1024"}[args.config]
         out = {
             "metric": "Mray/s (primary+secondary) on sponza_crytek 1080p; 1/2/4/8-GPU scaling",
@@ -668,7 +796,11 @@ def run_rank(args, world, backend):
                        "rays_answered_untraced": int(nee_all),
                        "rank_render_ms": rank_render_ms, "layers_per_pass": nl_pass,
                        "pass_groups": [list(g) for g in groups], "trace_build": timed_build,
-                       "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2)},
+                       "mean_tritest_per_ray": round(totals["tritest"] / max(totals["count_rays"], 1), 2),
+                       # textured hits of one layer (counting pass; 3 texel bytes each in SURVEY §8d's bytes)
+                       # and the scene's texture bytes (src/mesh.cpp:21-35 reads them)
+                       "texhit_per_layer": int(totals["texhit"]), "texhit_bytes_per_layer": 3 * int(totals["texhit"]),
+                       "texture_bytes": int(tex_bytes)},
             "roofline": roofline,
             "cpu_baseline": cpu,
             # value over the CPU baseline: the timed 16-thread share of the box, and the whole host's

@@ -156,7 +156,7 @@ PERF_NAMES = ("queries", "steps", "leaves", "masks", "tests", "vbytes", "sbytes"
 
 class CrTraceStats(C.Structure):
     _fields_ = [("launches", C.c_uint64 * 4), ("ms", C.c_double * 4), ("inner", C.c_uint64 * 4),
-                ("leaf", C.c_uint64 * 4), ("tritest", C.c_uint64 * 4)]
+                ("leaf", C.c_uint64 * 4), ("tritest", C.c_uint64 * 4), ("chunked_shades", C.c_uint64)]
 
 
 class CrTonemapParams(C.Structure):
@@ -628,6 +628,13 @@ class Device:
         return {name: {"launches": int(t.launches[i]), "ms": float(t.ms[i]), "inner": int(t.inner[i]),
                        "leaf": int(t.leaf[i]), "tritest": int(t.tritest[i])}
                 for i, name in enumerate(TRACE_KINDS)}
+
+    def chunked_shades(self) -> int:
+        """cr_get_trace_stats' chunked_shades: the wf_shade launches of the last wavefront render that
+        reserved queue slots in chunks."""
+        t = CrTraceStats()
+        self._chk(libs()[0].cr_get_trace_stats(self._c, C.byref(t)), "cr_get_trace_stats")
+        return int(t.chunked_shades)
 
     def diag(self) -> dict:
         """cr_get_diag: leaf-round shapes and the repeated-miss census of the last

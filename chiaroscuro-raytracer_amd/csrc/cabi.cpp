@@ -416,6 +416,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         A.cull = cull ? (const float4 *)c->d_cull : nullptr;
         A.cull_node = cull ? (const float4 *)c->d_cull_node : nullptr;
         c->tev.n = 0;
+        c->tev.chunked = 0;
         HIPCHK(hipEventRecord(c->ev0, st));
         if (cull)
             if (int e = cr::launch_cam_cull(A, c->n_refs, (float4 *)c->d_cull, (float4 *)c->d_cull_node, c->d_levels,
@@ -472,6 +473,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             c->last_trace.launches[k]++;
             c->last_trace.ms[k] += ms;
         }
+        c->last_trace.chunked_shades = (uint64_t)c->tev.chunked;
         for (int k = 0; k < cr::TK_TAIL; k++) { // the tail kernel's work is not split by kind
             c->last_trace.inner[k] = h[cr::CTR_TRACE + 3 * k];
             c->last_trace.leaf[k] = h[cr::CTR_TRACE + 3 * k + 1];

@@ -79,7 +79,7 @@ static int wait_comm(cr_ctx *c, ncclComm_t comm, hipStream_t st, const char *wha
 // the ranks, a buffer that cannot grow) then makes EVERY rank fail here with the same error, instead of
 // returning before the grouped send / receive and leaving its peers blocked in it until comm_timeout_ms.
 static int agree(cr_ctx *c, bool ok, hipStream_t st, const char *what) {
-    if (int r = grow(c, (void **)&c->d_flag, c->flag_bytes, sizeof(int))) return r;
+    // (d_flag exists since cr_comm_init: nothing that can fail on one rank alone precedes the all-reduce)
     HIPCHK(hipMemsetD32Async((hipDeviceptr_t)c->d_flag, ok ? 1 : 0, 1, st));
     ncclResult_t r = ncclAllReduce(c->d_flag, c->d_flag, 1, ncclInt32, ncclMin, c->comm, st);
     if (r == ncclInProgress) r = nccl_settle(c->comm);
@@ -160,6 +160,9 @@ int cr_comm_init(cr_ctx *c, int nranks, int rank, const uint8_t *id) {
     if (nranks < 1 || rank < 0 || rank >= nranks || !id) return fail(c, CR_E_INVALID, "bad nranks/rank/id");
     HIPCHK(hipSetDevice(c->device));
     release_dist(c);
+    // agree()'s flag word is allocated here, before any collective: a rank whose allocation fails then
+    // fails before the communicator exists, never between its peers' entry into an all-reduce and its own
+    if (int rr = grow(c, (void **)&c->d_flag, c->flag_bytes, sizeof(int))) return rr;
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
     // non-blocking init, polled against a deadline: a rank whose peers never join (a dead

@@ -314,7 +314,7 @@ struct WfStreams {
     hipEvent_t fork, join;
 };
 int num_wf_variants();
-// blocks of a wf_shade launch at the ctx's wf_shade_waves (its grid-stride grid)
+// the most blocks a chunked-append wf_shade launch has at the ctx's wf_shade_waves (spare-slot sizing)
 uint32_t wf_shade_blocks(int num_cus, int shade_waves);
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
@@ -335,6 +335,7 @@ struct TraceEvents {
     hipEvent_t *ev = nullptr; // [2 * cap]
     int *kind = nullptr;      // [cap]
     int cap = 0, n = 0;
+    int chunked = 0; // wf_shade launches that appended in chunks (WfArgs::app_chunk != 0)
 };
 // One chunk: camera, closest 1, then per generation shade, shadow || next closest, resolve.
 // Two chunks in flight (cr_set_option "wf_lanes" 2): each lane owns a buffer set

@@ -1786,19 +1786,32 @@ void wf_tail_geometry(int num_cus, uint32_t &block, uint32_t &blocks) {
 // Grid of the grid-stride wf_shade: every block resident at once.  wf_shade needs 71 VGPRs,
 // so a SIMD holds 7 of its waves, not 8: with 8 blocks per CU the eighth started only when
 // another had finished its whole share (the grid-stride loop gives every block the same).
-static uint32_t shade_grid(int num_cus, int waves, int bs = 256) {
-    static std::atomic<int> per_cu[2][3] = {{0, 0, 0}, {0, 0, 0}};
-    const int i = waves == 8 ? 1 : 0, j = bs == 1024 ? 2 : bs == 512 ? 1 : 0;
-    int b = per_cu[i][j].load();
+// The occupancy is queried for the instantiation actually launched (CH: the chunked appends, whose extra
+// chunk state may need more registers than the per-iteration form), so every block of the grid is resident
+// at once -- a chunked block owns one contiguous span of the queue, and a block that started late would
+// run its whole span after the others had finished.
+template <int MINW, bool CH, int BS> static int shade_occupancy() {
+    int b = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, wf_shade<MINW, CH, BS>, BS, 0);
+    return e != hipSuccess || b <= 0 ? 8 * 256 / BS : b;
+}
+static uint32_t shade_grid(int num_cus, int waves, int bs = 256, bool chunked = false) {
+    static std::atomic<int> per_cu[2][3][2] = {};
+    const int i = waves == 8 ? 1 : 0, j = bs == 1024 ? 2 : bs == 512 ? 1 : 0, k = chunked ? 1 : 0;
+    int b = per_cu[i][j][k].load();
     if (!b) {
-        hipError_t e;
-        if (j == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8, false, 1024> : wf_shade<1, false, 1024>, 1024, 0);
-        else if (j == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8, false, 512> : wf_shade<1, false, 512>, 512, 0);
-        else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, i ? wf_shade<8> : wf_shade<1>, 256, 0);
-        if (e != hipSuccess || b <= 0) b = 8 * 256 / bs;
-        per_cu[i][j].store(b);
+        if (k) b = j == 2 ? shade_occupancy<8, true, 1024>() : i ? shade_occupancy<8, true, 256>() : shade_occupancy<1, true, 256>();
+        else if (j == 2) b = i ? shade_occupancy<8, false, 1024>() : shade_occupancy<1, false, 1024>();
+        else if (j == 1) b = i ? shade_occupancy<8, false, 512>() : shade_occupancy<1, false, 512>();
+        else b = i ? shade_occupancy<8, false, 256>() : shade_occupancy<1, false, 256>();
+        per_cu[i][j][k].store(b);
     }
     return (uint32_t)(num_cus > 0 ? num_cus : 256) * (uint32_t)std::min(b, 8 * 256 / bs);
+}
+// Blocks of any chunked wf_shade launch at most (the spare queue slots hold every block's partial last chunk):
+// the larger of the 256- and 1024-thread chunked grids
+uint32_t wf_shade_blocks(int num_cus, int shade_waves) {
+    return std::max(shade_grid(num_cus, shade_waves == 8 ? 8 : 6, 256, true), shade_grid(num_cus, 8, 1024, true));
 }
 // wf_shade at the ctx's option "wf_shade_waves" (8, the default since round 4; or 6)
 // The append chunk of a wf_shade launch over nin rays (WfArgs::app_chunk): a power of two giving each
@@ -1810,8 +1823,7 @@ static uint32_t shade_grid(int num_cus, int waves, int bs = 256) {
 // change the order among equal keys -- 2278.5 / 2278.7 -> 2274.8 / 2270.4
 static uint32_t shade_app_chunk(const WfArgs &W, uint32_t nin, int num_cus) {
     if (W.fold || !W.qspare) return 0u;
-    // (the grid of the 256-thread build bounds the blocks of any build: a 1024-thread grid has fewer)
-    const uint32_t grid = shade_grid(num_cus, W.shade_waves == 8 ? 8 : 6);
+    const uint32_t grid = wf_shade_blocks(num_cus, W.shade_waves);
     const uint32_t want = nin / (grid * 16u), cap = W.qspare / grid;
     if (W.app_force) return W.app_force <= cap ? W.app_force : 0u;
     if (W.sort) return 0u;
@@ -1819,19 +1831,22 @@ static uint32_t shade_app_chunk(const WfArgs &W, uint32_t nin, int num_cus) {
     while (c * 2u <= want && c * 2u <= cap && c < 4096u) c *= 2u;
     return c <= want && c <= cap ? c : 0u;
 }
-uint32_t wf_shade_blocks(int num_cus, int shade_waves) { return shade_grid(num_cus, shade_waves == 8 ? 8 : 6); }
 static void launch_shade(const RenderArgs &A, const WfArgs &W, uint32_t g, int num_cus, hipStream_t st) {
     // (a chunk holds at least one iteration's appends: 1024-thread blocks need chunks of 1024 or more)
     if (W.app_chunk >= 1024 && W.shade_block == 1024 && W.shade_waves == 8)
-        hipLaunchKernelGGL((wf_shade<8, true, 1024>), dim3(shade_grid(num_cus, 8, 1024)), dim3(1024), 0, st, A, W, g);
+        hipLaunchKernelGGL((wf_shade<8, true, 1024>), dim3(shade_grid(num_cus, 8, 1024, true)), dim3(1024), 0, st, A, W, g);
     else if (W.app_chunk && W.shade_waves == 8)
-        hipLaunchKernelGGL((wf_shade<8, true>), dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
+        hipLaunchKernelGGL((wf_shade<8, true>), dim3(shade_grid(num_cus, 8, 256, true)), dim3(256), 0, st, A, W, g);
     else if (W.app_chunk)
-        hipLaunchKernelGGL((wf_shade<1, true>), dim3(shade_grid(num_cus, 6)), dim3(256), 0, st, A, W, g);
-    else if (W.shade_block == 1024)
+        hipLaunchKernelGGL((wf_shade<1, true>), dim3(shade_grid(num_cus, 6, 256, true)), dim3(256), 0, st, A, W, g);
+    else if (W.shade_block == 1024 && W.shade_waves == 8)
         hipLaunchKernelGGL((wf_shade<8, false, 1024>), dim3(shade_grid(num_cus, 8, 1024)), dim3(1024), 0, st, A, W, g);
-    else if (W.shade_block == 512)
+    else if (W.shade_block == 1024)
+        hipLaunchKernelGGL((wf_shade<1, false, 1024>), dim3(shade_grid(num_cus, 6, 1024)), dim3(1024), 0, st, A, W, g);
+    else if (W.shade_block == 512 && W.shade_waves == 8)
         hipLaunchKernelGGL((wf_shade<8, false, 512>), dim3(shade_grid(num_cus, 8, 512)), dim3(512), 0, st, A, W, g);
+    else if (W.shade_block == 512)
+        hipLaunchKernelGGL((wf_shade<1, false, 512>), dim3(shade_grid(num_cus, 6, 512)), dim3(512), 0, st, A, W, g);
     else if (W.shade_waves == 8)
         hipLaunchKernelGGL(wf_shade<8>, dim3(shade_grid(num_cus, 8)), dim3(256), 0, st, A, W, g);
     else
@@ -1904,6 +1919,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     uint32_t nin = W.P; // rays of closest queue g (generation 1: one per path)
     for (uint32_t g = 1; g <= (uint32_t)A.K && !err; g++) {
         W.app_chunk = v.shadow_dead ? shade_app_chunk(W, nin, num_cus) : 0u;
+        if (te && W.app_chunk) te->chunked++;
         launch_shade(A, W, g, num_cus, st);
         const bool dead = W.app_chunk != 0u; // shadow queue g may hold dead entries
         W.app_chunk = 0u;

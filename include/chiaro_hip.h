@@ -279,6 +279,9 @@ typedef struct cr_trace_stats {
     uint64_t launches[4];
     double ms[4];
     uint64_t inner[4], leaf[4], tritest[4];
+    /* wf_shade launches of the last render that reserved queue slots in chunks ("wf_app_chunk", or the
+     * automatic chunks of scenes traced in append order) */
+    uint64_t chunked_shades;
 } cr_trace_stats;
 int cr_get_trace_stats(cr_ctx *ctx, cr_trace_stats *out);
 /* Kernel variant / tuning knobs: "kernel" (0 = persistent wave-regeneration,

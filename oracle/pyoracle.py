@@ -7,16 +7,19 @@ See oracle.h for what is restated and what is pinned.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import subprocess
 from pathlib import Path
 
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB = HERE / "liboracle.so"
+# CHIARO_ORACLE_DIR: load the libraries from there instead (the sanitizer build, oracle/_san)
+_LIBDIR = Path(os.environ["CHIARO_ORACLE_DIR"]) if os.environ.get("CHIARO_ORACLE_DIR") else HERE
+LIB = _LIBDIR / "liboracle.so"
 # the same oracle.c at -O3 without the hot-path work counters (OR_LEAN): bench.py's timed
 # cpu_baseline leg only; its query / path counts equal liboracle.so's and its pixels are the same bits
-LEAN_LIB = HERE / "liboracle_lean.so"
+LEAN_LIB = _LIBDIR / "liboracle_lean.so"
 REF_LIB = HERE / "_ref" / "libref_harness.so"
 
 FP = C.POINTER(C.c_float)

@@ -153,12 +153,16 @@ class CpuOracleBackend:
     device = "cpu"
     dist_backend = "gloo"
 
-    def init_rank(self, world, local):
+    def init_rank(self, world, local, timeout_s=120.0):
         if world > 1:
+            import datetime
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout_s + 30.0))
             return dist
         return None
+
+    def collectives_version(self):
+        return "gloo"
 
     def synchronize(self):
         pass

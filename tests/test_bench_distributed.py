@@ -143,3 +143,31 @@ def test_frame_parity_detects_one_flipped_bit(ca, po, scenes):
     bad.view(np.uint32)[2, 5, 1] ^= 1
     r = bench.frame_parity(osc, bad, rows, cam, xres, yres, spp, i["k"], i["seed"], layers)
     assert r["differing"] == 1 and r["max_rel"] > 0.0
+
+
+def test_bench_stalled_rank_every_rank_exits_with_diagnostic(tmp_path):
+    """Hardening of the first 8-GPU run (bench.py DistWatch): rank 1 stalls before its first timed pass group
+    (CHIARO_TEST_STALL_RANK), so rank 0 waits in the group's plan all-reduce.  With --dist-timeout 6 rank 0
+    must end itself once that collective has been in flight for 6 s, printing its rank, device, pass group
+    and the collective, and the launcher then stops rank 1, which prints its own state (no collective, phase
+    render).  The whole job ends non-zero long before the stall would have ended, and each rank's status is
+    the collective-failure exit code (src/rayTracer.cpp:55,64)."""
+    import time
+    env = dict(os.environ, CHIARO_BENCH_BACKEND="%s:make" % (ROOT / "tests" / "bench_cpu_backend.py"),
+               MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", CHIARO_QUIET="1", CHIARO_TEST_STALL_RANK="1",
+               CHIARO_TEST_STALL_S="600")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--config",
+           "cornell", "--res", "40x24", "--spp", "1", "--no-cpu-baseline", "--dist-timeout", "6"]
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    took = time.monotonic() - t0
+    assert r.returncode != 0, r.stderr[-3000:]
+    assert took < 240, took  # (the stall alone is 600 s)
+    err = r.stderr
+    assert "bench: FAILED rank 0 device cpu:0 pass group layers 2..3: collective all_reduce in flight" in err, err[-3000:]
+    assert "collective timeout (6 s, --dist-timeout)" in err, err[-3000:]
+    assert "bench: TERMINATED rank 1 device cpu:1 pass group layers 2..3: no collective in flight (phase: render)" \
+        in err, err[-3000:]
+    assert "exitcode  : 3" in err or "exit code 3" in err or "exitcode: 3" in err, err[-3000:]

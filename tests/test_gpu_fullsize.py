@@ -3,9 +3,9 @@ build, pass groups, frame pieces) at the configuration's full frame and spp, com
 whole rows, bit for bit.
 
 The other GPU tests render small frames (<= 160 x 90); the driver's bench checks 8 rows of the sponza
-frame.  Here each configuration of SURVEY.md section 6 -- C1 cornell 256^2 x 32 spp, C2 cornell_box
-1024^2 x 500 spp, C3 nanobox stand-in 1080p x 128 spp, the headline sponza stand-in 1080p x 128 spp and
-C5 sponza 4K -- runs bench.py in a child process for two timed layers, and the frame's first, middle and
+frame.  Here each configuration of SURVEY.md section 6 (chiaroscuro_amd.scenes.CONFIGS) -- C1 cornell
+256^2 x 4 spp, C2 cornell_box 1024^2 x 500 spp, C3 nanobox stand-in 1080p x 64 spp, the headline sponza
+stand-in 1080p x 128 spp and C5 sponza 4K x 100 spp -- runs bench.py in a child process for two timed layers, and the frame's first, middle and
 last rows after both layers must equal the oracle's blend of the same layers (bench.frame_parity:
 or_render_pixels per layer, blended as src/rayTracer.cpp:64 does)."""
 import json

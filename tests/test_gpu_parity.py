@@ -27,6 +27,8 @@ TRACE_BUILDS += [int(b) for b in os.environ.get("CR_TEST_BUILDS", "").split()]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
 QUORUM_DEFAULT = -1  # ctx.hpp desc_quorum (8, but 0 for 1024 <= triangles < 65536)
+SHADE_BLOCK_DEFAULT = 1024  # ctx.hpp wf_shade_block
+SHADE_WAVES_DEFAULT = 8  # ctx.hpp wf_shade_waves
 
 
 @pytest.fixture(scope="module")
@@ -141,40 +143,43 @@ def test_wavefront_chunked_appends_bitexact(ca, sponza, cornell_mm, chunk):
     over its iterations, and the unused end of its last chunk becomes dead entries (ray w = NO_PATH, key
     ~0) that the sort, the traces, wf_resolve and the next wf_shade skip.  128 x 96 x 128 spp puts several
     iterations on each shade block, so appends straddle chunks.  The same bits and query counters as the
-    oracle, with sorted (sponza) and unsorted (cornell_box) queues, lean and counting builds."""
+    oracle, with sorted (sponza) and unsorted (cornell_box) queues.  Only the lean build chunks (the
+    counting and performed-work builds have no dead-entry shadow trace, so their appends stay
+    per-iteration): its render must report chunked wf_shade launches, or this test would pass with the
+    chunks silently disabled."""
     x, y, s = 128, 96, 128
     for pair in (sponza, cornell_mm):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("wf_app_chunk", chunk)
         try:
-            g, gc, o, oc = _render_both(ca, pair, x, y, s)
+            g, gc, o, oc = _render_both(ca, pair, x, y, s)  # (its last render is the lean one)
+            assert pair.dev.chunked_shades() > 0, "the lean render used no chunked appends"
         finally:
             pair.dev.set_option("wf_app_chunk", 0)
         assert_bitwise(g, o, "wf_app_chunk %d" % chunk)
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
-@pytest.mark.parametrize("waves", [6, 8, 512, 1024])
-def test_wavefront_shade_waves_bitexact(ca, sponza, nanobox, waves):
-    """wf_shade built for 8 waves per SIMD (the default; 64 VGPRs, spills) or its natural 6, or with
-    blocks of 512 / 1024 threads (option wf_shade_block: one append per that many rays): the same bits
+@pytest.mark.parametrize("waves,block", [(6, 256), (8, 256), (8, 512), (8, 1024), (6, 512), (6, 1024)])
+def test_wavefront_shade_waves_bitexact(ca, sponza, nanobox, waves, block):
+    """wf_shade built for 8 waves per SIMD (the default; 64 VGPRs, spills) or its natural 6, in blocks
+    of 256, 512 or 1024 threads (option wf_shade_block: one append per that many rays; 1024 is the
+    default): every (waves, block) pair launches its own instantiation, and all give the same bits
     and counters, counting and lean builds."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
-        if waves in (512, 1024):
-            pair.dev.set_option("wf_shade_block", waves)
-        else:
-            pair.dev.set_option("wf_shade_waves", waves)
+        pair.dev.set_option("wf_shade_block", block)
+        pair.dev.set_option("wf_shade_waves", waves)
         try:
             g, gc, o, oc = _render_both(ca, pair, x, y, s)
             pair.dev.set_option("counters", 0)
             g_lean = pair.dev.render(pair.camera(ca, x, y), ca.render_params(x, y, s, 6, 0xC41A05C0))
         finally:
             pair.dev.set_option("counters", 1)
-            pair.dev.set_option("wf_shade_waves", 8)
-            pair.dev.set_option("wf_shade_block", 256)
-        assert_bitwise(g, o, "wf_shade_waves %d" % waves)
-        assert_bitwise(g_lean, o, "wf_shade_waves %d lean" % waves)
+            pair.dev.set_option("wf_shade_waves", SHADE_WAVES_DEFAULT)
+            pair.dev.set_option("wf_shade_block", SHADE_BLOCK_DEFAULT)
+        assert_bitwise(g, o, "wf_shade_waves %d block %d" % (waves, block))
+        assert_bitwise(g_lean, o, "wf_shade_waves %d block %d lean" % (waves, block))
         assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 

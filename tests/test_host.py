@@ -102,7 +102,14 @@ def test_host_kdtree_equals_oracle(ca, po, scenes, config):
     orc = po.OracleScene(m.triangles(), leaf_size=sc.info["leaf_size"], textures=m.textures(),
                          build_threads=8).kd_export()
     if config == "nanobox":
-        assert len(m.textures()) == 4 and (m.triangles()["tex"] >= 0).sum() > 20000
+        # the stand-in's figure carries the real asset's texture set (data/nanosuit.mtl:11-75): five 1024^2
+        # RGBA and one 128^2 RGBA image, over 20 MB of texels, on ~19k triangles (19,058 in nanosuit.obj);
+        # the room adds a 256^2 RGB, a 128^2 RGBA and a 64^2 grey one
+        tex = m.textures()
+        shapes = sorted((w, h, nc) for w, h, nc, _ in tex)
+        assert shapes == sorted([(1024, 1024, 4)] * 5 + [(128, 128, 4), (256, 256, 3), (128, 128, 4), (64, 64, 1)])
+        assert sum(len(a) for *_, a in tex) >= 20 << 20
+        assert 18500 <= m.num_triangles <= 19500 and (m.triangles()["tex"] >= 0).sum() > 18500
     for k in ("is_leaf", "axis", "child", "leaf_first", "leaf_count", "refs"):
         np.testing.assert_array_equal(host[k], orc[k], err_msg=k)
     for k in ("split", "box"):
