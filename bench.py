@@ -168,6 +168,25 @@ def frame_parity(osc, frame_rows, rows, cam, xres, yres, spp, k, seed, nlayers):
                     "bit for bit (uint32 compare of every fp32 value)" % nlayers}
 
 
+def lane_util(iss, view, ceil_valu_frac=None):
+    """Active lanes of the issued wave-instructions of one trace kind (the issue ceilings count wave
+    instructions whatever their exec mask): VALU from rocprofv3 (SQ_THREAD_CYCLES_VALU / (64 x
+    SQ_ACTIVE_INST_VALU), profiles/pmc_issue_<config>.json), vector memory estimated from the
+    performed-work build's per-lane bytes over the profiled vector-load instructions at 16 B a lane (the
+    records are 16-B loads; the few 4- and 8-B loads make it a lower bound)."""
+    if not iss:
+        return None
+    out = {"valu": iss.get("valu_lane_util")}
+    vb = ((view or {}).get("bytes_per_launch") or {}).get("performed_vector")
+    vm = iss.get("vmem_rd_insts_per_launch")
+    out["vmem_est_16B"] = round(vb / 16 / vm / 64, 3) if vb and vm else None
+    if out["valu"] is not None and ceil_valu_frac is not None:
+        out["valu_issue_x_lanes"] = round(ceil_valu_frac * out["valu"], 3)
+        out["note"] = ("VALU issue %.2f of its ceiling x %.2f of the lanes active = %.2f of the lane-level "
+                       "peak" % (ceil_valu_frac, out["valu"], ceil_valu_frac * out["valu"]))
+    return out
+
+
 def issue_roofline(dom, iss, views, issue, pass_view, kind):
     """Roofline of the dominant trace kernel against the ceiling that binds it.
 
@@ -215,7 +234,8 @@ def issue_roofline(dom, iss, views, issue, pass_view, kind):
             "ta_busy_profiled": iss.get("ta_busy"),
             "ta_note": "vector-memory address path busy fraction from the rocprofv3 PMC pass (no live "
                        "counterpart): the trace kernels are co-limited by issue and the address path",
-            "hbm_bytes": {"frac": bytes_view["fabric_frac_of_hbm"], "note": "measured fabric bytes over the launch time"}}
+            "hbm_bytes": {"frac": bytes_view["fabric_frac_of_hbm"], "note": "measured fabric bytes over the launch time"},
+            "lane_util": lane_util(iss, dom, ceil_valu_frac=round(valu / VALU_PEAK_GIPS, 4))}
     bound = max(("valu", "salu"), key=lambda k: ceil[k]["frac"])
     b = ceil[bound]
     return {"bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": "Gwave-inst/s", "frac": b["frac"],
@@ -401,7 +421,7 @@ def main():
     ap.add_argument("--config", default="sponza", help="cornell | cornell_box | sponza | sponza_4k")
     ap.add_argument("--spp", type=int, default=0, help="override samples per step (default: config's)")
     ap.add_argument("--kernel", type=int, default=-1,
-                    help="2 wavefront (default), 0 persistent megakernel, 1 one-thread-per-pixel")
+                    help="2 wavefront (the only render kernel; the megakernel and thread-per-pixel kernels were removed)")
     ap.add_argument("--variant", type=int, default=-1, help="kernel build variant (default: the kernel's)")
     ap.add_argument("--gather", default="torch", choices=("torch", "cabi"),
                     help="N > 1: tile gather by torch.distributed (default) or the library's own RCCL "
@@ -659,8 +679,7 @@ def run_rank(args, world, backend):
                     pj = None
             except Exception:
                 pj = None
-        kernel_name = {0: "persistent megakernel", 1: "thread per pixel", 2: "wavefront"}[
-            args.kernel if args.kernel >= 0 else 2]
+        kernel_name = "wavefront"
         cpu = None
         parity = None
         osc = None

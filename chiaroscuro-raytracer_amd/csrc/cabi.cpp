@@ -4,9 +4,7 @@
 // kernels.hip header), the progressive accumulator, the counters and the
 // per-launch HIP events.  No C++ exception or hipError_t crosses the ABI.
 #include "ctx.hpp"
-#include "quadnodes.hpp"
 #include "leafcull.hpp"
-#include "planecull.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -112,7 +110,6 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     A.mode = mode;
     A.out = out;
     A.counters = c->d_counters;
-    A.work = c->d_work;
     A.full_counters = c->full_counters;
     A.perf_counters = c->perf_counters;
     A.diag_kinds = c->diag_kinds;
@@ -128,13 +125,13 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // re-swept under leaf-keyed queues (scripts/gpu_leaf_sweep.sh, 1080p x 128 spp, closest /
     // shadow): 56/48 397.4, 48/56 394.5, 48/48 395.9, 56/56 396.2 ms per pass; a rank of 8:
     // 59.96 vs 59.64 ms -> closest 48 / shadow 56
-    A.refill = c->refill ? c->refill : (c->kernel == 2 ? 48u : 16u);
+    A.refill = c->refill ? c->refill : 48u;
     // round 4: 60 on scenes whose queues are sorted (sponza 290.8 / 290.7 -> 289.8 / 290.1 ms per layer, nanobox
     // 143.4 / 143.3 -> 141.8 / 141.6), 56 on the unsorted small ones (cornell_box 95.7 -> 97.7 ms at 60)
     A.refill_shadow = c->refill_shadow ? c->refill_shadow
                                        : (c->refill ? c->refill : (c->n_tris >= SORT_MIN_TRIS ? 60u : 56u));
     // camera rays (64 samples of one pixel per wave): lock-step is best, 64 -> 933 vs 56 -> 924 Mray/s
-    A.refill_camera = c->refill_camera ? c->refill_camera : (c->refill ? c->refill : (c->kernel == 2 ? 64u : 16u));
+    A.refill_camera = c->refill_camera ? c->refill_camera : (c->refill ? c->refill : 64u);
     // wavefront trace builds (wavefront.hip kWf): 2 = LDS ring 8, 8 waves/SIMD, scalar loads for
     // wave-uniform nodes / leaves: 1003 vs 935 Mray/s for the same build without them (variant 1);
     // 6 = 2 + fat node records (a node and both children in 32 B: one dependent load per two
@@ -162,9 +159,7 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 43 / 44 = 40 / 42 with the short division in the shadow trace too: 358.2 -> 356.4 ms, nanobox
     // 163.7 -> 162.4 ms; 49 = 43 with the compressed leaf cull records (round 5: 48 B per leaf, three
     // loads instead of six): 2179 -> 2252 Mray/s at the driver's command, shadow 41.7 -> 40.0 ms
-    A.variant = c->variant >= 0 ? c->variant
-                : c->kernel == 2 ? (c->n_tris >= LEAF_CULL_MIN_TRIS ? 49 : 44)
-                                 : 0;
+    A.variant = c->variant >= 0 ? c->variant : (c->n_tris >= LEAF_CULL_MIN_TRIS ? 49 : 44);
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
@@ -212,20 +207,16 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
     }
     if (c->kernel == 2 && !c->full_counters && !cr::wf_variant_available(A.variant))
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
-                                         " is not compiled in (make ALL_VARIANTS=1)");
-    if (c->kernel == 2 && !c->full_counters && cr::wf_variant_quad(A.variant) && !c->S.quad)
-        return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
-                                         " needs the two-level node records, which this scene's leaves do not fit");
+                                         " does not exist (DESIGN.md §3 lists the measured builds that were removed)");
     if (c->perf_counters && (c->kernel != 2 || c->full_counters || !cr::wf_perf_available(A.variant)))
         return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18 and 26 only, "
                                      "without the counting build");
     c->last_build = c->kernel == 2 ? (c->full_counters ? -1 : A.variant) : -2;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
-    if (c->kernel == 0 || c->kernel == 2) {
-        const bool wf = c->kernel == 2;
+    {
+        const bool wf = true; // (the wavefront path tracer is the render kernel)
         uint32_t blk, blocks;
-        if (wf) cr::wf_trace_geometry(c->full_counters ? -1 : A.variant, c->num_cus, blk, blocks);
-        else cr::persistent_geometry(c->num_cus, c->waves_per_cu, blk, blocks);
+        cr::wf_trace_geometry(c->full_counters ? -1 : A.variant, c->num_cus, blk, blocks);
         A.gstride = blk * blocks;
         // samples per chunk: the per-sample buffer stays within SAMPLE_BUF_BYTES
         // and the work index within 31 bits
@@ -240,10 +231,9 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         if (nl > 1 && chunked) return fail(c, CR_E_INVALID, "layers per pass: the samples do not fit one buffer");
         // wavefront: a second stack-overflow area for the closest trace that runs beside a
         // shadow trace, per lane
-        if (cr::persistent_gstack_bytes(c->stack_depth, A.gstride) >= (1ull << 32)) // (gstack_at's 32-bit offsets)
+        if (cr::gstack_bytes(c->stack_depth, A.gstride) >= (1ull << 32)) // (gstack_at's 32-bit offsets)
             return fail(c, CR_E_INVALID, "stack-overflow area above 4 GiB");
-        if (int r = grow(c, &c->d_gstack, c->gstack_bytes,
-                         (wf ? 2 * c->wf_lanes : 1) * cr::persistent_gstack_bytes(c->stack_depth, A.gstride)))
+        if (int r = grow(c, &c->d_gstack, c->gstack_bytes, 2 * c->wf_lanes * cr::gstack_bytes(c->stack_depth, A.gstride)))
             return r;
         // large renders reserve the whole sample budget at once: a later pass of another shape (a pass
         // group's frame piece, cr_render_layers) then reuses the buffer instead of regrowing it
@@ -259,8 +249,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         A.run = (float *)c->d_run;
         cr::WfArgs W{};
         cr::WfArgs W2{};
-        const int lanes = wf ? c->wf_lanes : 1;
-        if (wf) {
+        const int lanes = c->wf_lanes;
+        {
             // path slots per wavefront chunk, and the queues / state carved from one buffer
             // per lane ... at most ~45% of the currently free HBM in all (the buffers are
             // reused, so only a growth needs the headroom).  Two lanes: two chunks in flight,
@@ -314,12 +304,12 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             // bytes of the buffers of a chunk of Pn paths with kb-bit sort keys
             auto need_for = [&](uint64_t Pn, int kb) -> size_t {
                 const uint64_t Qn = Pn + spare_for(Pn);
-                const size_t st = sort ? cr::wf_sort_tmp_bytes((uint32_t)Qn, kb, c->wf_sort_lib != 0) : 0;
+                const size_t st = sort ? cr::wf_sort_tmp_bytes((uint32_t)Qn, kb) : 0;
                 return (4 + 2 + 2) * 16 * (size_t)Qn + 8 * (size_t)Qn +
-                       (cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 13 * (size_t)Pn +
+                       (cr::WF_STATE + 2 * (size_t)p->k) * 16 * (size_t)Pn + 9 * (size_t)Pn +
                        (sort ? 32 * (size_t)Qn + st : 0) + cr::WF_CNT * sizeof(uint32_t) + 8192;
             };
-            const size_t sort_tmp = sort ? cr::wf_sort_tmp_bytes((uint32_t)Q, key_bits, c->wf_sort_lib != 0) : 0;
+            const size_t sort_tmp = sort ? cr::wf_sort_tmp_bytes((uint32_t)Q, key_bits) : 0;
             const size_t need = need_for(P, key_bits);
             // a chunk of more than a quarter of the path cap reserves the buffers of a whole-cap chunk
             // with the widest keys, so passes of other sizes (a pass group's frame pieces, the next
@@ -353,14 +343,11 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.shade_block = (uint32_t)c->wf_shade_block;
                 W.cnt = (uint32_t *)take(cr::WF_CNT * sizeof(uint32_t));
                 W.cxy = (float2 *)take(8 * (size_t)P);
-                W.ended = (uint32_t *)take(4 * (size_t)P);
                 W.mark = (uint8_t *)take((size_t)P);
-                W.fold = c->wf_fold;
                 W.shade_waves = c->wf_shade_waves;
                 W.sort = sort && nkeys <= (1ull << 32);
                 W.key_bits = key_bits;
                 W.key_bits_pixel = key_bits_pixel;
-                W.sort_lib = c->wf_sort_lib;
                 W.sort_min = c->wf_sort_min;
                 W.sort_tile = c->wf_sort_tile;
                 W.dir_res = leaf_keys ? dres_l : c->wf_dir_res;
@@ -379,7 +366,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.cam_fused = c->wf_cam_fuse;
                 W.ctl_ray = c->wf_ctl_ray;
                 W.vis_dw = c->wf_vis_dw;
-                W.vis_mark = c->wf_vis_mark && !c->wf_fold && !c->wf_tail_overlap && p->k <= 63 ? 1 : 0;
+                W.vis_mark = c->wf_vis_mark && !c->wf_tail_overlap && p->k <= 63 ? 1 : 0;
                 W.nee_skip = c->wf_nee_skip;
                 W.tail_waves = c->wf_tail_waves;
                 if (sort) {
@@ -399,10 +386,6 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             };
             carve(c->d_wf, W, 0);
             if (lanes == 2) carve(c->d_wf2, W2, 1);
-        } else {
-            if (int r = grow(c, &c->d_pathbuf, c->pathbuf_bytes, cr::persistent_pathbuf_bytes(p->k, A.gstride)))
-                return r;
-            A.pathbuf = (float4 *)c->d_pathbuf;
         }
         // screen-space cull boxes of this camera for the camera-ray trace (camcull.hpp),
         // computed inside the timed region of every render
@@ -427,11 +410,11 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
             A.s_count = (uint32_t)std::min<uint64_t>(chunk, spp_pass - s0);
             A.n_work = A.n_items * A.s_count;
             int e = 0;
-            if (wf && lanes == 2) {
+            if (lanes == 2) {
                 cr::WfLane L[2] = {{W, st, c->wfs.side, c->wfs.fork, c->wfs.join, c->lane_ev[0], c->hcnt},
                                    {W2, c->stream2, c->side2, c->fork2, c->join2, c->lane_ev[1], c->hcnt + 2}};
                 e = cr::run_wavefront_lanes(A, L, 2, c->num_cus, st, &c->tev);
-            } else if (wf) {
+            } else {
                 const uint32_t P = W.P;
                 for (uint32_t w0 = 0; w0 < A.n_work && !e; w0 += P) {
                     W.w0 = w0;
@@ -440,19 +423,10 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                     e = cr::launch_wavefront_chunk(A, W, c->num_cus, st, c->wfs, &c->tev);
                 }
                 W.P = P;
-            } else {
-                HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
-                e = cr::launch_persistent(A, c->waves_per_cu, c->num_cus, st);
             }
             if (!e) e = cr::launch_sum_samples(A, s0 == 0, s0 + A.s_count == spp_pass, st, c->sum_lds, c->sum_staged != 0);
             if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
         }
-        HIPCHK(hipEventRecord(c->ev1, st));
-    } else {
-        HIPCHK(hipMemsetAsync(c->d_work, 0, 16 * sizeof(uint32_t), st));
-        HIPCHK(hipEventRecord(c->ev0, st));
-        int e = cr::launch_render(A, c->kernel, c->block, c->waves_per_cu, c->num_cus, st);
-        if (e) return hip_fail(c, (hipError_t)e, "render kernel launch");
         HIPCHK(hipEventRecord(c->ev1, st));
     }
     unsigned long long h[cr::CTR_SLOTS];
@@ -520,8 +494,7 @@ cr_ctx *cr_create(int device) {
         hipEventCreateWithFlags(&c->lane_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&c->hcnt, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counters, cr::CTR_SLOTS * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->d_work, 16 * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc(&c->d_counters, cr::CTR_SLOTS * sizeof(unsigned long long)) != hipSuccess) {
         c->err = "device init failed";
         c->device = -1;
     }
@@ -536,14 +509,12 @@ void cr_destroy(cr_ctx *c) {
         free_scene(c);
         if (c->d_accum) hipFree(c->d_accum);
         if (c->d_gstack) hipFree(c->d_gstack);
-        if (c->d_pathbuf) hipFree(c->d_pathbuf);
         if (c->d_samples) hipFree(c->d_samples);
         if (c->d_run) hipFree(c->d_run);
         if (c->d_wf) hipFree(c->d_wf);
         if (c->d_cull) hipFree(c->d_cull);
         if (c->d_cull_node) hipFree(c->d_cull_node);
         if (c->d_counters) hipFree(c->d_counters);
-        if (c->d_work) hipFree(c->d_work);
         if (c->ev0) hipEventDestroy(c->ev0);
         for (int i = 0; i < 2 * c->tev.cap; i++) hipEventDestroy(c->tev.ev[i]);
         delete[] c->tev.ev;
@@ -648,8 +619,7 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
     // load_rec addresses records with a 32-bit byte offset
     if ((uint64_t)16 * cr::REC_STRIDE * ((uint64_t)d->n_refs + 1) > 0xFFFFFFFFull)
         return fail(c, CR_E_INVALID, "more than 89 M leaf references (triangle records exceed 4 GiB)");
-    // + one zero record past the last: the paired scalar loads of uniform leaves
-    // (trace build 13) may read the record after a leaf's last one
+    // + one zero record past the last (an empty leaf's `first` may be n_refs)
     std::vector<float4> recs((size_t)cr::REC_STRIDE * ((size_t)d->n_refs + 1), make_float4(0.f, 0.f, 0.f, 0.f));
     for (uint32_t r = 0; r < d->n_refs; r++) {
         const uint32_t t = d->refs[r];
@@ -662,27 +632,9 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         q[1] = make_float4(p[3] - p[0], p[4] - p[1], p[5] - p[2], 0.f);
         q[2] = make_float4(p[6] - p[0], p[7] - p[1], p[8] - p[2], 0.f);
     }
-    // plane records (planecull.hpp) for rays of unit length inside the padded box: Db bounds
-    // every coordinate of an origin (a hit point + 0.001 * normal) or vertex, Tb the segment
-    std::vector<float4> planes((size_t)d->n_refs + 3, make_float4(0.f, 0.f, 0.f, 0.f));
-    {
-        double Db = 0.0, diag = 0.0;
-        for (int i = 0; i < 3; i++) {
-            Db = std::max(Db, std::max(std::fabs((double)d->box_min[i]), std::fabs((double)d->box_max[i])));
-            diag += ((double)d->box_max[i] - d->box_min[i]) * ((double)d->box_max[i] - d->box_min[i]);
-        }
-        Db += 1.0;
-        const double Tb = 1.01 * std::sqrt(diag) + 2.0;
-        for (uint32_t r = 0; r < d->n_refs; r++) {
-            const float4 *q = recs.data() + (size_t)cr::REC_STRIDE * r;
-            const float a[3] = {q[0].x, q[0].y, q[0].z}, e1[3] = {q[1].x, q[1].y, q[1].z},
-                        e2[3] = {q[2].x, q[2].y, q[2].z};
-            float o[4];
-            cr::plane_record(a, e1, e2, Db, Tb, o);
-            planes[r] = make_float4(o[0], o[1], o[2], o[3]);
-        }
-    }
-    // leaf cull records (leafcull.hpp), per node of the new numbering; host threads
+    // leaf cull records (leafcull.hpp), per node of the new numbering; host threads.  The per-ray and
+    // fixed-pad forms stay on the host: they are the steps from which the packed (LC 4) and the
+    // compressed (LC 5) records the traces read are derived
     std::vector<float4> lcull((size_t)cr::LC_REC * NN, make_float4(0.f, 0.f, 0.f, 0.f));
     {
         const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -733,41 +685,6 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
                                (const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
                                (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u, lcg,
                                (uint32_t *)(lcullc.data() + (size_t)cr::LC_RECC * i));
-    // ... and in 32 B per node (LC 6, build 51 of make ALL_VARIANTS=1: the same grid and boxes, the cone and
-    // dt constants in 13 bits a group)
-#ifdef CR_ALL_VARIANTS
-    std::vector<uint4> lculls((size_t)cr::LC_RECS * NN, make_uint4(0u, 0u, 0u, 0u));
-#else
-    std::vector<uint4> lculls;
-#endif
-    for (uint32_t i = 0; i < (uint32_t)(lculls.size() / cr::LC_RECS); i++)
-        cr::leaf_cull_compress_s((const cr::LcFloat4 *)(lcull.data() + (size_t)cr::LC_REC * i),
-                                 (const cr::LcFloat4 *)(lcullf.data() + (size_t)cr::LC_REC * i),
-                                 (nodes[i].y & 3u) == 3u ? nodes[i].y >> 2 : 0u, lcg,
-                                 (uint32_t *)(lculls.data() + (size_t)cr::LC_RECS * i));
-    // two-level node records (quadnodes.hpp) and the packed cull records by first reference, for trace builds
-    // 46 / 47 (make ALL_VARIANTS=1: measured slower, wavefront.hip kWf); a scene whose leaves do not fit the
-    // records' words, or whose per-reference cull table would pass 4 GiB, keeps the fat-record builds only
-    // (S.quad null)
-    cr::QuadLayout ql;
-    std::string qerr;
-#ifdef CR_ALL_VARIANTS
-    const bool quad_ok = (uint64_t)16 * cr::LC_RECP * ((uint64_t)d->n_refs + 1) <= 0xFFFFFFFFull &&
-                         cr::quad_build((const cr::QuadNode *)nodes.data(), NN, d->n_refs, ql, qerr);
-#else
-    const bool quad_ok = false;
-#endif
-    std::vector<uint4> quad;
-    std::vector<float4> lcullq;
-    if (quad_ok) {
-        quad.resize(ql.slots);
-        std::memcpy(quad.data(), ql.rec.data(), 16 * (size_t)ql.slots);
-        lcullq.assign((size_t)cr::LC_RECP * ((size_t)d->n_refs + 1), make_float4(0.f, 0.f, 0.f, 0.f));
-        for (uint32_t i = 0; i < NN; i++)
-            if ((nodes[i].y & 3u) == 3u && (nodes[i].y >> 2))
-                std::memcpy(lcullq.data() + (size_t)cr::LC_RECP * nodes[i].x, lcullp.data() + (size_t)cr::LC_RECP * i,
-                            16 * cr::LC_RECP);
-    }
     std::vector<float4> tri((size_t)3 * nt), mn(nt), mkd(nt), mke(nt);
     std::vector<float2> muv((size_t)3 * nt);
     for (uint32_t t = 0; t < nt; t++) {
@@ -846,15 +763,14 @@ int cr_upload_scene(cr_ctx *c, const cr_scene_desc *d) {
         free_scene(c);
         return rc;
     }
-    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) || (rc = upload(c, planes, &c->S.planes)) || (rc = upload(c, lcull, &c->S.lcull)) || (rc = upload(c, lcullf, &c->S.lcullf)) || (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, lcullc, &c->S.lcullc)) || (rc = upload(c, lculls, &c->S.lculls)) || (rc = upload(c, tri, &c->S.tri)) ||
+    if ((rc = upload(c, nodes, &c->S.nodes)) || (rc = upload(c, fat, &c->S.fat)) || (rc = upload(c, recs, &c->S.recs)) ||
+        (rc = upload(c, lcullp, &c->S.lcullp)) || (rc = upload(c, lcullc, &c->S.lcullc)) || (rc = upload(c, tri, &c->S.tri)) ||
         (rc = upload(c, mn, &c->S.mat_n)) || (rc = upload(c, mkd, &c->S.mat_kd)) || (rc = upload(c, mke, &c->S.mat_ke)) ||
         (rc = upload(c, muv, &c->S.mat_uv)) || (rc = upload(c, lights, &c->S.lights)) ||
-        (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels)) ||
-        (quad_ok && ((rc = upload(c, quad, &c->S.quad)) || (rc = upload(c, lcullq, &c->S.lcullq))))) {
+        (rc = upload(c, texs, &c->S.texs)) || (rc = upload(c, texels, &c->S.texels))) {
         free_scene(c);
         return rc;
     }
-    c->S.qfbits = quad_ok ? ql.fbits : 0u;
     c->S.lcg = lcg;
     c->S.nlights = d->n_lights;
     c->S.n_nodes = d->n_nodes;
@@ -1248,8 +1164,9 @@ int cr_get_perf(cr_ctx *c, uint64_t *out, int n) {
 
 int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     if (!c || !key) return CR_E_INVALID;
-    const int64_t nvar = std::max(cr::num_persistent_variants(), cr::num_wf_variants());
-    if (!std::strcmp(key, "kernel") && (v == 0 || v == 1 || v == 2)) c->kernel = (int)v;
+    const int64_t nvar = cr::num_wf_variants();
+    // (the megakernel (0) and the thread-per-pixel kernel (1) were measured slower and removed: DESIGN.md §3)
+    if (!std::strcmp(key, "kernel") && v == 2) c->kernel = (int)v;
     else if (!std::strcmp(key, "counters") && (v == 0 || v == 1)) c->full_counters = (int)v;
     else if (!std::strcmp(key, "perf_counters") && (v == 0 || v == 1)) c->perf_counters = (int)v;
     else if (!std::strcmp(key, "wf_tail_overlap") && (v == 0 || v == 1)) c->wf_tail_overlap = (int)v;
@@ -1281,8 +1198,6 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "desc_quorum") && v >= -1 && v <= 64) c->desc_quorum = (int)v;
     else if (!std::strcmp(key, "comm_timeout_ms") && v >= 1 && v <= 3600000) c->comm_timeout_ms = (uint32_t)v;
     else if (!std::strcmp(key, "variant") && v >= -1 && v < nvar) c->variant = (int)v; // -1 default; clamped per kernel
-    else if (!std::strcmp(key, "block") && (v == 0 || v == 64 || v == 128 || v == 256)) c->block = (uint32_t)v;
-    else if (!std::strcmp(key, "waves_per_cu") && v >= 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
     else if (!std::strcmp(key, "refill") && v >= 0 && v <= 64) c->refill = (uint32_t)v; // 0: per-kernel default
     else if (!std::strcmp(key, "refill_shadow") && v >= 0 && v <= 64) c->refill_shadow = (uint32_t)v;
     else if (!std::strcmp(key, "refill_camera") && v >= 0 && v <= 64) c->refill_camera = (uint32_t)v;
@@ -1297,16 +1212,10 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_dir_res_shadow") && v >= 0 && v <= 256 && (v & (v - 1)) == 0)
         c->wf_dir_res_shadow = (uint32_t)v;
     else if (!std::strcmp(key, "wf_paths") && v >= 4096 && v <= (1ll << 30)) c->wf_paths = (uint32_t)v;
-#ifdef CR_SORT_LIB
-    else if (!std::strcmp(key, "wf_sort_lib") && (v == 0 || v == 1)) c->wf_sort_lib = (int)v;
-#else
-    else if (!std::strcmp(key, "wf_sort_lib") && v == 0) c->wf_sort_lib = 0; // (1: make SORT_LIB=1)
-#endif
     else if (!std::strcmp(key, "wf_lanes") && (v == 1 || v == 2)) c->wf_lanes = (int)v;
     else if (!std::strcmp(key, "wf_xcd") && v >= 0 && v <= 7) c->wf_xcd = (uint32_t)v;
     else if (!std::strcmp(key, "wf_leaf_keys") && (v == 0 || v == 1)) c->wf_leaf_keys = (int)v;
     else if (!std::strcmp(key, "wf_resolve_paths") && v >= 0 && v <= 64) c->wf_resolve_paths = (uint32_t)v;
-    else if (!std::strcmp(key, "wf_fold") && v >= 0 && v <= 2) c->wf_fold = (int)v;
     else if (!std::strcmp(key, "wf_shade_waves") && (v == 6 || v == 8)) c->wf_shade_waves = (int)v;
     else if (!std::strcmp(key, "wf_shade_block") && (v == 256 || v == 512 || v == 1024)) c->wf_shade_block = (int)v;
     else if (!std::strcmp(key, "wf_app_chunk") && (v == 0 || (v >= 256 && v <= 65536 && !(v & (v - 1))))) c->wf_app_chunk = (int)v;

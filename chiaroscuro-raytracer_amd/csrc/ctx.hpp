@@ -43,11 +43,10 @@ struct cr_ctx {
     std::vector<void *> scene_bufs;
     // work buffers
     unsigned long long *d_counters = nullptr;
-    uint32_t *d_work = nullptr;
     float *d_accum = nullptr;
     size_t accum_elems = 0;
-    void *d_gstack = nullptr, *d_pathbuf = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
-    size_t gstack_bytes = 0, pathbuf_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
+    void *d_gstack = nullptr, *d_samples = nullptr, *d_run = nullptr, *d_wf = nullptr;
+    size_t gstack_bytes = 0, samples_bytes = 0, run_bytes = 0, wf_bytes = 0;
     void *d_cull = nullptr;  // camera-ray cull boxes, one per leaf reference (+ 4), per render
     size_t cull_bytes = 0;
     void *d_cull_node = nullptr; // ... their per-leaf unions, one per kd node
@@ -58,7 +57,7 @@ struct cr_ctx {
     // options
     // Defaults from sweeps on MI355X, sponza stand-in 1080p x 128 spp:
     //   wavefront (kernel 2), trace variant 9, refill 64/56/48, sorted queues, tail below 1M rays
-    //   persistent megakernel (kernel 0), variant 0, refill 16:                615 Mray/s
+    //   (the persistent megakernel, kernel 0: 615 Mray/s; one thread per pixel, kernel 1: ~60; both removed)
     int kernel = 2;
     int full_counters = 1;
     int lc_debug = 0;                      // measurement only (RenderArgs::lc_debug)
@@ -69,9 +68,7 @@ struct cr_ctx {
     int perf_counters = 0;                 // RenderArgs::perf_counters (option "perf_counters")
     unsigned long long last_perf[cr::TK_N * cr::PERF_N] = {};
     int variant = -1;       // -1: the kernel's default build
-    uint32_t block = 0;
-    uint32_t waves_per_cu = 0;
-    uint32_t refill = 0;    // 0: the kernel's default (16 megakernel, 48 wavefront)
+    uint32_t refill = 0;    // 0: the default (48)
     uint32_t refill_shadow = 0; // wavefront shadow trace; 0: refill if set, else 56
     uint32_t refill_camera = 0; // wavefront generation-1 closest trace; 0: refill if set, else 64
     uint32_t wf_paths = 256u << 20; // wavefront: paths in flight per chunk (capped by free HBM)
@@ -119,7 +116,6 @@ struct cr_ctx {
     // render whose n_items * 12 B * spp exceeds it runs in sample chunks whose running sum
     // carries over in d_run (sum_samples) -- the 4K x 100 spp batches of C5 do
     uint64_t sample_buf = cr::SAMPLE_BUF_BYTES;
-    int wf_sort_lib = 0;              // 1: hipcub's radix sort for the queues (comparison)
     int wf_lanes = 1;                 // wavefront chunks in flight at once (1 or 2)
     // XCD-partitioned queues (WfArgs::xcd bits: 1 shadow, 2 secondary closest, 4 camera rays);
     // sponza 1080p x 128 spp, 2 interleaved rounds: 0 / 1 / 3 / 7 -> 435.1 / 432.4 / 431.4 / 423.1 ms
@@ -132,12 +128,6 @@ struct cr_ctx {
     uint32_t wf_leaf_shift = 1; // ... its node index >> this (a leaf and its sibling share a key region)
     // sweep (1080p x 128 spp, 2 rounds): 0 / 1 / 2 / 4 / 8 / 16 / 64 -> 399.2 / 394.6 / 394.8 / 394.8 / 393.8 / 393.6 / 394.5 ms
     uint32_t wf_resolve_paths = 16; // wf_resolve in path order for queues of at least P / this rays (0: never)
-    // WfArgs::fold: 0 wf_resolve's path-order sweep per generation; 1 / 2 lists instead of the sweep
-    // (round 4, bit-exact, slower: 1080p x 128 spp in pass groups, two interleaved rounds, ms per layer:
-    // sweep 322.9 / 323.4, fold 1 (continuing paths resolved in the next wf_shade) 324.5 / 324.6;
-    // sweep 322.5 / 322.9, fold 2 (resolved beside the closest trace from its queue) 325.6 / 325.3 --
-    // the sweep runs beside the closest trace of g + 1, off the critical path, and reads in path order)
-    int wf_fold = 0;
     // WfArgs::shade_waves (option "wf_shade_waves": 6 or 8); round 4, two interleaved rounds: sponza
     // 322.5 / 322.9 vs 322.6 / 322.2 ms per layer, cornell_box 108.4 / 108.7 vs 107.6 / 107.3 ms per pass
     int wf_shade_waves = 8;

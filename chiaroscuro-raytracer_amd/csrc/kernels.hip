@@ -1,16 +1,7 @@
-// kernels.hip -- CDNA4 (gfx950) kernels of the Chiaroscuro render loop:
-// the one-thread-per-pixel baseline render kernel, the ray-query kernels behind
-// cr_intersect / cr_intersect_shadow, the root-side tile blend, and the launch
-// dispatch (the persistent render kernel lives in persistent.hip).
-//
-// Hot path:
-//   camera sample (src/rayTracer.cpp:58-62) -> closest-hit kd traversal
-//   (src/kdtree.cpp:210-281) -> hit reconstruction (src/rayTracer.cpp:137-169)
-//   -> NEE light pick + shadow traversal (src/rayTracer.cpp:89-111,
-//   src/kdtree.cpp:283-344) -> Diffuse::sample_wi + Russian roulette
-//   (src/rayTracer.cpp:113-132, src/brdf.cpp:57-79) -> next bounce.
-// The reference's recursion `direct + w * sendRay(...)` is evaluated back to
-// front from per-bounce (direct, w) pairs so the float result is identical.
+// kernels.hip -- CDNA4 (gfx950) kernels around the render loop: the ray-query kernel behind
+// cr_intersect / cr_intersect_shadow (KDTree::intersectRay / intersectShadowRay, one query per
+// thread with the reference's recursion as an LDS stack), the root-side tile blend and the tonemap.
+// The render loop itself is the wavefront path tracer (wavefront.hip), its sample sum samples.hip.
 //
 // Layout in HBM (built by cabi.cpp):
 //   nodes  : uint2 per kd node {split bits | first ref, axis | child<<2 (axis 3 = leaf, count<<2)}
@@ -105,89 +96,6 @@ __device__ __forceinline__ bool traverse(const DevScene &S, const Stack &stk, f3
     }
 }
 
-// One camera path; RayTracer::sendRay (src/rayTracer.cpp:76-135) unrolled with
-// the (direct, w) pairs in registers.
-template <int MAXK>
-__device__ f3 trace_path(const RenderArgs &A, const Stack &stk, uint32_t x, uint32_t y, uint32_t sample, Ctr &c) {
-    const DevScene &S = A.S;
-    Rng rng = rng_make(A.seed, A.layer, y * A.xres + x, sample);
-    f3 origin = mk(A.cam[0], A.cam[1], A.cam[2]);
-    f3 dir = camera_dir(A, x, y, rng);
-    f3 D[MAXK], W[MAXK];
-    int k = 1;
-    f3 tail;
-    c.paths++;
-    for (;;) {
-        uint32_t t = 0;
-        float bx = 0.f, by = 0.f, dist = 0.f;
-        c.closest++;
-        if (!traverse<false>(S, stk, origin, dir, 0.f, 0xffffffffu, t, bx, by, dist, c)) {
-            tail = mk(A.bg[0], A.bg[1], A.bg[2]);
-            break;
-        }
-        c.hit++;
-        HitShade h = shade_hit(S, origin, t, bx, by, k);
-        if (h.textured) c.texhit++;
-        if (S.nlights) {
-            const Nee n = sample_light(S, h.p, h.normal, h.fcol, rng);
-            c.shadow++;
-            uint32_t dt;
-            float d0, d1, d2;
-            if (!traverse<true>(S, stk, n.origin, n.dir, n.distance, n.light, dt, d0, d1, d2, c))
-                h.direct = add(h.direct, n.contrib);
-        }
-        if (k == A.K) {
-            tail = h.direct;
-            break;
-        }
-        const float sx = rng_uniform(rng, -1.f, 1.f);
-        const float sy = rng_uniform(rng, -1.f, 1.f);
-        f3 wi;
-        float pdf;
-        sample_wi(h.normal, sx, sy, wi, pdf);
-        const float Kmax = std_max(std_max(h.fcol.x, h.fcol.y), h.fcol.z);
-        if (pdf == 0.f || rng_uniform(rng, 0.f, 1.f) > Kmax) {
-            tail = h.direct;
-            break;
-        }
-        const float cosine = fabsf(dot(h.normal, wi));
-        const f3 w = divs(muls(h.fcol, cosine), pdf * Kmax);
-#pragma unroll
-        for (int j = 0; j < MAXK; j++)
-            if (j == k - 1) {
-                D[j] = h.direct;
-                W[j] = w;
-            }
-        origin = add(h.p, muls(h.normal, 0.001f));
-        dir = wi;
-        k++;
-    }
-    f3 acc = tail; // back-to-front fold: r_j = D_j + W_j * r_{j+1}
-#pragma unroll
-    for (int j = MAXK - 1; j >= 0; j--)
-        if (j < k - 1) acc = add(D[j], mul(W[j], acc));
-    return acc;
-}
-
-// Kernel 1: one thread per pixel, sample loop in the thread (the reference's loop
-// nest, rayTracer.cpp:56-62).  Baseline the persistent kernel is measured against.
-template <int MAXK>
-__global__ void __launch_bounds__(128) render_simple(RenderArgs A) {
-    extern __shared__ uint32_t lds[];
-    const uint32_t depth = A.stack_depth;
-    Stack stk{lds, (float *)(lds + depth * blockDim.x), (float *)(lds + 2 * depth * blockDim.x), blockDim.x};
-    Ctr c = {};
-    const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t x, y;
-    if (item < A.n_items && item_pixel(A, item, x, y)) {
-        f3 temp = mk(0.f, 0.f, 0.f);
-        for (uint32_t s = 0; s < A.spp; s++) temp = add(temp, trace_path<MAXK>(A, stk, x, y, s, c));
-        write_pixel(A, x, y, item, temp);
-        c.pixels++;
-    }
-    flush_counters(A.counters, c);
-}
-
 // Ray-query kernel (cr_intersect / cr_intersect_shadow).
 __global__ void __launch_bounds__(128) intersect_kernel(QueryArgs Q) {
     extern __shared__ uint32_t lds[];
@@ -267,21 +175,6 @@ __global__ void __launch_bounds__(256) tonemap_kernel(TonemapArgs T) {
 }
 
 // ---------------------------------------------------------------- launch --
-int launch_render(const RenderArgs &A, int kernel, uint32_t block, uint32_t waves_per_cu, int num_cus,
-                  hipStream_t st) {
-    if (kernel == 0) return launch_persistent(A, waves_per_cu, num_cus, st);
-    (void)block;
-    const uint32_t blk = 128;
-    const size_t lds = (size_t)3 * A.stack_depth * blk * sizeof(uint32_t);
-    const uint32_t grid = (A.n_items + blk - 1) / blk;
-    if (grid == 0) return 0;
-    if (A.K <= 8)
-        hipLaunchKernelGGL(render_simple<8>, dim3(grid), dim3(blk), lds, st, A);
-    else
-        hipLaunchKernelGGL(render_simple<64>, dim3(grid), dim3(blk), lds, st, A);
-    return (int)hipGetLastError();
-}
-
 int launch_intersect(const QueryArgs &Q, hipStream_t st) {
     const uint32_t block = 128;
     const size_t lds = (size_t)3 * Q.stack_depth * block * sizeof(uint32_t);

@@ -87,24 +87,11 @@ struct DevScene {
     // {e2 = C-A, 0} -- bitwise what the reference computes per test.  (A 40-B SoA
     // split measured 15% slower: three cache lines per test instead of one or two.)
     const float4 *recs;
-    // one per leaf reference (+ 3 padding): the triangle's plane scaled by its rounding
-    // margin (planecull.hpp), the exact pre-test of the secondary / shadow traces
-    const float4 *planes;
-    // LC_REC (leafcull.hpp) per kd node: a leaf's references in two normal groups, each with
+    // leaf cull records (leafcull.hpp) per kd node: a leaf's references in two normal groups, each with
     // its box and normal cone -- the exact skip of the tests a unit-direction ray cannot pass
-    const float4 *lcull;
-    const float4 *lcullf; // the same records in the fixed-pad form (leaf_cull_fixed, trace builds with LC 3)
-    const float4 *lcullp; // ... packed (LC_RECP float4 per node, leaf_cull_pack, LC 4)
-    const uint4 *lcullc;  // ... compressed (LC_RECC uint4 per node on grid lcg, leaf_cull_compress, LC 5)
-    const uint4 *lculls;  // ... short compressed (LC_RECS uint4 per node on grid lcg, leaf_cull_compress_s, LC 6)
+    const float4 *lcullp; // packed (LC_RECP float4 per node, leaf_cull_pack, LC 4)
+    const uint4 *lcullc;  // compressed (LC_RECC uint4 per node on grid lcg, leaf_cull_compress, LC 5)
     LcGrid lcg;
-    // two-level node records (quadnodes.hpp: {w_n, w_c0, w_c1, meta} per slot; null when the scene's
-    // leaves do not fit their words) and the packed leaf cull records indexed by a leaf's FIRST
-    // reference (LC_RECP float4 per reference, only leaves' firsts filled: the QUAD traces' leaves carry
-    // their first reference, not a node id); a quad leaf word is first | count << qfbits
-    const uint4 *quad;
-    const float4 *lcullq;
-    uint32_t qfbits;
     float db;             // bound on |coordinate| of any origin or vertex (padded box + 1)
     const float4 *tri;    // 3 per triangle: A, B, C
     const float4 *mat_n;  // normal, w = emissive flag bits
@@ -145,14 +132,11 @@ struct RenderArgs {
     int mode;
     float *out;
     unsigned long long *counters; // 9 x u64
-    uint32_t *work;               // persistent-kernel work counter (zeroed per launch)
-    // persistent kernel only
     uint2 *gstack;                // traversal-stack overflow [stack_depth][gstride] {node, tmax bits}
-    float4 *pathbuf;              // per-bounce (direct, w) [2*K][gstride]
-    uint32_t gstride;             // threads in the persistent grid
+    uint32_t gstride;             // threads in the persistent trace grid
     int full_counters;            // 1: also count inner/leaf/tritest (SURVEY §8d bytes)
     int perf_counters;            // 1: the default build's kernels with performed-work counts (CTR_PERF)
-    int variant;                  // persistent-kernel variant index (kernels.hip kVariants)
+    int variant;                  // wavefront trace build (wavefront.hip kWf)
     uint32_t refill;              // idle lanes of a wave that trigger a path-state step / ray fetch
     uint32_t refill_shadow;       // wavefront shadow-trace kernel's threshold
     uint32_t refill_camera;       // wavefront closest trace of generation 1 (camera rays)
@@ -175,20 +159,11 @@ struct RenderArgs {
     uint32_t desc_quorum;         // lean wavefront traces: a round's descent stops once at most desc_quorum / 64
                                   // of its lanes still descend (they go on next round); 0: every lane reaches a leaf
 };
-int num_persistent_variants();
-
-// Workspace the persistent kernel needs for a grid of `threads` lanes:
-// stack overflow [depth][threads] x 8 B; lane buffer = PARK_SLOTS parked-state
-// float4s + (direct, w) float4 pairs per bounce, each [slot][threads].
-enum { PARK_SLOTS = 4 };
-inline size_t persistent_gstack_bytes(uint32_t depth, uint32_t threads) { return (size_t)depth * threads * 8; }
-inline size_t persistent_pathbuf_bytes(int K, uint32_t threads) {
-    return (size_t)(PARK_SLOTS + 2 * K) * threads * 16;
-}
+// Traversal-stack overflow area of a persistent trace grid of `threads` lanes: [depth][threads] x 8 B.
+inline size_t gstack_bytes(uint32_t depth, uint32_t threads) { return (size_t)depth * threads * 8; }
 // Sample buffer budget: a render is split into sample chunks whose per-sample
 // buffer fits in this many bytes (whole 1080p x 128 spp frames fit in one).
 enum : uint64_t { SAMPLE_BUF_BYTES = 4ull << 30 };
-int launch_persistent(const RenderArgs &A, uint32_t waves_per_cu, int num_cus, hipStream_t st);
 // Per-pixel in-order sum of one chunk's samples; `last` blends / writes the pixel.
 int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t st, uint32_t lds = 0, bool staged = true);
 
@@ -196,7 +171,7 @@ int launch_sum_samples(const RenderArgs &A, bool first, bool last, hipStream_t s
 // work items [w0, w0 + P) advance one bounce per generation through separate
 // kernels (camera, closest trace, shade, shadow trace, bounce) that exchange
 // rays through queues in HBM.
-// counters: closest count [g], shadow count [WF_G+g], work [2*WF_G+g], [3*WF_G+g], ended paths [4*WF_G+g];
+// counters: closest count [g], shadow count [WF_G+g], work [2*WF_G+g], [3*WF_G+g], (unused) [4*WF_G+g];
 // g <= K + 1 <= 65;
 // then the per-XCD work counters of the partitioned queues (WfArgs::xcd), WF_XSTRIDE apart
 // (one 64-B line each): closest [WF_XBASE + (g*8 + x)*WF_XSTRIDE], shadow after WF_G*8 of those
@@ -228,7 +203,6 @@ struct WfArgs {
     int sort;         // 1: write keys and sort the queues of large generations
     int key_bits;     // significant key bits (world keys included)
     int key_bits_pixel; // significant bits of the pixel keys (generation-1 queues): fewer digit passes
-    int sort_lib;     // 1: hipcub's radix sort instead of raysort.hip's (comparison)
     uint32_t sort_min;   // queues shorter than this are traced in append order
     uint32_t sort_tile;  // log2 of the pixel sub-tile edge of the key (3: 8x8 pixels)
     uint32_t dir_res;    // octahedral direction bins per axis (8: 64 bins; power of two)
@@ -260,12 +234,6 @@ struct WfArgs {
     uint32_t dir_res_s; // leaf keys: direction bins per axis of the SHADOW queues' keys
     int key_bits_s;     // significant bits of the shadow queues' keys
     int tail_waves;     // waves per SIMD of the lean tail launch (4, 5, 6)
-    // fold = 1 (option "wf_fold"): no sweep over the paths per generation -- wf_shade(g)
-    // lists the paths whose hit at g ends them (ended, count at cnt[4 WF_G + g]), wf_fold(g) folds
-    // those after the shadow trace, and the paths that continue have their bounce g resolved where
-    // they are read next (wf_shade(g + 1), or wf_tail at pickup).  0 (the default): wf_resolve
-    int fold;
-    uint32_t *ended;    // [P] paths that ended at the generation being folded
     int shade_waves;    // wf_shade's build: 8 waves per SIMD (64 VGPRs, spills) or else its natural 6
     // wf_shade's queue appends in chunks (set per launch by launch_wavefront_chunk): a block reserves
     // app_chunk slots of a queue with one atomic and fills them over its iterations; the unused end of
@@ -291,7 +259,7 @@ struct WfArgs {
     // that bounce (SHADOW_VIS / SHADOW_OCC) instead of occ[slot] -- wf_resolve then reads no occ entries,
     // which a sorted shadow queue scatters over the paths (option "wf_vis_dw")
     int vis_dw;
-    // 1 (option "wf_vis_mark", needs fold 0, no overlapped tail, K <= 63): the resolve marks are
+    // 1 (option "wf_vis_mark", no overlapped tail, K <= 63): the resolve marks are
     // (k << 2) | visible << 1 | ended; wf_shade writes PS3 = direct + contrib (the reference's add for a
     // visible NEE ray, done there) and a mark with visible 0, the shadow trace sets visible for an
     // unoccluded answer (one byte, nothing for an occluded one), and wf_resolve touches only the paths
@@ -303,10 +271,10 @@ struct WfArgs {
     int nee_skip;
 };
 // rays 2x2 float4, hits 2, shadow ray 2, exclude + occ 8 B, state, (direct, w) pairs, 2 x 2 sort keys + perms,
-// camera sample position, ended list, resolve mark
+// camera sample position, resolve mark
 // spare: + 21 for the queue arrays' spare slots of chunked appends, P / 8 of them at 168 B (cabi.cpp spare_for)
 inline size_t wf_bytes_per_path(int K, bool spare) {
-    return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 4 + 1 + (spare ? 21 : 0);
+    return (size_t)(4 + 2 + 2 + WF_STATE + 2 * K) * 16 + 8 + 32 + 8 + 1 + (spare ? 21 : 0);
 }
 // Second stream and fork / join events of a render (shadow trace g beside closest trace g + 1).
 struct WfStreams {
@@ -319,7 +287,6 @@ uint32_t wf_shade_blocks(int num_cus, int shade_waves);
 // true when the variant's camera trace skips Moller-Trumbore tests by the cull boxes
 bool wf_variant_culls(int variant);
 bool wf_variant_available(int variant); // compiled in (the default compile holds builds 0, 15, 18, 26)
-bool wf_variant_quad(int variant);      // its secondary / shadow traces read DevScene::quad
 bool wf_perf_available(int variant);    // a performed-work instance of this trace build exists (18, 26)
 // cull boxes of this render's camera for the nrefs leaf references (+ 4 padding boxes)
 // and their unions per subtree (node_boxes[n_nodes]): leaves first, then the inner
@@ -359,9 +326,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W, int num_cus, hi
 // raysort.hip: stable radix sort of (key, value) pairs; lib: hipcub's instead
 int sort_queue(uint32_t *keys[2], uint32_t *vals[2], uint32_t n, int end_bit, void *tmp, size_t &tmp_bytes,
                hipStream_t st, bool lib = false, bool iota = false, bool keep_keys = true);
-size_t wf_sort_tmp_bytes(uint32_t n, int key_bits, bool lib = false);
-// Persistent grid geometry chosen by launch_render (block threads, blocks).
-void persistent_geometry(int num_cus, uint32_t waves_per_cu, uint32_t &block, uint32_t &blocks);
+size_t wf_sort_tmp_bytes(uint32_t n, int key_bits);
 
 struct QueryArgs {
     DevScene S;
@@ -389,8 +354,6 @@ struct TonemapArgs {
     float m, s, kl, f, defog, gamma;
 };
 
-int launch_render(const RenderArgs &A, int kernel, uint32_t block, uint32_t waves_per_cu, int num_cus,
-                  hipStream_t st);
 int launch_intersect(const QueryArgs &Q, hipStream_t st);
 int launch_blend(const BlendArgs &B, hipStream_t st);
 int launch_tonemap(const TonemapArgs &T, hipStream_t st);

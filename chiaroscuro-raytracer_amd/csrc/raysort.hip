@@ -20,9 +20,9 @@
 // No step waits on another block (no look-back chains): every kernel ends after
 // a fixed amount of work whatever the scheduling.
 // Traffic per pass: 4 B read (upsweep) + 8 B read + 8 B written (downsweep) per pair.
-// The hipcub DeviceRadixSort this replaced is kept as cr_set_option "wf_sort_lib" 1
-// for comparison.
-#ifdef CR_SORT_LIB // (make SORT_LIB=1: hipcub's sort as the comparison path, wf_sort_lib 1)
+// The hipcub DeviceRadixSort this replaced is the checker of tests/test_gpu_sort.py
+// (tests/native/sort_check.hip compiles this file with CR_SORT_LIB; the product does not).
+#ifdef CR_SORT_LIB // (the sort test's comparison path: hipcub's DeviceRadixSort)
 #include <hipcub/hipcub.hpp>
 #endif
 

@@ -1,5 +1,5 @@
-// traverse.hpp -- the resumable kd traversal shared by the persistent megakernel
-// (persistent.hip) and the wavefront trace kernels (wavefront.hip).
+// traverse.hpp -- the resumable kd traversal of the wavefront trace kernels and the tail kernel
+// (wavefront.hip).
 #pragma once
 #include "leafcull.hpp"
 #include "render_common.hpp"
@@ -63,13 +63,6 @@ __device__ __forceinline__ void diag_flush(unsigned long long *ctrs, const Diag 
         if ((threadIdx.x & 63) == 0 && s) atomicAdd(&ctrs[CTR_DIAG + i], s);
     }
 }
-
-// Phase clock of a wave (measurement builds, PROF): shader-clock cycles spent in
-// trav_round's descent, leaf cull, leaf tests and stack pop, and the calls' total.
-struct Prof {
-    uint64_t desc, cull, test, pop, calls;
-};
-__device__ __forceinline__ uint64_t prof_now() { return __builtin_amdgcn_s_memtime(); }
 
 // Performed work of one lane (perf builds, PERF_* in kernels.hpp): what the kernel executes and
 // the bytes its loads and stores move -- vector accesses per lane, scalar loads once per wave
@@ -165,19 +158,6 @@ __device__ __forceinline__ TriRec sload_rec(const float4 *p) {
     return TriRec{make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]),
                   make_float4(b[0], b[1], b[2], b[3])};
 }
-// Two consecutive records with one wait (96 B: the record after a leaf's last one
-// is in bounds, cr_upload_scene pads the buffer with one).
-__device__ __forceinline__ void sload_rec2(const float4 *p, TriRec &r0, TriRec &r1) {
-    cr_v16f a;
-    cr_v8f b;
-    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx8 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(a), "=&s"(b)
-                 : "s"(p));
-    r0 = TriRec{make_float4(a[0], a[1], a[2], a[3]), make_float4(a[4], a[5], a[6], a[7]),
-                make_float4(a[8], a[9], a[10], a[11])};
-    r1 = TriRec{make_float4(a[12], a[13], a[14], a[15]), make_float4(b[0], b[1], b[2], b[3]),
-                make_float4(b[4], b[5], b[6], b[7])};
-}
 // Four consecutive cull boxes (64 B; cull buffers carry three padding boxes).
 __device__ __forceinline__ cr_v16f sload_box4(const float4 *p) {
     cr_v16f r;
@@ -213,25 +193,7 @@ __device__ __forceinline__ void sload_fat_box_n(const uint4 *fat, const float4 *
     b = make_uint4(r[4], r[5], r[6], r[7]);
     box = make_float4(x[0], x[1], x[2], x[3]);
 }
-// A leaf cull record (LC_REC = 7 float4, 112 B) under one scalar-load wait.
-__device__ __forceinline__ void sload_lcull(const float4 *p, LcFloat4 (&r)[LC_REC]) {
-    cr_v16f a;
-    cr_v8f b;
-    cr_v4f c;
-    asm volatile("s_load_dwordx16 %0, %3, 0x0\n\ts_load_dwordx8 %1, %3, 0x40\n\ts_load_dwordx4 %2, %3, 0x60\n\t"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "=&s"(a), "=&s"(b), "=&s"(c)
-                 : "s"(p));
-#pragma unroll
-    for (int i = 0; i < 4; i++) r[i] = LcFloat4{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]};
-    r[4] = LcFloat4{b[0], b[1], b[2], b[3]};
-    r[5] = LcFloat4{b[4], b[5], b[6], b[7]};
-    r[6] = LcFloat4{c[0], c[1], c[2], c[3]};
-}
-// The references of the leaf at `node` that the lane's ray (o, d: unit, segment [0, tmax])
-// must test (leafcull.hpp); bits < count.
-// FORM 0: per-ray bound records (S.lcull), 1: fixed-pad (S.lcullf), 2: packed fixed-pad (S.lcullp),
-// 3: packed fixed-pad by first reference (S.lcullq)
+// A packed leaf cull record (LC_RECP float4, 96 B) under one scalar-load wait.
 __device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_REC]) {
     cr_v16f a;
     cr_v8f b;
@@ -243,7 +205,7 @@ __device__ __forceinline__ void sload_lcullp(const float4 *p, LcFloat4 (&r)[LC_R
     r[4] = LcFloat4{b[0], b[1], b[2], b[3]};
     r[5] = LcFloat4{b[4], b[5], b[6], b[7]};
 }
-// FORM 4: the compressed records (S.lcullc, 48 B: three 16-B loads, or one 48-B scalar load pair)
+// A compressed leaf cull record (S.lcullc, 48 B: three 16-B loads, or one 48-B scalar load pair)
 __device__ __forceinline__ void sload_lcullc(const uint4 *p, uint32_t (&w)[12]) {
     cr_v8u a;
     cr_v4u b;
@@ -255,31 +217,10 @@ __device__ __forceinline__ void sload_lcullc(const uint4 *p, uint32_t (&w)[12]) 
 #pragma unroll
     for (int i = 0; i < 4; i++) w[8 + i] = b[i];
 }
-// FORM 5: the short compressed records (S.lculls, 32 B: two 16-B loads, or one scalar load)
-__device__ __forceinline__ void sload_lculls(const uint4 *p, uint32_t (&w)[8]) {
-    cr_v8u a;
-    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(a) : "s"(p));
-#pragma unroll
-    for (int i = 0; i < 8; i++) w[i] = a[i];
-}
-template <bool SC, int FORM = 0>
+// The references of the leaf at `node` that the lane's ray (o, d: unit, segment [0, tmax]) must test
+// (leafcull.hpp); bits < count.  FORM 2: packed fixed-pad records (S.lcullp), 4: compressed (S.lcullc).
+template <bool SC, int FORM>
 __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, uint32_t count, f3 o, f3 d, float tmax) {
-    if (FORM == 5) {
-        uint32_t w[8];
-        if (SC && wave_uniform(node)) {
-            sload_lculls(S.lculls + (size_t)LC_RECS * __builtin_amdgcn_readfirstlane(node), w);
-        } else {
-            const uint4 *p = (const uint4 *)((const char *)S.lculls + node * (uint32_t)(16 * LC_RECS));
-#pragma unroll
-            for (int i = 0; i < LC_RECS; i++) {
-                const uint4 v = p[i];
-                w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
-            }
-        }
-        const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
-        const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
-        return leaf_cull_mask_s(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, w, count, S.lcg);
-    }
     if (FORM == 4) {
         uint32_t w[12];
         if (SC && wave_uniform(node)) {
@@ -296,13 +237,12 @@ __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, 
         const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
         return leaf_cull_mask_c(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, w, count, S.lcg);
     }
+    static_assert(FORM == 2 || FORM == 4, "leaf cull record forms: 2 (packed) or 4 (compressed)");
     LcFloat4 rec[LC_REC];
-    constexpr int NR = FORM >= 2 ? LC_RECP : LC_REC;
-    // FORM 3: the packed records indexed by the leaf's first reference (QUAD traces: `node` is that)
-    const float4 *recs = FORM == 3 ? S.lcullq : FORM == 2 ? S.lcullp : (FORM == 1 ? S.lcullf : S.lcull);
+    constexpr int NR = LC_RECP;
+    const float4 *recs = S.lcullp;
     if (SC && wave_uniform(node)) {
-        if (FORM >= 2) sload_lcullp(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
-        else sload_lcull(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
+        sload_lcullp(recs + (size_t)NR * __builtin_amdgcn_readfirstlane(node), rec);
     } else {
         const float4 *p = (const float4 *)((const char *)recs + node * (uint32_t)(16 * NR));
 #pragma unroll
@@ -324,9 +264,7 @@ __device__ __forceinline__ uint32_t leaf_mask(const DevScene &S, uint32_t node, 
     const float ov[3] = {o.x, o.y, o.z}, dv[3] = {d.x, d.y, d.z};
     // v_rcp_f32: within 1 ulp of 1/d (the check allows 2, tests/native/leafcull_check.cpp)
     const float inv[3] = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)};
-    if (FORM >= 2) return leaf_cull_mask_packed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
-    if (FORM == 1) return leaf_cull_mask_fixed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
-    return leaf_cull_mask(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, S.db, rec, count);
+    return leaf_cull_mask_packed(ov, dv, inv, lc_unit(d.x, d.y, d.z), tmax, rec, count);
 }
 
 template <bool SC> __device__ __forceinline__ float4 load_box(const float4 *b, uint32_t i) {
@@ -336,18 +274,6 @@ template <bool SC> __device__ __forceinline__ float4 load_box(const float4 *b, u
 template <bool SC> __device__ __forceinline__ uint2 load_node(const DevScene &S, uint32_t node) {
     if (SC && wave_uniform(node)) return sload_node(S.nodes + __builtin_amdgcn_readfirstlane(node));
     return S.nodes[node];
-}
-
-// Two-level node records (DevScene::quad, quadnodes.hpp): 16 B per record root, one dwordx4 (or one
-// s_load_dwordx4 when the wave is uniform) per two descent levels.
-__device__ __forceinline__ uint4 sload_quad(const uint4 *p) {
-    cr_v4u r;
-    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p));
-    return make_uint4(r[0], r[1], r[2], r[3]);
-}
-template <bool SC> __device__ __forceinline__ uint4 load_quad(const DevScene &S, uint32_t slot) {
-    if (SC && wave_uniform(slot)) return sload_quad(S.quad + __builtin_amdgcn_readfirstlane(slot));
-    return *(const uint4 *)((const char *)S.quad + slot * 16u);
 }
 
 // Fat node records (DevScene::fat): 32 B per node, {self, child 0, child 1}, so
@@ -375,29 +301,24 @@ template <bool SC> __device__ __forceinline__ void load_fat(const DevScene &S, u
 #endif
 }
 
-// PF: software-pipelined leaf loop (triangle j+1's loads issued before j is
+// The leaf loop is software-pipelined (triangle j+1's loads issued before j is
 // tested).  Measured and dropped: the same unrolled by two with unconditional
 // loads (no register rotation copies, but count-1 leaves fetch a second record:
 // -2.3%), and compiler-scheduled, pipelined scalar loads for uniform leaves
-// (address_space(4): -2.5% against the asm s_load + wait below).
+// (address_space(4): -2.5% against the asm s_load + wait below).  The other measured
+// and dropped knobs (DESIGN.md keeps their numbers): the top of the tree in LDS, a
+// uniform leaf's records two per wait, per-reference plane records, two-level 16-B node
+// records, the per-ray, fixed-pad and short leaf cull record forms, the phase clock.
 // BF: the decisions as selects instead of divergent branches (the trace kernels
 // are bound by the scalar unit's exec-mask bookkeeping, SURVEY §8d / DESIGN §3.3):
 // a descent step branches only around its stack push, and a uniform leaf's
 // triangle tests keep their result by select (tri_test_wave).
-// TILE (FAT builds): fat records of nodes 0..TILE-1 -- the top of the tree, which
-// cr_upload_scene numbers breadth-first -- are read from the block's LDS copy
-// `tile` instead of through the vector-memory address path.
-// UL2 (BF + SC builds): a uniform leaf's records come two per scalar-load wait.
-// PLANE (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a triangle
-// test runs only when the lane's segment [0, tmax) is not proven to stay on one side of
-// the triangle's plane (S.planes, planecull.hpp) -- on one side the test cannot accept.
-// A uniform leaf reads four plane records per scalar load.
-// CULL (camera rays; BF + SC, PF 1): a triangle test runs only when the lane's sample
+// CULL (camera rays; BF + SC): a triangle test runs only when the lane's sample
 // position (csx, csy) lies in the reference's cull box (camcull.hpp) -- outside it the
 // test cannot accept, so skipping it changes nothing.  A uniform leaf reads four boxes
 // per scalar load and tests a triangle only if some lane is inside its box; a divergent
 // lane reads its box (16 B) and, inside, the record (48 B).
-// LC (secondary closest / shadow rays, unit directions; BF + SC, PF 1): a leaf's tests run only
+// LC (secondary closest / shadow rays, unit directions; BF + SC): a leaf's tests run only
 // for the references its cull record (leafcull.hpp) cannot exclude for this ray and segment.
 // A trace build's configuration: every knob of trav_round and wf_trace (wavefront.hip), named.  The
 // defaults are the plain reference build; a build is a type deriving from this and restating what it
@@ -410,31 +331,22 @@ struct TraceDefaults {
     static constexpr bool SC = false;     // scalar loads of wave-uniform nodes and leaves
     static constexpr bool FD = false;     // exact short split division by the ray's RN(1/d)
     static constexpr bool FAT = false;    // fat node records (a node and its children per load)
-    static constexpr int PF = 1;          // leaf loop: 1 one record ahead, 2 unrolled by two, 0 none
     static constexpr bool CAM = false;    // the generation-1 closest (camera-ray) instantiation
     static constexpr bool BF = false;     // branch-light steps and uniform-leaf tests by select
-    static constexpr int TILE = 0;        // fat records of the first TILE nodes in LDS
-    static constexpr bool UL2 = false;    // a uniform leaf's records two per scalar-load wait
     static constexpr int CULL = 0;        // camera cull boxes: 1 references and leaves, 2 also subtrees
-    static constexpr int PLANE = 0;       // plane records of secondary / shadow rays
-    static constexpr int LC = 0;          // leaf cull records (1 per-ray, 2 passing culled leaves, 3 fixed, 4 packed, 5 compressed, 6 short)
-    static constexpr bool PROF = false;   // phase clock (measurement only)
+    static constexpr int LC = 0;          // leaf cull records (4 packed, 5 compressed)
     static constexpr bool PC = false;     // performed-work counters (measurement only)
-    static constexpr bool QUAD = false;   // two-level 16-B node records (quadnodes.hpp) instead of fat ones
     static constexpr bool DEAD = false;   // shadow queues with dead entries (wf_shade's chunked appends) skipped
 };
 
 template <class C>
 __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
-                                               Ctr &c, const uint4 *tile = nullptr, float csx = 0.f,
-                                               float csy = 0.f, const float4 *cull = nullptr,
+                                               Ctr &c, float csx = 0.f, float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
-                                               Prof *pf = nullptr, Pc *pc = nullptr, uint32_t quorum = 0) {
-    static constexpr int R = C::R, PF = C::PF, TILE = C::TILE, CULL = C::CULL, PLANE = C::PLANE, LC = C::LC;
-    static constexpr bool FULL = C::FULL, FD = C::FD, SC = C::SC, FAT = C::FAT, BF = C::BF, UL2 = C::UL2;
-    static constexpr bool QUAD = C::QUAD;
-    uint64_t pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0;
+                                               Pc *pc = nullptr, uint32_t quorum = 0) {
+    static constexpr int R = C::R, CULL = C::CULL, LC = C::LC;
+    static constexpr bool FULL = C::FULL, FD = C::FD, SC = C::SC, FAT = C::FAT, BF = C::BF;
     // quorum (lean FAT builds without the camera cull): the wave's descent stops at a fetch once at most
     // quorum / 64 of the lanes that entered the round still descend; those keep T.node (the node to fetch)
     // and their interval and go on next round -- the same node visits with the same intervals, so the
@@ -442,7 +354,6 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     const uint32_t nbusy = quorum ? (uint32_t)__popcll(__ballot(1)) : 0u;
     constexpr uint32_t PENDING_LEAF = 0xfffffffeu;
     bool pending = false;
-    if (pf) pt0 = prof_now();
     if (pc && wave_leader()) pc->waves++;
     // performed-work accounting of record loads (pc: perf builds)
     auto lrec = [&](uint32_t i) -> TriRec {
@@ -453,18 +364,13 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         pc_load(pc, true, 16u * REC_STRIDE);
         return sload_rec(q);
     };
-    static_assert(!CULL || (BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "cull: lean BF + SC builds");
+    static_assert(!CULL || (BF && SC && !FULL), "cull: lean BF + SC builds");
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
-    static_assert(!PLANE || (!CULL && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "plane: lean BF + SC builds");
-    static_assert(!LC || (!CULL && !PLANE && BF && SC && PF == 1 && !FULL && !UL2 && !TILE), "leaf cull: lean BF + SC builds");
-    static_assert(!QUAD || (BF && SC && !CULL && !PLANE && !TILE && !UL2 && LC != 2 && !FULL), "quad records: lean BF + SC builds");
-    static_assert(LC < 5 || !QUAD, "compressed leaf cull records: indexed by node (fat-record builds)");
+    static_assert(!LC || ((LC == 4 || LC == 5) && !CULL && BF && SC && !FULL), "leaf cull: lean BF + SC builds, forms 4 / 5");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
-    // (sh: the children's positions are child + (side << sh) -- 0 for node ids and a record root's middle
-    // children, 2 for a middle node's child records in QUAD codes)
-    auto step = [&](uint2 nd, uint32_t sh = 0) -> uint32_t {
+    auto step = [&](uint2 nd) -> uint32_t {
         if (pc) pc->steps++;
 #ifdef CR_PAD_STEP // issue-cost calibration only: CR_PAD_STEP extra VALU per shadow descent step
         if (C::SHADOW) {
@@ -499,7 +405,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                 const uint32_t slot = (T.sp & (R - 1)) * bdim + tid;
                 if (pc && T.nl == R) pc->vb += 8;
                 if (T.nl == R) gstack_at(gstk, T.sp - R, gstride, gid) = ring[slot]; // spill the oldest
-                ring[slot] = make_uint2(child + (below << sh), __float_as_uint(T.tmax));
+                ring[slot] = make_uint2(child + below, __float_as_uint(T.tmax));
             }
             T.nl = push && T.nl < R ? T.nl + 1 : T.nl;
             T.sp += push ? 1u : 0u;
@@ -518,7 +424,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             T.tmax = tsplit;
             k = 1u - below;
         }
-        T.node = child + (k << sh);
+        T.node = child + k;
         return k;
     };
     uint2 nd;
@@ -543,55 +449,10 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
         T.tmax = __uint_as_float(e.y);
     };
-    // LC 2: a leaf whose references are all excluded is passed like an empty leaf -- the lane
-    // pops and descends to its next leaf in the same round, so the round's tests run on every lane
-    for (;;) {
-    culled = false;
-    if (QUAD) { // two levels per 16-B record (quadnodes.hpp); T.node is a position code slot << 2 | sel
-        uint4 q;
-        auto fetchq = [&](uint32_t code) {
-            const uint32_t slot = code >> 2;
-            pc_load(pc, SC && wave_uniform(slot), 16);
-            q = load_quad<SC>(S, slot);
-        };
-        // the record root at `code` (sel 0): its word and axis; its children are the record's middle nodes
-        auto root_view = [&](uint32_t code) { return make_uint2(q.x, (q.w & 3u) | ((code + 1u) << 2)); };
-        // middle node k: its word and axis; its children are the records at gb_k, gb_k + 1 (codes stride 4)
-        auto mid_view = [&](uint32_t k) {
-            const uint32_t gb = (q.w >> 6) + (((k != 0u) & (((q.w >> 2) & 3u) != 3u)) ? 2u : 0u);
-            return make_uint2(k ? q.z : q.y, ((q.w >> (2u + 2u * k)) & 3u) | (gb << 4));
-        };
-        fetchq(T.node);
-        const uint32_t sel = T.node & 3u;
-        nd = sel ? mid_view(sel - 1u) : root_view(T.node);
-        if (sel && (nd.y & 3u) != 3u) { // a popped middle node: its own step, then its child's record
-            step(nd, 2);
-            fetchq(T.node);
-            nd = root_view(T.node);
-        }
-        while ((nd.y & 3u) != 3u) {
-            const uint32_t k = step(nd);
-            nd = mid_view(k);
-            if ((nd.y & 3u) != 3u) {
-                step(nd, 2);
-                if (quorum && (uint32_t)__popcll(__ballot(1)) * 64u <= nbusy * quorum) {
-                    nd = make_uint2(PENDING_LEAF, 3u); // (no leaf word has `first` 0xfffffffe's bits and count)
-                } else {
-                    fetchq(T.node);
-                    nd = root_view(T.node);
-                }
-            }
-        }
-        pending = quorum && nd.x == PENDING_LEAF;
-        // the leaf's word -> {first, 3 | count << 2}, the fat records' leaf form
-        if (!pending) nd = make_uint2(nd.x & ((1u << S.qfbits) - 1u), 3u | ((nd.x >> S.qfbits) << 2));
-    } else if (FAT) { // two levels per dependent load: a node's record carries its children's
+    if (FAT) { // two levels per dependent load: a node's record carries its children's
         uint4 f0, f1;
         auto fetch = [&](uint32_t node) {
-            if (TILE && node < (uint32_t)TILE) {
-                f0 = tile[2 * node];
-                f1 = tile[2 * node + 1];
-            } else if (CULL >= 2) { // the record and the subtree box, loads issued together
+            if (CULL >= 2) { // the record and the subtree box, loads issued together
                 float4 b;
                 pc_load(pc, SC && wave_uniform(node), 48);
                 if (SC && wave_uniform(node)) {
@@ -661,42 +522,22 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         const float4 lb = load_box<SC>(cull_node, T.node);
         lin = csx >= lb.x && csx <= lb.y && csy >= lb.z && csy <= lb.w;
     }
-    if (pf) pt1 = prof_now();
     // LC: the references to test (bit j: first + j); count > LC_MAXREFS: every one (lmask unused)
     lmask = 0u;
     if (LC && count && count <= (uint32_t)LC_MAXREFS) {
-        // LC 3: the fixed-pad records; leaves below lc_min: every reference, no check
-        // (QUAD: the records are indexed by the leaf's first reference)
-        const uint32_t lcid = QUAD ? first : T.node;
+        // leaves below lc_min: every reference, no check
+        const uint32_t lcid = T.node;
         if (pc && count >= lc_min) {
             pc->masks++;
-            pc_load(pc, SC && wave_uniform(lcid), 16u * (LC == 6 ? LC_RECS : LC == 5 ? LC_RECC : LC == 4 ? LC_RECP : LC_REC));
+            pc_load(pc, SC && wave_uniform(lcid), 16u * (LC == 5 ? LC_RECC : LC_RECP));
         }
-        lmask = count >= lc_min ? leaf_mask<SC, LC == 6 ? 5 : LC == 5 ? 4 : LC == 4 ? (QUAD ? 3 : 2) : (LC == 3 ? 1 : 0)>(S, lcid, count, o, d, T.tmax)
+        lmask = count >= lc_min ? leaf_mask<SC, LC == 5 ? 4 : 2>(S, lcid, count, o, d, T.tmax)
                                 : (count >= 32 ? 0xffffffffu : (1u << count) - 1u);
         if (lc_debug) lmask = lc_debug == 1 ? (count >= 32 ? 0xffffffffu : (1u << count) - 1u) : 0u;
     }
-    if (LC == 2 && count <= (uint32_t)LC_MAXREFS && !lmask && T.sp) {
-        pop_entry();
-        continue;
-    }
-    break;
-    }
-    if (pf) pt2 = prof_now();
     bool found = false, occluded = false;
     uint32_t tri = 0;
     float bx = 0.f, by = 0.f;
-    // the phase clock at a return
-    auto prof_out = [&]() {
-        if (pf) {
-            const uint64_t t4 = prof_now();
-            pf->desc += pt1 - pt0;
-            pf->cull += pt2 - pt1;
-            pf->test += pt3 - pt2;
-            pf->pop += t4 - pt3;
-            pf->calls++;
-        }
-    };
     // one triangle of the leaf (kdtree.cpp:235-246 / 309-320); false: stop the leaf
     auto test = [&](const TriRec &r) -> bool {
         const uint32_t id = rec_id(r);
@@ -808,29 +649,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             found = found | acc;
             return true;
         };
-        // PLANE: the test of a triangle every active lane's segment stays on one side of is skipped
-        auto needs = [&](float nx, float ny, float nz, float w) -> bool {
-            const float s0 = dot(mk(nx, ny, nz), o) - w;
-            const float s1 = s0 + T.tmax * dot(mk(nx, ny, nz), d);
-            return !((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f));
-        };
-        if (PLANE == 1) {
-            const float4 *pb = S.planes + uf;
-            bool go = true;
-            for (uint32_t j = 0; j < uc && go; j += 4) {
-                pc_load(pc, true, 64);
-                const cr_v16f pl = sload_box4(pb + j);
-#pragma unroll
-                for (uint32_t k = 0; k < 4; k++) {
-                    if (j + k >= uc) break;
-                    if (__ballot(needs(pl[4 * k], pl[4 * k + 1], pl[4 * k + 2], pl[4 * k + 3])) &&
-                        !utest(srec(base + (size_t)REC_STRIDE * (j + k)), j + k)) {
-                        go = false;
-                        break;
-                    }
-                }
-            }
-        } else if (CULL) {
+        if (CULL) {        } else if (CULL) {
             const float4 *cb = cull + uf;
             for (uint32_t j = 0; j < uc && __ballot(lin); j += 4) {
                 pc_load(pc, true, 64);
@@ -852,13 +671,6 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
                 if (!__ballot(in)) continue;
                 if (!utest(srec(base + (size_t)REC_STRIDE * j), j, in)) break;
             }
-        } else if (UL2) {
-            for (uint32_t j = 0; j < uc; j += 2) {
-                TriRec r0, r1;
-                pc_load(pc, true, 32u * REC_STRIDE);
-                sload_rec2(base + (size_t)REC_STRIDE * j, r0, r1);
-                if (!utest(r0, j) || j + 1 >= uc || !utest(r1, j + 1)) break;
-            }
         } else {
             for (uint32_t j = 0; j < uc; j++)
                 if (!utest(srec(base + (size_t)REC_STRIDE * j), j)) break;
@@ -868,31 +680,6 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         for (uint32_t j = 0; j < count; j++) {
             tally_tri(first + j);
             if (!test(srec(base + (size_t)REC_STRIDE * j))) break;
-        }
-    } else if (PF == 2) { // pipelined, unrolled by two: the record sets alternate roles, no copies
-        TriRec ra, rb;
-        if (count) ra = lrec(first);
-        for (uint32_t j = 0; j < count; j += 2) {
-            if (j + 1 < count) rb = lrec(first + j + 1);
-            tally_tri(first + j);
-            if (!test(ra)) break;
-            if (j + 1 >= count) break;
-            if (j + 2 < count) ra = lrec(first + j + 2);
-            tally_tri(first + j + 1);
-            if (!test(rb)) break;
-        }
-    } else if (PLANE) { // plane records pipelined one ahead; a record only when the plane is crossed
-        float4 np = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (count) np = S.planes[first];
-        if (pc && count) pc->vb += 16;
-        for (uint32_t j = 0; j < count; j++) {
-            const float4 pl = np;
-            if (j + 1 < count) np = S.planes[first + j + 1];
-            if (pc && j + 1 < count) pc->vb += 16;
-            const float s0 = dot(mk(pl.x, pl.y, pl.z), o) - pl.w;
-            const float s1 = s0 + T.tmax * dot(mk(pl.x, pl.y, pl.z), d);
-            if (!((s0 > 1.f && s1 > 1.f) || (s0 < -1.f && s1 < -1.f)))
-                if (!test(lrec(first + j))) break;
         }
     } else if (LC && count <= (uint32_t)LC_MAXREFS) { // the mask's references, pipelined one ahead
         uint32_t m = lmask;
@@ -930,35 +717,21 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
         }
     } else {
         TriRec nx;
-        if (PF && count) nx = lrec(first);
-        for (uint32_t j = 0; j < count; j++) {
+        if (count) nx = lrec(first);
+        for (uint32_t j = 0; j < count; j++) { // software pipeline: triangle j+1's loads before j's test
             tally_tri(first + j);
-            TriRec r;
-            if (PF) { // software pipeline: issue triangle j+1's loads before testing j
-                r = nx;
-                if (j + 1 < count) nx = lrec(first + j + 1);
-            } else {
-                r = lrec(first + j);
-            }
+            const TriRec r = nx;
+            if (j + 1 < count) nx = lrec(first + j + 1);
             if (!test(r)) break;
         }
     }
-    if (pf) pt3 = prof_now();
-    if (occluded) {
-        prof_out();
-        return ST_OCCLUDED;
-    }
+    if (occluded) return ST_OCCLUDED;
     if (found) {
         d = mk(bx, by, __uint_as_float(tri));
-        prof_out();
         return ST_HIT;
     }
-    if (T.sp == 0) {
-        prof_out();
-        return shadow ? ST_VISIBLE : ST_MISS;
-    }
+    if (T.sp == 0) return shadow ? ST_VISIBLE : ST_MISS;
     pop_entry();
-    prof_out();
     return shadow ? ST_SHADOW : ST_CLOSEST;
 }
 

@@ -39,33 +39,11 @@ enum : uint32_t { NO_SLOT = 0xffffffffu, NO_PATH = 0xffffffffu, DEAD_RAY = 1u };
 // (the overlapped tail traces those; triangle ids stay below 2^31)
 enum : uint32_t { SEXCL_CONT = 0x80000000u };
 
-// Block-aggregated append (call with the whole block, uniformly): one global
-// atomicAdd per block instead of one per wave -- same-address atomics from
-// every wave of the grid serialise in one L2 slice.  Slots keep lane order
-// within a wave and wave order within the block.
+// Block-aggregated appends (call with the whole block, uniformly): one global atomicAdd per block and
+// queue instead of one per wave -- same-address atomics from every wave of the grid serialise in one L2
+// slice.  Slots keep lane order within a wave and wave order within the block.
 // (lds: one word per wave of the block, up to 16, then the base)
 enum : uint32_t { APP_W = 16 };
-__device__ __forceinline__ uint32_t block_append(uint32_t *counter, bool pred, uint32_t *lds /* [APP_W + 1] */) {
-    const uint64_t m = __ballot(pred);
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    if (lane == 0) lds[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t s = 0;
-        for (uint32_t w = 0; w < (blockDim.x >> 6); w++) {
-            const uint32_t c = lds[w];
-            lds[w] = s;
-            s += c;
-        }
-        lds[APP_W] = s ? atomicAdd(counter, s) : 0u;
-    }
-    __syncthreads();
-    const uint32_t slot = lds[APP_W] + lds[wave] +
-                          __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    __syncthreads(); // lds reused by the next call
-    return slot;
-}
-
 // N appends of one block at once (wf_shade's shadow and closest queues): one barrier round and
 // the N global atomics in flight together instead of one after another.  lds: [2][4 N + N] words,
 // the half `buf` alternating between consecutive calls (so no barrier is needed before the next
@@ -166,7 +144,6 @@ __device__ __forceinline__ uint32_t *cnt_closest(const WfArgs &W, uint32_t g) { 
 __device__ __forceinline__ uint32_t *cnt_shadow(const WfArgs &W, uint32_t g) { return W.cnt + WF_G + g; }
 __device__ __forceinline__ uint32_t *work_closest(const WfArgs &W, uint32_t g) { return W.cnt + 2 * WF_G + g; }
 __device__ __forceinline__ uint32_t *work_shadow(const WfArgs &W, uint32_t g) { return W.cnt + 3 * WF_G + g; }
-__device__ __forceinline__ uint32_t *cnt_ended(const WfArgs &W, uint32_t g) { return W.cnt + 4 * WF_G + g; }
 
 // Queue sort key (raysort.hip): 8x8-pixel sub-tile of the path's pixel, then an
 // 8x8 octahedral direction bin.  Any deterministic key is exact -- it only
@@ -340,18 +317,11 @@ __device__ __forceinline__ bool nee_visible(const WfArgs &W, uint32_t slot) {
 // C: the build's configuration (traverse.hpp TraceDefaults; the builds: namespace tc below)
 template <class C>
 __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W, uint32_t g) {
-    static constexpr bool SHADOW = C::SHADOW, FULL = C::FULL, CAM = C::CAM, PROF = C::PROF, PC = C::PC;
-    static constexpr int R = C::R, TILE = C::TILE, CULL = C::CULL;
+    static constexpr bool SHADOW = C::SHADOW, FULL = C::FULL, CAM = C::CAM, PC = C::PC;
+    static constexpr int CULL = C::CULL;
     static_assert(!CULL || (CAM && !SHADOW), "the cull applies to camera rays");
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
-    // TILE: the top of the tree (fat records of nodes 0..TILE-1) copied into LDS after the stack ring
-    uint4 *tile = (uint4 *)(ring_lds + R * blockDim.x);
-    if (TILE) {
-        const uint32_t nt = 2u * min((uint32_t)TILE, S.n_nodes);
-        for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) tile[i] = S.fat[i];
-        __syncthreads();
-    }
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63u;
     const uint32_t n = SHADOW ? *cnt_shadow(W, g) : *cnt_closest(W, g);
     uint32_t *work = SHADOW ? work_shadow(W, g) : work_closest(W, g);
@@ -369,14 +339,10 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
     // XCD partition (WfArgs::xcd): wave-uniform range part = xs % 256, WF_XCDS ranges tried
     // in turn (xs / 256 of them drained); one register, the rest is derived at refill
     uint32_t xs = blockIdx.x % WF_XCDS;
-    Prof pf = {0, 0, 0, 0, 0};
     Pc pc = {};
-    const uint64_t pstart = PROF ? prof_now() : 0;
-    uint64_t prefill = 0, nrefill = 0;
     for (;;) {
         const uint64_t need_m = __ballot(state == ST_NEED_WORK), busy_m = __ballot(state == busy_st);
         if (need_m && (busy_m == 0 || (uint32_t)__popcll(need_m) >= refill)) {
-            const uint64_t pr0 = PROF ? prof_now() : 0;
             const bool xp = (W.xcd >> (SHADOW ? 0 : (g == 1 ? 2 : 1))) & 1u;
             uint32_t *xwork = W.cnt + WF_XBASE + ((SHADOW ? WF_G : 0u) + g) * WF_XCDS * WF_XSTRIDE;
             for (;;) { // refill; a ray culled by the root box is answered at once and refetched
@@ -441,10 +407,6 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
                 }
                 issued = __builtin_amdgcn_readfirstlane(issued + (uint32_t)__popcll(__ballot(iss)));
             }
-            if (PROF) {
-                prefill += prof_now() - pr0;
-                nrefill++;
-            }
         }
         if (!__any(state == busy_st)) {
             if (!__any(state != ST_DONE)) break;
@@ -452,24 +414,18 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
         }
         if (state == busy_st) {
             const uint32_t r = trav_round<C>(A.lc_debug, A.lc_min,
-                S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, tile, csx, csy, A.cull,
-                A.cull_node, FULL ? &dg : nullptr, PROF ? &pf : nullptr, PC ? &pc : nullptr, A.desc_quorum);
+                S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, csx, csy, A.cull,
+                A.cull_node, FULL ? &dg : nullptr, PC ? &pc : nullptr, A.desc_quorum);
             if (r != busy_st) {
                 if (PC) pc.vb += SHADOW ? (W.vis_mark ? (r == ST_OCCLUDED ? 0u : 1u) : 4u) : 16u;
                 if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
-                // w: the hit's leaf + 1 (QUAD: its record slot + 1), the queue sort's key region
+                // w: the hit's leaf + 1, the queue sort's key region
                 else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
-                                                           __float_as_uint(d.y), (C::QUAD ? T.node >> 2 : T.node) + 1u)
+                                                           __float_as_uint(d.y), T.node + 1u)
                                               : make_uint4(0u, 0u, 0u, 0u);
                 state = ST_NEED_WORK;
             }
         }
-    }
-    if (PROF && (threadIdx.x & 63u) == 0 && ((A.diag_kinds >> (SHADOW ? TK_SHADOW : TK_CLOSEST)) & 1u)) {
-        // cycles per wave: trav_round phases, the loop's total (the kinds of "diag_kinds")
-        const uint64_t tot = prof_now() - pstart;
-        const uint64_t v[8] = {pf.desc, pf.cull, pf.test, pf.pop, pf.calls, tot, prefill, nrefill};
-        for (int i = 0; i < 8; i++) atomicAdd(&A.counters[CTR_DIAG + i], (unsigned long long)v[i]);
     }
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
     else c.closest = issued;
@@ -632,19 +588,6 @@ __device__ __forceinline__ bool shade_next(const RenderArgs &A, const WfArgs &W,
     return nee;
 }
 
-// The pending NEE term of bounce gp of a path that continues (W.fold): D = direct + (visible ? contrib :
-// 0) (rayTracer.cpp:96-99, the reference's single add), written back over dw[2(gp-1)] -- where the
-// path is read next (wf_shade(gp + 1), wf_tail at pickup), before anything folds or overwrites PS3.
-// The shadow result occ[slot] is generation gp's: the next shadow trace has not run yet.
-__device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32_t gp) {
-    float4 &dk = W.dw[(size_t)(2 * (gp - 1)) * W.P + p];
-    const float4 d4 = dk;
-    const uint32_t slot = __float_as_uint(d4.w);
-    f3 direct = ld3(d4);
-    if (nee_visible(W, slot)) direct = add(direct, ld3(PS(W, 3, p)));
-    dk = pk(direct, 0u);
-}
-
 // ----------------------------------------------------------------- shade --
 // Every closest ray of generation g: misses finish their path with the
 // background; hits run shade_next and append their NEE ray to shadow queue g and
@@ -655,7 +598,7 @@ __device__ __forceinline__ void resolve_prev(const WfArgs &W, uint32_t p, uint32
 template <int MINW, bool CH = false, int BS = 256>
 __global__ void __launch_bounds__(BS, MINW) wf_shade(RenderArgs A, WfArgs W, uint32_t g) {
     __shared__ unsigned long long tl[T_N];
-    __shared__ uint32_t app[APP_W + 1], app2[2 * (APP_W + 3) * 2];
+    __shared__ uint32_t app2[2 * (APP_W + 3) * 2];
     if (threadIdx.x < T_N) tl[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t n = *cnt_closest(W, g);
@@ -694,8 +637,6 @@ __global__ void __launch_bounds__(BS, MINW) wf_shade(RenderArgs A, WfArgs W, uin
             if (in && !hit) W.mark[i] = 0; // no resolve mark (wf_resolve)
             tally(tl, T_PATHS, in && p != NO_PATH);
         }
-        // (fold: bounce g - 1 of every path read here, hit or miss, before it is folded or shaded on)
-        if (W.fold == 1 && g >= 2 && in && p != NO_PATH) resolve_prev(W, p, g - 1);
         bool textured = false, nee = false, cont = false, skipped = false;
         ShadowRay sh = {mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, 0u};
         f3 org = mk(0.f, 0.f, 0.f), wi = mk(0.f, 0.f, 0.f), direct = mk(0.f, 0.f, 0.f);
@@ -721,13 +662,7 @@ __global__ void __launch_bounds__(BS, MINW) wf_shade(RenderArgs A, WfArgs W, uin
                 W.key[0][0][j] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res_s * W.dir_res_s) + dir_bin(sh.d, W.dir_res_s)
                                  : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, sh.o, sh.d)
                                                                                  : sort_key(A, W, p, sh.d);
-                if (W.sort_lib) W.perm[0][0][j] = j; // (raysort.hip takes the identity itself)
             }
-        }
-        if (W.fold) { // (uniform: every thread of the block calls block_append)
-            const bool ends = hit && !cont;
-            const uint32_t je = block_append(cnt_ended(W, g), ends, app);
-            if (ends) W.ended[je] = p;
         }
         if (cont) {
             next_rays[2 * (size_t)jc] = pk(org, p);
@@ -736,7 +671,6 @@ __global__ void __launch_bounds__(BS, MINW) wf_shade(RenderArgs A, WfArgs W, uin
                 W.key[1][0][jc] = W.leaf_keys ? ((h.w - 1u) >> W.leaf_shift) * (W.dir_res * W.dir_res) + dir_bin(wi, W.dir_res)
                                   : (W.world_keys && g >= (uint32_t)W.world_keys) ? world_key(A, W, org, wi)
                                                                                   : sort_key(A, W, p, wi);
-                if (W.sort_lib) W.perm[1][0][jc] = jc;
             }
         }
         tally(tl, T_HIT, hit);
@@ -761,7 +695,6 @@ __global__ void __launch_bounds__(BS, MINW) wf_shade(RenderArgs A, WfArgs W, uin
                 if (!q) W.sexcl[j] = 0u;
                 if (W.sort) {
                     W.key[q][0][j] = 0xffffffffu;
-                    if (W.sort_lib) W.perm[q][0][j] = j;
                 }
             }
         }
@@ -820,25 +753,6 @@ __global__ void __launch_bounds__(256) wf_resolve(RenderArgs A, WfArgs W, uint32
         // (overlapped tail: a continuing path is the tail's, which resolves this bounce itself)
         if (W.ended_only && !(m & 1u)) continue;
         resolve_path(A, W, p, g, m);
-    }
-}
-
-// W.fold: after the shadow trace of generation g, the paths that ended at g (wf_shade's list, in
-// the order it met them -- path order for every queue of a chunk): their last bounce's NEE term,
-// then the back-to-front fold into samples[w].  No pass over the other paths.
-__global__ void __launch_bounds__(256) wf_fold(RenderArgs A, WfArgs W, uint32_t g) {
-    const uint32_t n = *cnt_ended(W, g);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        // (overlapped tail: only the ended paths are here, which the tail never takes; fold: no vis_mark)
-        resolve_path(A, W, W.ended[i], g, 1u);
-    }
-    // fold 2: the paths that go on -- closest queue g + 1 -- have their bounce g resolved here too (beside
-    // the closest trace of g + 1, off the critical path), unless an overlapped tail resolves them itself
-    if (W.fold == 2 && !W.ended_only && g < (uint32_t)A.K) {
-        const uint32_t nc = *cnt_closest(W, g + 1);
-        const float4 *rays = W.ray[(g + 1) & 1];
-        for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nc; j += gridDim.x * blockDim.x)
-            resolve_prev(W, __float_as_uint(rays[2 * (size_t)j].w), g);
     }
 }
 
@@ -921,8 +835,6 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
                         nshadow++;
                         state = trav_begin(S, o, d, true, s1.w, T) ? ST_SHADOW : ST_VISIBLE;
                     } else if (p != NO_PATH) {
-                        // (fold: the path's bounce g0 - 1 is still pending; overlapped tails resolve it above)
-                        if (W.fold == 1 && g0 >= 2) resolve_prev(W, p, g0 - 1);
                         start_closest(); // (a dead camera ray of a partial tile: no query)
                     }
                 }
@@ -983,8 +895,8 @@ __global__ void __launch_bounds__(256, MINW) wf_tail(RenderArgs A, WfArgs W, uin
         if (busy) {
             const bool shadow = state == ST_SHADOW;
             const uint32_t r = trav_round<TailCfg<FULL, R, LC>>(A.lc_debug, A.lc_min, S, ring_lds, W.gstack, W.gstride, gid, o, d,
-                                                                        shadow, exclude, T, c, nullptr, 0.f, 0.f,
-                                                                        nullptr, nullptr, nullptr, nullptr,
+                                                                        shadow, exclude, T, c, 0.f, 0.f,
+                                                                        nullptr, nullptr, nullptr,
                                                                         PC ? &pc : nullptr, FULL ? 0u : A.desc_quorum);
             if (r != (shadow ? ST_SHADOW : ST_CLOSEST)) state = r;
         }
@@ -1032,12 +944,7 @@ enum : uint32_t { PACKET_DEPTH = 256 }; // >= the deepest tree cr_upload_scene a
 // entry it owns.
 // FD: the split distance by the exact short division from the ray's RN(1/d) per axis, kept in
 // VGPRs (div_by_rcp: Markstein's correction, the full division outside its checked range).
-// SPEC: the fat record and subtree box of the node the packet reaches if both of a fetch's levels go to
-// the near child (the eye's side: the packet's common near child) are loaded right after the fetch, while
-// the two levels' lane work runs -- only when that node's parent record is inner and its index is inside
-// the tree (a leaf's words hold a reference range, not a child index), and used when it is the next fetch.
-typedef const __attribute__((address_space(4))) cr_v4u k_v4u;
-template <int R, int S, bool PC = false, bool FD = false, bool SPEC = false>
+template <int R, int S, bool PC = false, bool FD = false>
 __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W, uint32_t g) {
     extern __shared__ uint32_t pring_lds[]; // [R][blockDim][S] per-ray tmax bits at push
     __shared__ uint32_t pnode[4][PACKET_DEPTH];
@@ -1255,9 +1162,6 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
             }
         };
         bool go = any_active();
-        uint32_t spec = 0xffffffffu; // SPEC: the node whose records sf0, sf1, sb were loaded ahead
-        uint4 sf0 = make_uint4(0u, 0u, 0u, 0u), sf1 = sf0;
-        float4 sb = make_float4(0.f, 0.f, 0.f, 0.f);
         while (go) {
             // fetch node cn: its record, both children's records and its subtree box
             uint4 f0, f1;
@@ -1267,37 +1171,7 @@ __global__ void __launch_bounds__(256, 8) wf_trace_packet(RenderArgs A, WfArgs W
                 pc.sb += 48;
                 pc.waves++;
             }
-            if (SPEC && cn == spec) {
-                f0 = sf0;
-                f1 = sf1;
-                b = sb;
-            } else {
-                sload_fat_box_n(Sc.fat, cnode, cn, f0, f1, b);
-            }
-            if (SPEC) { // the near-near grandchild (all uniform: the eye, the records)
-                spec = 0xffffffffu;
-                if ((f0.y & 3u) != 3u) {
-                    const uint32_t a0 = f0.y & 3u;
-                    const float e0 = a0 == 0u ? eye_s[0] : (a0 == 1u ? eye_s[1] : eye_s[2]);
-                    const bool below0 = e0 < __uint_as_float(f0.x);
-                    const uint32_t rx = below0 ? f0.z : f1.x, ry = below0 ? f0.w : f1.y; // the near child's record
-                    if ((ry & 3u) != 3u) { // inner: ry >> 2 is a child index (a leaf's is a reference count)
-                        const uint32_t a1 = ry & 3u;
-                        const float e1 = a1 == 0u ? eye_s[0] : (a1 == 1u ? eye_s[1] : eye_s[2]);
-                        const uint32_t gc = (ry >> 2) + (e1 < __uint_as_float(rx) ? 0u : 1u);
-                        if (gc < Sc.n_nodes) {
-                            spec = __builtin_amdgcn_readfirstlane(gc);
-                            // (compiler-visible scalar loads: it places the wait before the first use)
-                            const k_v4u *kf = (const k_v4u *)Sc.fat, *kb = (const k_v4u *)cnode;
-                            const cr_v4u x0 = kf[2u * spec], x1 = kf[2u * spec + 1u], xb = kb[spec];
-                            sf0 = make_uint4(x0[0], x0[1], x0[2], x0[3]);
-                            sf1 = make_uint4(x1[0], x1[1], x1[2], x1[3]);
-                            sb = make_float4(__uint_as_float(xb[0]), __uint_as_float(xb[1]), __uint_as_float(xb[2]),
-                                             __uint_as_float(xb[3]));
-                        }
-                    }
-                }
-            }
+            sload_fat_box_n(Sc.fat, cnode, cn, f0, f1, b);
 #pragma unroll
             for (int s = 0; s < S; s++) active[s] = active[s] & inb(s, b);
             uint2 nd = make_uint2(f0.x, f0.y);
@@ -1395,11 +1269,10 @@ struct WfVariant {
     void (*camera)(RenderArgs, WfArgs, uint32_t);
     void (*closest)(RenderArgs, WfArgs, uint32_t);
     void (*shadow)(RenderArgs, WfArgs, uint32_t);
-    int ring, waves_per_simd, tile;
+    int ring, waves_per_simd;
     int cull; // the camera trace reads the cull boxes (1: references and leaves, 2: also subtrees)
     int packet; // the camera trace is a packet trace (needs a near child common to all camera rays)
     int lc;     // the tail kernel's leaf cull form (trav_round's LC; 0: none)
-    int quad = 0; // the secondary / shadow traces read the two-level records (DevScene::quad)
     // the shadow trace of a queue wf_shade appended in chunks (its dead entries skipped); null: the build's
     // wf_shade appends per iteration
     void (*shadow_dead)(RenderArgs, WfArgs, uint32_t) = nullptr;
@@ -1430,152 +1303,58 @@ struct ShadowFatLc5Fd : ClosestFatLc5 { static constexpr bool SHADOW = true, FD 
 struct ShadowFatLc5FdDead : ShadowFatLc5Fd { static constexpr bool DEAD = true; };
 struct ClosestFatLc5Perf : ClosestFatLc5 { static constexpr bool PC = true; };
 struct ShadowFatLc5Perf : ClosestFatLc5Perf { static constexpr bool SHADOW = true; };
-// ... and with the short compressed records (32 B per leaf: two loads, or one scalar load)
-struct ClosestFatLc6 : Fat { static constexpr int LC = 6; };
-struct ShadowFatLc6Fd : ClosestFatLc6 { static constexpr bool SHADOW = true, FD = true; };
-struct ClosestFatLc6Perf : ClosestFatLc6 { static constexpr bool PC = true; };
-struct ShadowFatLc6Perf : ClosestFatLc6Perf { static constexpr bool SHADOW = true; };
-// + two-level 16-B node records (quadnodes.hpp: one dwordx4 per two descent levels instead of the fat
-// records' dwordx4 + dwordx2; 46, 47)
-struct ClosestQuadLc : ClosestFatLc { static constexpr bool QUAD = true; };
-struct ShadowQuadLcFd : ShadowFatLcFd { static constexpr bool QUAD = true; };
-struct ClosestQuad : ClosestFat { static constexpr bool QUAD = true; };
-struct ShadowQuadFd : ShadowFatFd { static constexpr bool QUAD = true; };
 // the performed-work counting instances (RenderArgs::perf_counters; measurement only)
 struct ClosestFatLcPerf : ClosestFatLc { static constexpr bool PC = true; };
 struct ShadowFatLcPerf : ShadowFatLc { static constexpr bool PC = true; };
 struct ClosestFatPerf : ClosestFat { static constexpr bool PC = true; };
 struct ShadowFatPerf : ShadowFat { static constexpr bool PC = true; };
-struct ClosestQuadLcPerf : ClosestQuadLc { static constexpr bool PC = true; };
-struct ShadowQuadLcPerf : ShadowFatLcPerf { static constexpr bool QUAD = true; };
-struct ClosestQuadPerf : ClosestQuad { static constexpr bool PC = true; };
-struct ShadowQuadPerf : ShadowFatPerf { static constexpr bool QUAD = true; };
 // the counting build (SURVEY §8d work counters, diagnostics: RenderArgs::full_counters), 1 wave per SIMD
 struct Count : TraceDefaults { static constexpr bool FULL = true; static constexpr int MINW = 1; };
 struct CameraCount : Count { static constexpr bool CAM = true; };
 struct ClosestCount : Count {};
 struct ShadowCount : Count { static constexpr bool SHADOW = true; };
-#ifdef CR_ALL_VARIANTS
-// the measured and superseded builds, by their knobs in TraceDefaults order
-template <bool SHADOW_, int R_, int MINW_, bool SC_, bool FD_, bool FAT_, int PF_, bool CAM_, bool BF_, int TILE_,
-          bool UL2_, int CULL_, int PLANE_, int LC_, bool PROF_ = false>
-struct Cfg : TraceDefaults {
-    static constexpr bool SHADOW = SHADOW_, SC = SC_, FD = FD_, FAT = FAT_, CAM = CAM_, BF = BF_, UL2 = UL2_, PROF = PROF_;
-    static constexpr int R = R_, MINW = MINW_, PF = PF_, TILE = TILE_, CULL = CULL_, PLANE = PLANE_, LC = LC_;
-};
-#endif
 } // namespace tc
 
 // (macro arguments with commas come parenthesised: CR_UNPAREN strips the parentheses)
 #define CR_ID(...) __VA_ARGS__
 #define CR_UNPAREN(x) CR_ID x
 #define CR_WF3(CAM, CL, SH, ...) {wf_trace<CR_UNPAREN(CAM)>, wf_trace<CR_UNPAREN(CL)>, wf_trace<CR_UNPAREN(SH)>, __VA_ARGS__}
-#define CR_WFK(CAMK, CL, SH, ...) {CR_UNPAREN(CAMK), wf_trace<CR_UNPAREN(CL)>, wf_trace<CR_UNPAREN(SH)>, __VA_ARGS__}
-#ifdef CR_ALL_VARIANTS
-#define CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, PL)                                                     \
-    CR_WF3((tc::Cfg<false, R, W, SC, FD, FAT, PF, true, BF, TL, U2, CU, 0, 0>),                                 \
-           (tc::Cfg<false, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL, 0>),                                \
-           (tc::Cfg<true, R, W, SC, FD, FAT, PF, false, BF, TL, U2, 0, PL, 0>), R, W, TL, CU, 0, 0)
-#define CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, CU) CR_WF_P(R, W, SC, FD, FAT, PF, BF, TL, U2, CU, 0)
-#define CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, U2) CR_WF_C(R, W, SC, FD, FAT, PF, BF, TL, U2, 0)
-#define CR_WF_T(R, W, SC, FD, FAT, PF, BF, TL) CR_WF_U(R, W, SC, FD, FAT, PF, BF, TL, false)
-#define CR_WF_BF(R, W, SC, FD, FAT, PF, BF) CR_WF_T(R, W, SC, FD, FAT, PF, BF, 0)
-#define CR_WF_PF(R, W, SC, FD, FAT, PF) CR_WF_BF(R, W, SC, FD, FAT, PF, false)
-#define CR_WF(R, W, SC, FD, FAT) CR_WF_PF(R, W, SC, FD, FAT, 1)
-// 17-25: packet camera traces with the secondary / shadow builds of the round-2 / round-3 experiments
-#define CR_WF_LC(S, LCV, W, PROF)                                                                              \
-    CR_WFK(S, (tc::Cfg<false, 8, W, true, false, true, 1, false, true, 0, false, 0, 0, LCV, PROF>),              \
-           (tc::Cfg<true, 8, W, true, false, true, 1, false, true, 0, false, 0, 0, LCV, PROF>), 8, W, 0, 2, 1, 0)
-#endif
-
 // The trace builds by number (cr_set_option "variant").  The default compile holds the plain reference
 // build 0, build 15 (the packet camera trace's fallback for an eye on a split plane), 18 and 26 (round 2's
 // and round 3's defaults), 40 / 42 (26 / 18 with the exact short division in the camera packet) and the
-// defaults 43 / 44 (40 / 42 with it in the shadow trace too).  The measured and superseded builds -- each
-// described below and in DESIGN.md §3 / §6 -- compile with `make ALL_VARIANTS=1`; the rejected builds
-// 27-39, 41 and 45 are gone (DESIGN.md keeps their numbers).
+// defaults 43 / 44 (40 / 42 with it in the shadow trace too) and 49 (43 with the compressed leaf cull
+// records).  The measured and superseded builds 1-14, 16, 17, 19-25, 27-39, 41, 45-48 and 51 are gone;
+// DESIGN.md keeps their numbers.
 struct WfBuild {
     int id;
     WfVariant v;
 };
 static const WfBuild kWf[] = {
-    {0, CR_WF3((tc::CameraRef), (tc::ClosestRef), (tc::ShadowRef), 4, 8, 0, 0, 0, 0)},
+    {0, CR_WF3((tc::CameraRef), (tc::ClosestRef), (tc::ShadowRef), 4, 8, 0, 0, 0)},
     // 15: fat records, scalar loads, branch-light steps; the camera trace skips the tests, leaves and
     // subtrees whose screen-space cull box excludes the sample
-    {15, CR_WF3((tc::CameraCull), (tc::ClosestFat), (tc::ShadowFat), 8, 8, 0, 2, 0, 0)},
+    {15, CR_WF3((tc::CameraCull), (tc::ClosestFat), (tc::ShadowFat), 8, 8, 2, 0, 0)},
     // 18: 15 whose camera rays traverse as one packet of 128 per wave (two per lane; wf_trace_packet)
-    {18, {wf_trace_packet<8, 2>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFat>, 8, 8, 0, 2, 1, 0}},
+    {18, {wf_trace_packet<8, 2>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFat>, 8, 8, 2, 1, 0}},
     // 26: 18 whose secondary closest and shadow traces skip the references a leaf's packed cull record
     // (leafcull.hpp: two normal groups, each a box and a normal cone) excludes for the ray; the tail
     // kernel culls the same way
-    {26, {wf_trace_packet<8, 2>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLc>, 8, 8, 0, 2, 1, 4}},
+    {26, {wf_trace_packet<8, 2>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLc>, 8, 8, 2, 1, 4}},
     // 40: 26 whose camera packet divides by the rays' RN(1/d) kept in VGPRs (FD; the packet's spills are
     //     outside its loops): camera trace 41.0 -> 37.7 ms, 363.1 -> 360.0 ms per pass
-    {40, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLc>, 8, 8, 0, 2, 1, 4}},
+    {40, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLc>, 8, 8, 2, 1, 4}},
     // 42: 18 with 40's camera packet (the default below LEAF_CULL_MIN_TRIS triangles)
-    {42, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFat>, 8, 8, 0, 2, 1, 0}},
+    {42, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFat>, 8, 8, 2, 1, 0}},
     // 43 / 44 (the defaults): 40 / 42 whose shadow trace divides by the ray's RN(1/d) in VGPRs too (FD;
     //     no spills at 8 waves once the stack-overflow pointer and the query count stopped occupying
     //     VGPRs): 357.5 / 355.3 vs 358.4 / 358.1 ms per pass, nanobox 162.4 vs 163.7 ms (shadow 30.7 -> 29.9)
-    {43, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
-    {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 0, 2, 1, 0, 0,
+    {43, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 2, 1, 4}},
+    {44, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFat>, wf_trace<tc::ShadowFatFd>, 8, 8, 2, 1, 0,
           wf_trace<tc::ShadowFatFdDead>}},
     // 49: 43 whose secondary closest, shadow and tail traces read the compressed leaf cull records
     //     (leafcull.hpp LC_RECC: boxes on the scene's 16-bit grid, octahedral axes, half constants)
-    {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 0, 2, 1, 5, 0,
+    {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 2, 1, 5,
           wf_trace<tc::ShadowFatLc5FdDead>}},
-#ifdef CR_ALL_VARIANTS
-    // 51: 49 with the short compressed records (leafcull.hpp LC_RECS: 32 B per leaf, the boxes of 49, each
-    //     group's octahedral axis, kappa and dt in 13 bits: two loads per leaf record instead of three, one
-    //     scalar load for a uniform leaf).  Bit-exact; two interleaved rounds at the driver's command: 2266.4 /
-    //     2261.0 (49) vs 2257.0 / 2255.1 Mray/s, shadow 39.8 / 40.0 -> 40.1 / 40.2 ms per launch -- the coarser
-    //     cones and constants leave 4.9% more triangle tests per shadow launch (2.924 -> 3.068 G), which cost
-    //     what the leaf records' third load did
-    {51, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc6>, wf_trace<tc::ShadowFatLc6Fd>, 8, 8, 0, 2, 1, 6}},
-    // 48: 43 whose camera packet loads the near-near grandchild's records ahead (SPEC), issued before the
-    //     current node's box test so the next fetch finds them in SGPRs.  Bit-exact; two interleaved
-    //     rounds at the driver's command 2187.0 / 2191.7 (43) vs 2114.9 / 2114.3 Mray/s: camera trace
-    //     34.9 -> 44.5 ms -- the loads that miss (the packet goes elsewhere 28% of the time,
-    //     tests/native/packet_check.cpp) and the 12 SGPRs they hold cost more than the wait they hide.
-    //     (Its first runs faulted at full size: traverse.hpp's two-load asm blocks lacked early-clobber
-    //     outputs; scripts/smem_hazard.py now checks every built object for that.)
-    {48, {wf_trace_packet<8, 2, false, true, true>, wf_trace<tc::ClosestFatLc>, wf_trace<tc::ShadowFatLcFd>, 8, 8, 0, 2, 1, 4}},
-    // 46 / 47: 43 / 44 whose secondary closest and shadow traces descend over the two-level 16-B records
-    //     (quadnodes.hpp; the same decisions at the same nodes with the same intervals, one dwordx4 per
-    //     two levels instead of a dwordx4 + dwordx2: 46% fewer descent fetch instructions on the sponza
-    //     stand-in, scripts/quad_census.py).  Round 5, two interleaved rounds at the driver's command:
-    //     2183.1 / 2182.1 (43) vs 2134.7 / 2138.5 Mray/s (46); shadow 41.6 -> 42.8 ms, closest beside it
-    //     73.2 -> 75.2 ms -- the traces are not bound by their count of vector loads (the L1 is at 0.82 of
-    //     its tag rate, profiles/r05_pmc_mem_sponza.json) but by instruction issue, and the quad records'
-    //     middle-node views and the resumption of a popped middle child add VALU and SALU per level
-    {46, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestQuadLc>, wf_trace<tc::ShadowQuadLcFd>, 8, 8, 0, 2, 1, 4, 1}},
-    {47, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestQuad>, wf_trace<tc::ShadowQuadFd>, 8, 8, 0, 2, 1, 0, 1}},
-    {1, CR_WF(8, 8, false, false, false)}, {2, CR_WF(8, 8, true, false, false)}, {3, CR_WF(8, 6, false, false, false)},
-    {4, CR_WF(8, 6, true, false, false)}, {5, CR_WF(8, 8, true, true, false)}, {6, CR_WF(8, 8, true, false, true)},
-    {7, CR_WF(8, 8, false, false, true)}, {8, CR_WF_PF(8, 8, true, false, false, 2)},
-    {9, CR_WF_BF(8, 8, true, false, true, 1, true)},
-    // 10-12: build 9 with the top of the tree in LDS (TILE nodes, 32 B each, after the stack ring:
-    // 8 blocks x (R x 2 KiB + TILE x 32 B) within the CU's 160 KiB)
-    {10, CR_WF_T(8, 8, true, false, true, 1, true, 128)}, {11, CR_WF_T(4, 8, true, false, true, 1, true, 384)},
-    {12, CR_WF_T(4, 8, true, false, true, 1, true, 0)},
-    // 13: build 9 with a uniform leaf's records two per scalar-load wait
-    {13, CR_WF_U(8, 8, true, false, true, 1, true, 0, true)},
-    // 14: build 9 whose camera trace skips triangle tests and leaves by the screen-space cull boxes
-    {14, CR_WF_C(8, 8, true, false, true, 1, true, 0, false, 1)},
-    // 16: 15 whose secondary closest and shadow traces skip the tests their segment cannot pass by the
-    // triangle's plane (planecull.hpp)
-    {16, CR_WF_P(8, 8, true, false, true, 1, true, 0, false, 2, 1)},
-    // 17: 15 whose camera rays traverse as one packet per wave, one ray per lane
-    {17, CR_WF_LC((wf_trace_packet<8, 1>), 0, 8, false)},
-    // 19: 18 with the per-ray-bound leaf cull records; 20: 19 whose lanes pass a leaf with every reference
-    // excluded and descend to the next one in the same round; 21 / 22: 19 / 20 at 6 waves per SIMD
-    {19, CR_WF_LC((wf_trace_packet<8, 2>), 1, 8, false)}, {20, CR_WF_LC((wf_trace_packet<8, 2>), 2, 8, false)},
-    {21, CR_WF_LC((wf_trace_packet<8, 2>), 1, 6, false)}, {22, CR_WF_LC((wf_trace_packet<8, 2>), 2, 6, false)},
-    // 23 / 24: 18 / 19 with the phase clock of the secondary and shadow traces (measurement only)
-    {23, CR_WF_LC((wf_trace_packet<8, 2>), 0, 8, true)}, {24, CR_WF_LC((wf_trace_packet<8, 2>), 1, 8, true)},
-    // 25: 19 with the fixed-pad records (one dot product and a slab test per group)
-    {25, CR_WF_LC((wf_trace_packet<8, 2>), 3, 8, false)},
-#endif
 };
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 // the build numbered `variant`, or null when it is not compiled in
@@ -1590,38 +1369,22 @@ static const WfVariant &wf_build_or_ref(int variant) {
 }
 // Builds 26 and 18 with the performed-work counts (RenderArgs::perf_counters; measurement only)
 static const WfVariant kWfPerf26 = {wf_trace_packet<8, 2, true>, wf_trace<tc::ClosestFatLcPerf>,
-                                    wf_trace<tc::ShadowFatLcPerf>, 8, 8, 0, 2, 1, 4};
+                                    wf_trace<tc::ShadowFatLcPerf>, 8, 8, 2, 1, 4};
 static const WfVariant kWfPerf18 = {wf_trace_packet<8, 2, true>, wf_trace<tc::ClosestFatPerf>,
-                                    wf_trace<tc::ShadowFatPerf>, 8, 8, 0, 2, 1, 0};
+                                    wf_trace<tc::ShadowFatPerf>, 8, 8, 2, 1, 0};
 // ... and builds 40 / 42 (26 / 18 with the FD camera packet: the same work, the division shortened)
 static const WfVariant kWfPerf40 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLcPerf>,
-                                    wf_trace<tc::ShadowFatLcPerf>, 8, 8, 0, 2, 1, 4};
+                                    wf_trace<tc::ShadowFatLcPerf>, 8, 8, 2, 1, 4};
 static const WfVariant kWfPerf42 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatPerf>,
-                                    wf_trace<tc::ShadowFatPerf>, 8, 8, 0, 2, 1, 0};
+                                    wf_trace<tc::ShadowFatPerf>, 8, 8, 2, 1, 0};
 // ... and build 49 (the compressed leaf cull records: the same work, half the mask bytes)
 static const WfVariant kWfPerf49 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc5Perf>,
-                                    wf_trace<tc::ShadowFatLc5Perf>, 8, 8, 0, 2, 1, 5};
-#ifdef CR_ALL_VARIANTS
-// ... and build 51 (the short leaf cull records)
-static const WfVariant kWfPerf51 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc6Perf>,
-                                    wf_trace<tc::ShadowFatLc6Perf>, 8, 8, 0, 2, 1, 6};
-// ... and builds 46 / 47 (the quad-record descent: fewer, smaller node loads, the same steps)
-static const WfVariant kWfPerf46 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestQuadLcPerf>,
-                                    wf_trace<tc::ShadowQuadLcPerf>, 8, 8, 0, 2, 1, 4, 1};
-static const WfVariant kWfPerf47 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestQuadPerf>,
-                                    wf_trace<tc::ShadowQuadPerf>, 8, 8, 0, 2, 1, 0, 1};
-#endif
+                                    wf_trace<tc::ShadowFatLc5Perf>, 8, 8, 2, 1, 5};
 // (43 / 44 count through 40 / 42's instances: their shadow trace's short division does the same work)
 bool wf_perf_available(int variant) {
-    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 || variant == 49 ||
-           (wf_variant_available(variant) && (variant == 46 || variant == 47 || variant == 51));
+    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 || variant == 49;
 }
 static const WfVariant &perf_variant(int variant) {
-#ifdef CR_ALL_VARIANTS
-    if (variant == 46) return kWfPerf46;
-    if (variant == 47) return kWfPerf47;
-    if (variant == 51) return kWfPerf51;
-#endif
     return variant == 18 ? kWfPerf18
            : variant == 49 ? kWfPerf49
            : (variant == 40 || variant == 43) ? kWfPerf40
@@ -1629,7 +1392,7 @@ static const WfVariant &perf_variant(int variant) {
                                               : kWfPerf26;
 }
 static const WfVariant kWfCount = {wf_trace<tc::CameraCount>, wf_trace<tc::ClosestCount>, wf_trace<tc::ShadowCount>,
-                                   8, 4, 0, 0, 0, 0};
+                                   8, 4, 0, 0, 0};
 // one past the largest build number (option validation)
 int num_wf_variants() {
     int m = 0;
@@ -1649,7 +1412,6 @@ static bool camera_fuses(const WfVariant &v, const RenderArgs &A, const WfArgs &
 }
 bool wf_variant_culls(int variant) { return wf_build(variant) && wf_build(variant)->cull; }
 bool wf_variant_available(int variant) { return wf_build(variant) != nullptr; }
-bool wf_variant_quad(int variant) { return wf_build(variant) && wf_build(variant)->quad; }
 
 // One thread per leaf reference: its cull box for this render's camera (camcull.hpp),
 // from the record's A, e1, e2 -- the floats the triangle test uses.  Boxes
@@ -1730,7 +1492,7 @@ static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStre
     size_t tb = W.sort_tmp_bytes;
     const int bits = pixel ? W.key_bits_pixel : (set == 0 ? W.key_bits_s : W.key_bits);
     // (the trace reads the permutation only: the last pass writes no keys)
-    const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, W.sort_lib != 0, W.sort_lib == 0, false);
+    const int sel = sort_queue(keys, vals, n, bits, W.sort_tmp, tb, st, false, true, false);
     if (sel < 0) {
         err = (int)hipErrorUnknown;
         return nullptr;
@@ -1822,7 +1584,7 @@ uint32_t wf_shade_blocks(int num_cus, int shade_waves) {
 // on sorted queues (sponza stand-in) wf_shade gains 9 % but the shadow trace loses 1.7 % -- the chunks
 // change the order among equal keys -- 2278.5 / 2278.7 -> 2274.8 / 2270.4
 static uint32_t shade_app_chunk(const WfArgs &W, uint32_t nin, int num_cus) {
-    if (W.fold || !W.qspare) return 0u;
+    if (!W.qspare) return 0u;
     const uint32_t grid = wf_shade_blocks(num_cus, W.shade_waves);
     const uint32_t want = nin / (grid * 16u), cap = W.qspare / grid;
     if (W.app_force) return W.app_force <= cap ? W.app_force : 0u;
@@ -1865,7 +1627,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     wf_tail_geometry(num_cus, tblk, tblocks);
     if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds =
-        (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4);
+        (size_t)v.ring * blk * sizeof(uint2);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
     int err = 0;
     // the rest of the chunk from closest queue g on, in one launch
@@ -1875,20 +1637,12 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, s, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
-#ifdef CR_ALL_VARIANTS
-        else if (A.perf_counters && v.lc == 6)
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 6, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
-#endif
         else if (A.perf_counters && v.lc == 5)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
         else if (A.perf_counters)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, s, A, Wt, g);
-#ifdef CR_ALL_VARIANTS
-        else if (v.lc == 6)
-            launch_tail_lean<6>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
-#endif
         else if (v.lc == 5)
             launch_tail_lean<5>(Wt.tail_waves, tblk, num_cus, tlds, s, A, Wt, g);
         else if (v.lc == 4)
@@ -1957,7 +1711,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, st, TK_SHADOW, true))) break;
         hipLaunchKernelGGL(dead ? v.shadow_dead : v.shadow, dim3(sblocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, TK_SHADOW, false))) break;
-        hipLaunchKernelGGL(W.fold ? wf_fold : wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
         W.ended_only = 0u;
         if (next || overlap)
             if ((err = (int)hipEventRecord(ss.join, ss.side)) || (err = (int)hipStreamWaitEvent(st, ss.join, 0)))
@@ -1981,7 +1735,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
     for (int i = 0; i < nl; i++)
         if (L[i].W.gstride < blk * blocks || L[i].W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds =
-        (size_t)v.ring * blk * sizeof(uint2) + (size_t)v.tile * 2 * sizeof(uint4);
+        (size_t)v.ring * blk * sizeof(uint2);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8;
     int err = 0;
     struct Run {
@@ -1996,20 +1750,12 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_TAIL, true))) return;
         if (A.full_counters)
             hipLaunchKernelGGL((wf_tail<true, 8, TAIL_MINW>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
-#ifdef CR_ALL_VARIANTS
-        else if (A.perf_counters && v.lc == 6)
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 6, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
-#endif
         else if (A.perf_counters && v.lc == 5)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (A.perf_counters && v.lc == 4)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 4, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (A.perf_counters)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 0, true>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
-#ifdef CR_ALL_VARIANTS
-        else if (v.lc == 6)
-            hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 6>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
-#endif
         else if (v.lc == 5)
             hipLaunchKernelGGL((wf_tail<false, 8, TAIL_MINW, 5>), dim3(tblocks), dim3(tblk), tlds, ln.st, A, W, g);
         else if (v.lc == 4)
@@ -2081,7 +1827,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
         if ((err = trace_event(te, ln.st, TK_SHADOW, true))) return true;
         hipLaunchKernelGGL(v.shadow, dim3(sblocks), dim3(blk), lds, ln.st, A, Ws, g);
         if ((err = trace_event(te, ln.st, TK_SHADOW, false))) return true;
-        hipLaunchKernelGGL(r.W.fold ? wf_fold : wf_resolve, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, g);
+        hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, ln.st, A, r.W, g);
         if (next) {
             if ((err = (int)hipEventRecord(ln.join, ln.side)) || (err = (int)hipStreamWaitEvent(ln.st, ln.join, 0)))
                 return true;
@@ -2125,10 +1871,10 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
 }
 
 // Bytes of sort workspace for queues of up to n rays (temp storage only).
-size_t wf_sort_tmp_bytes(uint32_t n, int key_bits, bool lib) {
+size_t wf_sort_tmp_bytes(uint32_t n, int key_bits) {
     size_t tb = 0;
     uint32_t *k[2] = {nullptr, nullptr}, *v[2] = {nullptr, nullptr};
-    sort_queue(k, v, n, key_bits, nullptr, tb, nullptr, lib);
+    sort_queue(k, v, n, key_bits, nullptr, tb, nullptr, false);
     return tb;
 }
 

@@ -1,9 +1,8 @@
 """Kernel-name classification shared by the profile summaries (rocprofv3 kernel names).
 
 The trace kernels are wf_trace<C> with C a build configuration of csrc/wavefront.hip's namespace
-tc: named types for the compiled-by-default builds (cr::tc::ShadowFatLcFd, cr::tc::ClosestCount,
-cr::tc::ClosestFatLcPerf, ...) and cr::tc::Cfg<SHADOW, R, MINW, SC, FD, FAT, PF, CAM, ...> for the
-ALL_VARIANTS ones; the camera packet is wf_trace_packet<R, S, PC, FD>; the tail wf_tail<FULL, ...>.
+tc (cr::tc::ShadowFatLc5Fd, cr::tc::ClosestCount, cr::tc::ClosestFatLc5Perf, ...); the camera packet
+is wf_trace_packet<R, S, PC, FD>; the tail wf_tail<FULL, ...>.
 """
 import re
 
@@ -22,9 +21,6 @@ def trace_info(name: str):
     if not m:
         return None
     t = m.group(1)
-    if t == "Cfg":  # Cfg<SHADOW, R, MINW, SC, FD, FAT, PF, CAM, ...> (ALL_VARIANTS builds, all lean)
-        a = [x.strip() for x in re.search(r"Cfg<([^>]*)>", name).group(1).split(",")]
-        return ("shadow" if a[0] == "true" else ("camera" if a[7] == "true" else "closest")), "lean"
     kind = "shadow" if t.startswith("Shadow") else ("camera" if t.startswith("Camera") else "closest")
     mode = "counting" if t.endswith("Count") else ("perf" if t.endswith("Perf") else "lean")
     return kind, mode
@@ -32,8 +28,6 @@ def trace_info(name: str):
 
 def is_counting(name: str) -> bool:
     """The counting and performed-work instances (not timed kernels)."""
-    if re.search(r"render_dynamic<\w+, true,", name):
-        return True
     info = trace_info(name)
     return info is not None and info[1] != "lean"
 

@@ -11,4 +11,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ
 echo "pass a ok"
 timeout -s KILL 300 rocprofv3 --pmc TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE -d $OUT/b -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/b.log 2>&1 || { echo "pass b failed"; exit 1; }
 echo "pass b ok"
+# lane utilisation of the VALU (rocprofv3's VALUUtilization: thread-cycles / (64 x active VALU cycles))
+timeout -s KILL 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU -d $OUT/c -o pmc --output-format csv -- python3 bench.py $ARGS > $OUT/c.log 2>&1 || { echo "pass c failed"; exit 1; }
+echo "pass c ok"
 find $OUT -name "*.csv"

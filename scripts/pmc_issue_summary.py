@@ -6,6 +6,8 @@ per dispatch-averaged instruction counts and the issue utilisation they imply,
                 unit per CU, one instruction per cycle)
 with the shader clock from SQ_BUSY_CYCLES / (32 shader engines x kernel time), and
     TA busy   = TA_BUSY_avr / (GRBM_GUI_ACTIVE / 8 XCDs)  (vector-memory address path)
+    VALU lanes = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)  (rocprofv3's VALUUtilization:
+                the active lanes of an issued VALU instruction, pass c)
     python scripts/pmc_issue_summary.py gpurun_out/pmc_issue/a/pmc_counter_collection.csv \
         profiles/pmc_issue_sponza.json [spp]
 """
@@ -24,7 +26,8 @@ def main(src, dst, spp=128):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     ns = collections.defaultdict(dict)
     srcb = src.replace("/a/", "/b/")  # pass b: TA busy (vector-memory address path)
-    for f in (src, srcb):
+    srcc = src.replace("/a/", "/c/")  # pass c: VALU lane utilisation
+    for f in (src, srcb, srcc):
         try:
             rows = list(csv.DictReader(open(f)))
         except FileNotFoundError:
@@ -51,6 +54,8 @@ def main(src, dst, spp=128):
         }
         if v.get("GRBM_GUI_ACTIVE"):  # TA busy cycles (average TA) over the kernel's cycles per XCD
             out[k]["ta_busy"] = round(v["TA_BUSY_avr"] / (v["GRBM_GUI_ACTIVE"] / 8), 3)
+        if v.get("SQ_ACTIVE_INST_VALU"):
+            out[k]["valu_lane_util"] = round(v["SQ_THREAD_CYCLES_VALU"] / (64 * v["SQ_ACTIVE_INST_VALU"]), 3)
     # per lean trace kind (bench.py roofline.issue): SHADOW, FULL, ..., CAM[, BF] template args
     kinds = {}
     for k, v in out.items():
@@ -60,7 +65,8 @@ def main(src, dst, spp=128):
         kind = info[0]
         d = v["dispatches"]
         kinds[kind] = {"kernel": k, "valu_issue_busy": v["valu_issue_busy"], "salu_issue_busy": v["salu_issue_busy"],
-                       "ta_busy": v.get("ta_busy"), "shader_clock_ghz": v["shader_clock_ghz"],
+                       "ta_busy": v.get("ta_busy"), "valu_lane_util": v.get("valu_lane_util"),
+                       "shader_clock_ghz": v["shader_clock_ghz"],
                        "salu_per_valu": v["salu_per_valu"], "dispatches": d,
                        "avg_launch_ms": round(v["seconds"] * 1e3 / d, 3),
                        # per-launch instruction counts: bench.py roofline (issue ceilings) divides

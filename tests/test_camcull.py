@@ -1,6 +1,5 @@
-"""CPU checks of the exact test skips of trace builds 14-16: the camera-ray cull boxes
-(csrc/camcull.hpp) and the plane records of the secondary / shadow traces
-(csrc/planecull.hpp).
+"""CPU checks of the exact test skip of the culling camera traces (builds 15 and later): the
+camera-ray cull boxes (csrc/camcull.hpp).
 
 The camera trace of build 14 skips a Moller-Trumbore test when the ray's screen
 position lies outside the triangle's cull box; that is exact only if the test can
@@ -21,8 +20,6 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 SRC = ROOT / "tests" / "native" / "camcull_check.cpp"
 HDR = ROOT / "chiaroscuro-raytracer_amd" / "csrc" / "camcull.hpp"
-PSRC = ROOT / "tests" / "native" / "planecull_check.cpp"
-PHDR = ROOT / "chiaroscuro-raytracer_amd" / "csrc" / "planecull.hpp"
 
 
 def _build(tmp_path, header_dir, src=SRC):
@@ -59,26 +56,3 @@ def test_margins_are_needed(tmp_path):
     exe = _build(tmp_path, tmp_path / "hdr")
     viol = sum(_run(exe, s, 20000)[0] for s in (1, 2))
     assert viol > 0
-
-
-@pytest.mark.parametrize("seed", [1, 2])
-def test_plane_record_is_conservative(tmp_path, seed):
-    """Secondary / shadow rays (unit directions inside the scene box): every accepted
-    (ray, tmax) passes the plane check, over slivers, tiny triangles, grazing rays,
-    origins on the plane and tmax within ulps of the hit."""
-    exe = _build(tmp_path, PHDR.parent, PSRC)
-    viol, tested, accepted, skipped = _run(exe, seed, 4000)
-    assert tested > 1_000_000 and accepted > 100_000 and skipped > 100_000
-    assert viol == 0
-
-
-def test_plane_margin_is_needed(tmp_path):
-    """With the margin 4000 times smaller the checker finds accepted tests the plane
-    check would skip."""
-    src = PHDR.read_text()
-    old = "const double mu = 4.0 * u * E * (21.0 * Db + 12.0 * Tb);"
-    assert old in src
-    (tmp_path / "hdr").mkdir()
-    (tmp_path / "hdr" / "planecull.hpp").write_text(src.replace(old, "const double mu = 1e-3 * u * E * (21.0 * Db + 12.0 * Tb);"))
-    exe = _build(tmp_path, tmp_path / "hdr", PSRC)
-    assert _run(exe, 1, 4000)[0] > 0
