@@ -649,7 +649,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             found = found | acc;
             return true;
         };
-        if (CULL) {        } else if (CULL) {
+        if (CULL) {
             const float4 *cb = cull + uf;
             for (uint32_t j = 0; j < uc && __ballot(lin); j += 4) {
                 pc_load(pc, true, 64);
