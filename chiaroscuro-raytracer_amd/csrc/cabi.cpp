@@ -360,6 +360,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                 W.leaf_keys = leaf_keys ? 1 : 0;
                 W.leaf_shift = c->wf_leaf_shift;
                 W.resolve_paths = c->wf_resolve_paths;
+                W.measure_skip = c->wf_measure_skip;
                 W.tail_overlap = c->wf_tail_overlap;
                 W.sort_g1 = c->wf_sort_g1;
                 W.cam_lean = c->wf_cam_lean;
@@ -1216,6 +1217,7 @@ int cr_set_option(cr_ctx *c, const char *key, int64_t v) {
     else if (!std::strcmp(key, "wf_xcd") && v >= 0 && v <= 7) c->wf_xcd = (uint32_t)v;
     else if (!std::strcmp(key, "wf_leaf_keys") && (v == 0 || v == 1)) c->wf_leaf_keys = (int)v;
     else if (!std::strcmp(key, "wf_resolve_paths") && v >= 0 && v <= 64) c->wf_resolve_paths = (uint32_t)v;
+    else if (!std::strcmp(key, "wf_measure_skip") && v >= 0 && v <= 3) c->wf_measure_skip = (uint32_t)v;
     else if (!std::strcmp(key, "wf_shade_waves") && (v == 6 || v == 8)) c->wf_shade_waves = (int)v;
     else if (!std::strcmp(key, "wf_shade_block") && (v == 256 || v == 512 || v == 1024)) c->wf_shade_block = (int)v;
     else if (!std::strcmp(key, "wf_app_chunk") && (v == 0 || (v >= 256 && v <= 65536 && !(v & (v - 1))))) c->wf_app_chunk = (int)v;

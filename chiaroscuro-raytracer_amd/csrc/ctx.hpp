@@ -128,6 +128,7 @@ struct cr_ctx {
     uint32_t wf_leaf_shift = 1; // ... its node index >> this (a leaf and its sibling share a key region)
     // sweep (1080p x 128 spp, 2 rounds): 0 / 1 / 2 / 4 / 8 / 16 / 64 -> 399.2 / 394.6 / 394.8 / 394.8 / 393.8 / 393.6 / 394.5 ms
     uint32_t wf_resolve_paths = 16; // wf_resolve in path order for queues of at least P / this rays (0: never)
+    uint32_t wf_measure_skip = 0;   // WfArgs::measure_skip (measurement only: wrong images)
     // WfArgs::shade_waves (option "wf_shade_waves": 6 or 8); round 4, two interleaved rounds: sponza
     // 322.5 / 322.9 vs 322.6 / 322.2 ms per layer, cornell_box 108.4 / 108.7 vs 107.6 / 107.3 ms per pass
     int wf_shade_waves = 8;

@@ -220,6 +220,9 @@ struct WfArgs {
     // record's w carries the leaf + 1 -- instead of pixel / world-position keys
     int leaf_keys;
     uint32_t resolve_paths; // wf_resolve sweeps queues of >= P / this rays in path order (0: never)
+    // measurement only (option "wf_measure_skip", WRONG images): bit 0 no wf_resolve launch, bit 1 no queue
+    // sort -- upper bounds of what a cheaper resolve / sort could gain
+    uint32_t measure_skip;
     uint32_t leaf_shift; // leaf keys: the node index >> leaf_shift (depth-first numbering: a run of
                          // consecutive nodes is one region of the tree)
     // Overlapped tail (launch_wavefront_chunk): the tail kernel for closest queue g + 1 starts beside

@@ -1487,7 +1487,7 @@ void wf_trace_geometry(int variant, int num_cus, uint32_t &block, uint32_t &bloc
 // pixel: the queue's keys are pixel keys (wf_shade of a generation below world_keys), which
 // need fewer bits than world keys -- one digit pass fewer for a rank's share of a frame
 static const uint32_t *order_queue(const WfArgs &W, int set, uint32_t n, hipStream_t st, int &err, bool pixel) {
-    if (!W.sort || err || n < W.sort_min) return nullptr;
+    if (!W.sort || err || n < W.sort_min || (W.measure_skip & 2u)) return nullptr;
     uint32_t *keys[2] = {W.key[set][0], W.key[set][1]}, *vals[2] = {W.perm[set][0], W.perm[set][1]};
     size_t tb = W.sort_tmp_bytes;
     const int bits = pixel ? W.key_bits_pixel : (set == 0 ? W.key_bits_s : W.key_bits);
@@ -1711,7 +1711,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
         if ((err = trace_event(te, st, TK_SHADOW, true))) break;
         hipLaunchKernelGGL(dead ? v.shadow_dead : v.shadow, dim3(sblocks), dim3(blk), lds, st, A, W, g);
         if ((err = trace_event(te, st, TK_SHADOW, false))) break;
-        hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
+        if (!(W.measure_skip & 1u)) hipLaunchKernelGGL(wf_resolve, dim3(sgrid), dim3(256), 0, st, A, W, g);
         W.ended_only = 0u;
         if (next || overlap)
             if ((err = (int)hipEventRecord(ss.join, ss.side)) || (err = (int)hipStreamWaitEvent(st, ss.join, 0)))
