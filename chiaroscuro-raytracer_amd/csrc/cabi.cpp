@@ -209,8 +209,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
                                          " does not exist (DESIGN.md §3 lists the measured builds that were removed)");
     if (c->perf_counters && (c->kernel != 2 || c->full_counters || !cr::wf_perf_available(A.variant)))
-        return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18 and 26 only, "
-                                     "without the counting build");
+        return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18, 26, 40, 42, 43, 44 "
+                                     "and 49 only, without the counting build");
     c->last_build = c->kernel == 2 ? (c->full_counters ? -1 : A.variant) : -2;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     {
@@ -1082,6 +1082,7 @@ static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, cons
     if (!c->has_scene) return fail(c, CR_E_NOSCENE, "no scene uploaded");
     if (n == 0) return CR_OK;
     if (!orig || !dir || !hit) return fail(c, CR_E_INVALID, "null query arrays");
+    if (shadow && (!dist || !light)) return fail(c, CR_E_INVALID, "null shadow distance / light arrays");
     HIPCHK(hipSetDevice(c->device));
     char *buf = nullptr;
     const size_t fbytes = (size_t)n * 3 * sizeof(float);
@@ -1095,10 +1096,11 @@ static int run_query(cr_ctx *c, uint32_t n, bool shadow, const float *orig, cons
     Q.shadow = shadow ? 1u : 0u;
     Q.stack_depth = c->stack_depth;
     float *d_orig = (float *)take(fbytes), *d_dir = (float *)take(fbytes);
-    float *d_dist = (float *)take(n * sizeof(float));
-    uint32_t *d_light = (uint32_t *)take(n * sizeof(uint32_t));
-    uint32_t *d_hit = (uint32_t *)take(n * sizeof(uint32_t)), *d_tri = (uint32_t *)take(n * sizeof(uint32_t));
-    float *d_bary = (float *)take(2 * n * sizeof(float)), *d_do = (float *)take(n * sizeof(float));
+    const size_t nb = (size_t)n * 4u; // bytes of one float / uint32 per query
+    float *d_dist = (float *)take(nb);
+    uint32_t *d_light = (uint32_t *)take(nb);
+    uint32_t *d_hit = (uint32_t *)take(nb), *d_tri = (uint32_t *)take(nb);
+    float *d_bary = (float *)take(2 * nb), *d_do = (float *)take(nb);
     hipError_t e = hipMemcpy(d_orig, orig, fbytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d_dir, dir, fbytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && shadow) e = hipMemcpy(d_dist, dist, n * sizeof(float), hipMemcpyHostToDevice);

@@ -6,6 +6,8 @@ glibc's sinf / cosf algorithm (equal to the host libm on every |x| < 120), so
 pixels, ray-query results and the query counters must be identical -- also
 against the oracle calling libm itself (test_parity_vs_libm_trig_oracle).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -621,6 +623,15 @@ def test_ray_queries_bitexact(ca, sponza, cornell):
         dist = (rng.random(n) * np.linalg.norm(hi - lo)).astype(np.float32)
         assert np.array_equal(pair.dev.intersect_shadow(o, d, dist, light),
                               pair.oracle.intersect_shadow(o, d, dist, light))
+        # a shadow query without its distance or light arrays is refused, not read through a null pointer
+        lib, hit = ca.libs()[0], np.zeros(n, np.uint32)
+        o, d = np.ascontiguousarray(o, np.float32), np.ascontiguousarray(d, np.float32)
+        dist, light = np.ascontiguousarray(dist, np.float32), np.ascontiguousarray(light, np.uint32)
+        for dp, lp in ((None, light), (dist, None)):
+            rc = lib.cr_intersect_shadow(pair.dev._c, n, ca._ptr(o), ca._ptr(d), None if dp is None else ca._ptr(dp),
+                                         None if lp is None else ca._ptr(lp, ctypes.c_uint32),
+                                         ca._ptr(hit, ctypes.c_uint32))
+            assert ca.CR_ERRORS.get(rc) == "CR_E_INVALID"
 
 
 @pytest.mark.parametrize("case", ["cornell", "sponza", "nanobox"])
