@@ -1,4 +1,4 @@
-"""SIMD-efficiency diagnostics of the persistent kernel (one counting launch).
+"""SIMD-efficiency diagnostics of the wavefront kernel's counting build (one counting render).
     python scripts/diag.py [--config sponza] [--spp 8]
 lane efficiency of a phase = lane work / (64 x wave iterations of that phase)."""
 import argparse

@@ -1,5 +1,5 @@
 /* Exactness check of the kd-descent split distance with a per-ray reciprocal
- * (persistent.hip split_distance_r):
+ * (device_math.hpp div_by_rcp, the FD trace builds):
  *     y  = RN(1/b)                  once per ray and axis
  *     q0 = RN(a*y);  r = fma(-q0, b, a);  q = fma(r, y, q0)
  * claimed equal to RN(a/b) whenever 2^-40 <= |b| <= 2^40 and 2^-60 <= |q0| <= 2^60.
