@@ -96,14 +96,14 @@ __device__ __forceinline__ bool tri_test(f3 o, f3 d, const TriRec &r, float tmax
 // tri_test with the scalar unit in mind (BF trace builds): the early exits are
 // wave-uniform (taken when no active lane can still accept) and the lanes that
 // already failed compute on, masked by `ok`, so no exec-mask bookkeeping runs per
-// test.  Same values, same acceptance.
+// test.  Same values, same acceptance.  live: false for a lane with no test (it never accepts).
 __device__ __forceinline__ bool tri_test_wave(f3 o, f3 d, const TriRec &r, float tmax, float &ux, float &uy,
-                                              float &t) {
+                                              float &t, bool live = true) {
     const f3 v0 = ld3(r.a), e1 = ld3(r.b), e2 = ld3(r.c);
     const f3 p = cross(d, e2);
     const float aa = dot(e1, p);
     // (bitwise logic on the lane masks: no short-circuit exec branches)
-    bool ok = !((aa < 1.19209290e-7F) & (aa > -1.19209290e-7F));
+    bool ok = live & !((aa < 1.19209290e-7F) & (aa > -1.19209290e-7F));
     if (!__ballot(ok)) return false;
     const float f = rcp_rn_wave(aa);
     const f3 sv = sub(o, v0);

@@ -15,6 +15,7 @@ enum : uint32_t {
     ST_MISS = 6,
     ST_OCCLUDED = 7,
     ST_VISIBLE = 8,
+    ST_LEAFX = 9,     // LX builds: the lane's leaf tests wait for the wave's leaf exchange (leaf_exchange)
 };
 
 // True when every active lane holds the same x.
@@ -337,14 +338,39 @@ struct TraceDefaults {
     static constexpr int LC = 0;          // leaf cull records (4 packed, 5 compressed)
     static constexpr bool PC = false;     // performed-work counters (measurement only)
     static constexpr bool DEAD = false;   // shadow queues with dead entries (wf_shade's chunked appends) skipped
+    static constexpr bool LX = false;     // a divergent leaf's masked tests spread over the wave (leaf_exchange)
 };
+
+// A lane's deferred leaf (LX builds): the references of the leaf whose first record is `first` that its
+// cull mask keeps (bit j: first + j).
+struct LeafX {
+    uint32_t mask, first;
+};
+
+// The stack's top entry becomes the query's node and interval (stack invariant).
+template <int R>
+__device__ __forceinline__ void trav_pop(uint2 *ring, uint2 *gstk, uint32_t gstride, uint32_t gid, Trav &T,
+                                         Pc *pc = nullptr) {
+    T.sp--;
+    uint2 e;
+    if (T.nl) {
+        e = ring[(T.sp & (R - 1)) * blockDim.x + threadIdx.x];
+        T.nl--;
+    } else {
+        e = gstack_at(gstk, T.sp, gstride, gid);
+        if (pc) pc->vb += 8;
+    }
+    T.node = e.x;
+    T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
+    T.tmax = __uint_as_float(e.y);
+}
 
 template <class C>
 __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, const DevScene &S, uint2 *ring, uint2 *gstk, uint32_t gstride,
                                                uint32_t gid, f3 o, f3 &d, bool shadow, uint32_t exclude, Trav &T,
                                                Ctr &c, float csx = 0.f, float csy = 0.f, const float4 *cull = nullptr,
                                                const float4 *cull_node = nullptr, Diag *dg = nullptr,
-                                               Pc *pc = nullptr, uint32_t quorum = 0) {
+                                               Pc *pc = nullptr, uint32_t quorum = 0, LeafX *lx = nullptr) {
     static constexpr int R = C::R, CULL = C::CULL, LC = C::LC;
     static constexpr bool FULL = C::FULL, FD = C::FD, SC = C::SC, FAT = C::FAT, BF = C::BF;
     // quorum (lean FAT builds without the camera cull): the wave's descent stops at a fetch once at most
@@ -367,6 +393,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(!CULL || (BF && SC && !FULL), "cull: lean BF + SC builds");
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     static_assert(!LC || ((LC == 4 || LC == 5) && !CULL && BF && SC && !FULL), "leaf cull: lean BF + SC builds, forms 4 / 5");
+    static_assert(!C::LX || (LC && !C::PC), "leaf exchange: lean leaf-cull builds");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -434,21 +461,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     bool culled = false;
     uint32_t first, count, lmask;
     bool lin;
-    // the stack's top entry becomes the query's node and interval (stack invariant)
-    auto pop_entry = [&]() {
-        T.sp--;
-        uint2 e;
-        if (T.nl) {
-            e = ring[(T.sp & (R - 1)) * bdim + tid];
-            T.nl--;
-        } else {
-            e = gstack_at(gstk, T.sp, gstride, gid);
-            if (pc) pc->vb += 8;
-        }
-        T.node = e.x;
-        T.tmin = T.tmax; // == the popped entry's split distance (stack invariant)
-        T.tmax = __uint_as_float(e.y);
-    };
+    auto pop_entry = [&]() { trav_pop<R>(ring, gstk, gstride, gid, T, pc); };
     if (FAT) { // two levels per dependent load: a node's record carries its children's
         uint4 f0, f1;
         auto fetch = [&](uint32_t node) {
@@ -681,6 +694,12 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
             tally_tri(first + j);
             if (!test(srec(base + (size_t)REC_STRIDE * j))) break;
         }
+    } else if (C::LX && LC && count <= (uint32_t)LC_MAXREFS) { // tests deferred to the wave's leaf exchange
+        if (lmask) {
+            lx->mask = lmask;
+            lx->first = first;
+            return ST_LEAFX;
+        }
     } else if (LC && count <= (uint32_t)LC_MAXREFS) { // the mask's references, pipelined one ahead
         uint32_t m = lmask;
         if (pc) { // the divergent leaf loop's shape: iterations = the largest lane mask
@@ -733,6 +752,125 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     if (T.sp == 0) return shadow ? ST_VISIBLE : ST_MISS;
     pop_entry();
     return shadow ? ST_SHADOW : ST_CLOSEST;
+}
+
+// ------------------------------------------------------------ leaf exchange --
+// LX builds.  In a divergent leaf round the leaf cull leaves tests in ~16 of a wave's lanes, ~5 each, and
+// the per-lane loop runs as long as the longest mask: 6 iterations at 0.2 of the lanes.
+// Here the whole wave (every lane, busy or idle) tests the round's (lane, reference) pairs 64 at a time:
+// pair i belongs to the lane whose exclusive prefix of mask popcounts is the largest one <= i, and is that
+// lane's (i - prefix)-th mask bit.  The answers are the per-lane loop's:
+//   shadow: occluded == some masked reference other than the excluded one accepts for [0, tmax] -- an OR,
+//           whatever the order (kdtree.cpp:309-320);
+//   closest: the loop keeps a hit when t < the current tmax, so it ends with the smallest t over the
+//           accepting references and, among equal t (+0 == -0), the first in mask order
+//           (kdtree.cpp:235-246); the pairs are reduced in ascending (window, lane) = mask order with a
+//           strict <, which selects the same reference, and its own ux, uy, t are taken.
+// Every lane of the wave must be active.  marks: 64 words of LDS owned by the wave.
+
+// the position of the q-th (from 0) set bit of m (q < popcount(m))
+__device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t q) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t w = 16; w >= 1; w >>= 1) {
+        const uint32_t c = (uint32_t)__builtin_popcount(m & ((1u << w) - 1u));
+        const bool up = q >= c;
+        q = up ? q - c : q;
+        m = up ? m >> w : m;
+        pos = up ? pos + w : pos;
+    }
+    return pos;
+}
+__device__ __forceinline__ uint32_t bperm(uint32_t addr, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)v);
+}
+__device__ __forceinline__ float bpermf(uint32_t addr, float v) { return __uint_as_float(bperm(addr, __float_as_uint(v))); }
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+template <bool SHADOW>
+__device__ __forceinline__ void leaf_exchange(const DevScene &S, volatile lds_u32 *lx, uint32_t m, uint32_t first,
+                                              f3 o, f3 d, float tmax, uint32_t exclude, bool &occluded, bool &found,
+                                              float &bx, float &by, float &bt, uint32_t &tri) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = (uint32_t)__builtin_popcount(m);
+    // exclusive prefix P of c over the lanes and the total, bit-sliced (c <= 32)
+    uint32_t P = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+        const uint64_t bal = __ballot((c >> b) & 1u);
+        P += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u)) << b;
+        total += (uint32_t)__popcll(bal) << b;
+    }
+    // this lane's pairs: [P, E) (packed: one register through the exchange)
+    const uint32_t pe = P | ((P + c) << 16);
+    occluded = found = false;
+    // lx: [0, 64) the window's start marks, [64, 128) every lane's mask, [128, 192) its leaf's first record
+    // (read from LDS by the pairs' testers, so they hold no registers during the exchange)
+    volatile lds_u32 *const marks = lx;
+    lx[64 + lane] = m;
+    lx[128 + lane] = first;
+    uint32_t carry = 0, carry_q = 0; // the owner of the pair before the window, and its rank + 1
+    for (uint32_t base = 0; base < total; base += 64u) {
+        // the owner of pair base + lane: the last lane that starts at or before it
+        uint32_t ln = threadIdx.x & 63u; // (re-derived per window: values hoisted out of this loop hold registers)
+        asm volatile("" : "+v"(ln));
+        marks[ln] = 0u;
+        const uint32_t P0 = pe & 0xffffu, E0 = pe >> 16;
+        if (E0 > P0 && P0 >= base && P0 < base + 64u) marks[P0 - base] = ln + 1u;
+        const uint32_t mv = marks[ln];
+        // the last start at or before this lane: s = ln - (its distance below), none when the shifted mask is 0
+        const uint64_t upto = __ballot(mv != 0u) << (63u - ln);
+        const uint32_t back = upto ? (uint32_t)__builtin_clzll(upto) : 0u;
+        const uint32_t sm = bperm((ln - back) << 2, mv);
+        const uint32_t owner = upto ? sm - 1u : carry;
+        // q: the pair's rank among its owner's (a carried owner started before the window)
+        const uint32_t q = upto ? back : ln + carry_q;
+        carry = __builtin_amdgcn_readlane(owner, 63);
+        carry_q = __builtin_amdgcn_readlane(q, 63) + 1u;
+        const bool live = base + ln < total;
+        const uint32_t a = owner << 2;
+        const uint32_t om = lx[64 + owner], of = lx[128 + owner];
+        const f3 oo = mk(bpermf(a, o.x), bpermf(a, o.y), bpermf(a, o.z));
+        const f3 od = mk(bpermf(a, d.x), bpermf(a, d.y), bpermf(a, d.z));
+        const float ot = bpermf(a, tmax);
+        const uint32_t j = nth_bit(om, q);                    // (any value < 32 for a dead lane)
+        const uint32_t ref = live ? of + j : 0u;              // (record 0: a dead lane's harmless load)
+        const TriRec r = load_rec(S, ref);
+        float ux, uy, t;
+        bool acc = tri_test_wave(oo, od, r, ot, ux, uy, t, live);
+        if (SHADOW) {
+            acc = acc & (rec_id(r) != bperm(a, exclude));
+            const uint64_t h = __ballot(acc);
+            // this lane's pairs in the window: [lo, hi)
+            const uint32_t P1 = pe & 0xffffu, E1 = pe >> 16;
+            const int lo = (int)P1 - (int)base, hi = (int)E1 - (int)base;
+            const int l = lo < 0 ? 0 : lo, e = hi > 64 ? 64 : hi;
+            if (h && l < e) {
+                const uint64_t bits = h >> l;
+                occluded = occluded | ((e - l == 64 ? bits : bits & ((1ull << (e - l)) - 1ull)) != 0ull);
+            }
+            // every lane with pairs past the window is occluded already: done
+            if (!__ballot(E1 > P1 && !occluded && E1 > base + 64u)) break;
+        } else {
+            uint64_t h = __ballot(acc);
+            while (h) { // ascending lanes = ascending mask order within each owner
+                const uint32_t w = (uint32_t)__builtin_ctzll(h);
+                h &= h - 1ull;
+                const uint32_t ow = __builtin_amdgcn_readlane(owner, w);
+                const float tw = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(t), w));
+                const float uxw = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ux), w));
+                const float uyw = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uy), w));
+                const uint32_t idw = __builtin_amdgcn_readlane(rec_id(r), w);
+                const bool take = lane == ow && (!found || (__float_as_uint(tw) & 0x7fffffffu) <
+                                                               (__float_as_uint(bt) & 0x7fffffffu));
+                found = found | take;
+                bt = take ? tw : bt;
+                bx = take ? uxw : bx;
+                by = take ? uyw : by;
+                tri = take ? idw : tri;
+            }
+        }
+    }
 }
 
 // Per-query tallies are wave-aggregated LDS atomics: the callers run in

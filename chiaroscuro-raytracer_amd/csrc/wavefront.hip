@@ -412,19 +412,45 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
             if (!__any(state != ST_DONE)) break;
             continue;
         }
-        if (state == busy_st) {
-            const uint32_t r = trav_round<C>(A.lc_debug, A.lc_min,
+        LeafX lx = {0u, 0u};
+        uint32_t r = busy_st;
+        if (state == busy_st)
+            r = trav_round<C>(A.lc_debug, A.lc_min,
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, csx, csy, A.cull,
-                A.cull_node, FULL ? &dg : nullptr, PC ? &pc : nullptr, A.desc_quorum);
-            if (r != busy_st) {
-                if (PC) pc.vb += SHADOW ? (W.vis_mark ? (r == ST_OCCLUDED ? 0u : 1u) : 4u) : 16u;
-                if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
-                // w: the hit's leaf + 1, the queue sort's key region
-                else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
-                                                           __float_as_uint(d.y), T.node + 1u)
-                                              : make_uint4(0u, 0u, 0u, 0u);
-                state = ST_NEED_WORK;
+                A.cull_node, FULL ? &dg : nullptr, PC ? &pc : nullptr, A.desc_quorum, C::LX ? &lx : nullptr);
+        // LX: the deferred leaves' tests by the whole wave (traverse.hpp leaf_exchange), then each deferred
+        // lane ends its round as trav_round does after a leaf
+        if (C::LX && __ballot(r == ST_LEAFX)) {
+            __shared__ uint32_t lx_lds[4][192]; // per wave (blocks of 256 threads: wf_trace_geometry)
+            bool occl, fnd;
+            float bx = 0.f, by = 0.f, bt = 0.f;
+            uint32_t tri = 0u;
+            const bool deferred = r == ST_LEAFX;
+            leaf_exchange<SHADOW>(S, (volatile lds_u32 *)lx_lds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], deferred ? lx.mask : 0u,
+                                  lx.first, o, d, T.tmax, exclude, occl, fnd, bx, by, bt, tri);
+            if (deferred) {
+                if (occl) {
+                    r = ST_OCCLUDED;
+                } else if (fnd) {
+                    d = mk(bx, by, __uint_as_float(tri));
+                    T.tmax = bt;
+                    r = ST_HIT;
+                } else if (T.sp == 0) {
+                    r = SHADOW ? ST_VISIBLE : ST_MISS;
+                } else {
+                    trav_pop<C::R>(ring_lds, W.gstack, W.gstride, gid, T);
+                    r = busy_st;
+                }
             }
+        }
+        if (state == busy_st && r != busy_st) { // the query's result: the answer stored, the lane free
+            if (PC) pc.vb += SHADOW ? (W.vis_mark ? (r == ST_OCCLUDED ? 0u : 1u) : 4u) : 16u;
+            if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
+            // w: the hit's leaf + 1, the queue sort's key region
+            else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
+                                                       __float_as_uint(d.y), T.node + 1u)
+                                          : make_uint4(0u, 0u, 0u, 0u);
+            state = ST_NEED_WORK;
         }
     }
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
@@ -1276,6 +1302,7 @@ struct WfVariant {
     // the shadow trace of a queue wf_shade appended in chunks (its dead entries skipped); null: the build's
     // wf_shade appends per iteration
     void (*shadow_dead)(RenderArgs, WfArgs, uint32_t) = nullptr;
+    int shadow_waves = 0; // waves per SIMD of the shadow trace's grid (0: waves_per_simd)
 };
 
 // The trace configurations of the builds (traverse.hpp TraceDefaults), by what they restate.
@@ -1301,6 +1328,12 @@ struct ShadowFatFdDead : ShadowFatFd { static constexpr bool DEAD = true; };
 struct ClosestFatLc5 : Fat { static constexpr int LC = 5; };
 struct ShadowFatLc5Fd : ClosestFatLc5 { static constexpr bool SHADOW = true, FD = true; };
 struct ShadowFatLc5FdDead : ShadowFatLc5Fd { static constexpr bool DEAD = true; };
+// + the leaf exchange (traverse.hpp leaf_exchange: a divergent leaf's masked tests spread over the wave)
+struct ClosestFatLc5Lx : ClosestFatLc5 { static constexpr bool LX = true; };
+struct ShadowFatLc5FdLx : ShadowFatLc5Fd { static constexpr bool LX = true; };
+struct ShadowFatLc5FdDeadLx : ShadowFatLc5FdDead { static constexpr bool LX = true; };
+struct ShadowFatLc5FdLx7 : ShadowFatLc5FdLx { static constexpr int MINW = 7; };
+struct ShadowFatLc5FdDeadLx7 : ShadowFatLc5FdDeadLx { static constexpr int MINW = 7; };
 struct ClosestFatLc5Perf : ClosestFatLc5 { static constexpr bool PC = true; };
 struct ShadowFatLc5Perf : ClosestFatLc5Perf { static constexpr bool SHADOW = true; };
 // the performed-work counting instances (RenderArgs::perf_counters; measurement only)
@@ -1355,6 +1388,14 @@ static const WfBuild kWf[] = {
     //     (leafcull.hpp LC_RECC: boxes on the scene's 16-bit grid, octahedral axes, half constants)
     {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 2, 1, 5,
           wf_trace<tc::ShadowFatLc5FdDead>}},
+    // 53 / 54: 49 whose shadow trace (53) or shadow and secondary closest traces (54) test a divergent
+    //     leaf round's masked references with the whole wave (the leaf exchange)
+    {53, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5FdLx>, 8, 8, 2, 1, 5,
+          wf_trace<tc::ShadowFatLc5FdDeadLx>}},
+    {55, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5FdLx7>, 8, 8, 2, 1, 5,
+          wf_trace<tc::ShadowFatLc5FdDeadLx7>, 7}},
+    {54, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5Lx>, wf_trace<tc::ShadowFatLc5FdLx>, 8, 8, 2, 1, 5,
+          wf_trace<tc::ShadowFatLc5FdDeadLx>}},
 };
 static const int kNumWf = (int)(sizeof(kWf) / sizeof(kWf[0]));
 // the build numbered `variant`, or null when it is not compiled in
@@ -1623,7 +1664,8 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
                                            : wf_build_or_ref(A.variant);
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
-    const uint32_t cblocks = blocks, sblocks = blocks;
+    const uint32_t cblocks = blocks;
+    const uint32_t sblocks = v.shadow_waves ? blocks / (uint32_t)v.waves_per_simd * (uint32_t)v.shadow_waves : blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds =
@@ -1730,7 +1772,8 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
                                            : wf_build_or_ref(A.variant);
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
-    const uint32_t cblocks = blocks, sblocks = blocks;
+    const uint32_t cblocks = blocks;
+    const uint32_t sblocks = v.shadow_waves ? blocks / (uint32_t)v.waves_per_simd * (uint32_t)v.shadow_waves : blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     for (int i = 0; i < nl; i++)
         if (L[i].W.gstride < blk * blocks || L[i].W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;

@@ -20,8 +20,9 @@ ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit",
 # keeps their numbers): the plain reference build 0, 15 (the packet camera
 # trace's fallback), round 2's default 18, 26 (leaf cull records), 40 / 42 (26 / 18 with the exact
 # short division in the camera packet), 43 / 44 (40 / 42 with it in the shadow trace) and the default 49
-# (43 with the compressed leaf cull records)
-TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44, 49]
+# (43 with the compressed leaf cull records); 53 / 54 / 55 (49 with the leaf exchange in the shadow trace,
+# in the shadow and secondary closest traces, and in the shadow trace at 7 waves per SIMD)
+TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44, 49, 53, 54, 55]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
 QUORUM_DEFAULT = -1  # ctx.hpp desc_quorum (8, but 0 for 1024 <= triangles < 65536)
