@@ -158,8 +158,10 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // 3.54 -> 3.55 on cornell_box (short packets: the reciprocals cost what they save);
     // 43 / 44 = 40 / 42 with the short division in the shadow trace too: 358.2 -> 356.4 ms, nanobox
     // 163.7 -> 162.4 ms; 49 = 43 with the compressed leaf cull records (round 5: 48 B per leaf, three
-    // loads instead of six): 2179 -> 2252 Mray/s at the driver's command, shadow 41.7 -> 40.0 ms
-    A.variant = c->variant >= 0 ? c->variant : (c->n_tris >= LEAF_CULL_MIN_TRIS ? 49 : 44);
+    // loads instead of six): 2179 -> 2252 Mray/s at the driver's command, shadow 41.7 -> 40.0 ms;
+    // 54 = 49 with the leaf exchange in the shadow and secondary closest traces (round 6: a divergent leaf
+    // round's masked tests spread over the whole wave): 2315 -> 2362 Mray/s, shadow 39.2 -> 38.3 ms
+    A.variant = c->variant >= 0 ? c->variant : (c->n_tris >= LEAF_CULL_MIN_TRIS ? 54 : 44);
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
@@ -209,8 +211,8 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
         return fail(c, CR_E_INVALID, "trace build " + std::to_string(A.variant) +
                                          " does not exist (DESIGN.md §3 lists the measured builds that were removed)");
     if (c->perf_counters && (c->kernel != 2 || c->full_counters || !cr::wf_perf_available(A.variant)))
-        return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18, 26, 40, 42, 43, 44 "
-                                     "and 49 only, without the counting build");
+        return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18, 26, 40, 42, 43, 44, "
+                                     "49 and 53-57 only, without the counting build");
     c->last_build = c->kernel == 2 ? (c->full_counters ? -1 : A.variant) : -2;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     {

@@ -16,14 +16,22 @@ struct Ctr {
     uint32_t leaf_rounds = 0, leaf_distinct = 0, leaf_records = 0, leaf_fit21 = 0, leaf_fit56 = 0;
 };
 __device__ __forceinline__ uint32_t wave_count(bool pred) { return (uint32_t)__popcll(__ballot(pred)); }
+// The lane's index in its wave, recomputed at every use (two VALU; volatile: never hoisted or shared),
+// so the trace kernels' persistent loops hold no register with threadIdx.x (at 64 VGPRs it was spilled).
+__device__ __forceinline__ uint32_t lane_id() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 // True in exactly one active lane (the lowest): `if (wave_leader()) n++` counts
 // iterations of the enclosing (possibly divergent) loop as the WAVE executes them.
 __device__ __forceinline__ bool wave_leader() {
-    return (threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
+    return lane_id() == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
 }
 
 // Call with the whole wave converged.
 __device__ __forceinline__ void flush_counters(unsigned long long *ctrs, const Ctr &c, uint32_t uniform = 0u) {
+    const uint32_t ln = lane_id();
     const uint32_t v[CTR_N] = {c.closest,   c.shadow,    c.inner,      c.leaf,       c.tritest,
                                c.hit,       c.texhit,    c.paths,      c.pixels,     c.wave_desc,
                                c.wave_tri,  c.wave_round, c.wave_query, c.wave_desc_uniform, c.wave_tri_uniform,
@@ -36,7 +44,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long *ctrs, const C
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
         }
-        if ((threadIdx.x & 63) == 0 && s) atomicAdd(&ctrs[i], s);
+        if (ln == 0 && s) atomicAdd(&ctrs[i], s);
     }
 }
 

@@ -56,12 +56,13 @@ __device__ __forceinline__ void diag_begin(Diag *dg) {
     if (dg) dg->n = 0;
 }
 __device__ __forceinline__ void diag_flush(unsigned long long *ctrs, const Diag &dg) {
+    const uint32_t ln = lane_id();
 #pragma unroll
     for (int i = 0; i < DIAG_N; i++) {
         unsigned long long s = dg.v[i];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-        if ((threadIdx.x & 63) == 0 && s) atomicAdd(&ctrs[CTR_DIAG + i], s);
+        if (ln == 0 && s) atomicAdd(&ctrs[CTR_DIAG + i], s);
     }
 }
 
@@ -80,6 +81,7 @@ __device__ __forceinline__ void pc_load(Pc *pc, bool scalar, uint32_t bytes) {
 }
 // Call with the whole wave converged: the lane sums go to ctrs[0 .. PERF_N).
 __device__ __forceinline__ void pc_flush(unsigned long long *ctrs, const Pc &pc) {
+    const uint32_t ln = lane_id();
     const unsigned long long v[PERF_N] = {pc.q,     pc.steps,   pc.leaves, pc.masks,  pc.tests,  pc.vb,
                                           pc.sb,    pc.waves,   pc.drounds, pc.diters, pc.dlanes, pc.dtests};
 #pragma unroll
@@ -87,7 +89,7 @@ __device__ __forceinline__ void pc_flush(unsigned long long *ctrs, const Pc &pc)
         unsigned long long x = v[i];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&ctrs[i], x);
+        if (ln == 0 && x) atomicAdd(&ctrs[i], x);
     }
 }
 
@@ -348,6 +350,8 @@ struct LeafX {
 };
 
 // The stack's top entry becomes the query's node and interval (stack invariant).
+// ring: the LDS ring's column of the wave's lane 0 ([slot][blockDim.x]); gstk as gstack_at's.
+// ring: the LDS ring [slot][blockDim.x]; gstk / gid: the stack-overflow area and the lane's global index.
 template <int R>
 __device__ __forceinline__ void trav_pop(uint2 *ring, uint2 *gstk, uint32_t gstride, uint32_t gid, Trav &T,
                                          Pc *pc = nullptr) {
@@ -393,7 +397,7 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
     static_assert(!CULL || (BF && SC && !FULL), "cull: lean BF + SC builds");
     static_assert(CULL < 2 || FAT, "subtree cull: fat-record builds");
     static_assert(!LC || ((LC == 4 || LC == 5) && !CULL && BF && SC && !FULL), "leaf cull: lean BF + SC builds, forms 4 / 5");
-    static_assert(!C::LX || (LC && !C::PC), "leaf exchange: lean leaf-cull builds");
+    static_assert(!C::LX || LC, "leaf exchange: leaf-cull builds");
     const uint32_t bdim = blockDim.x, tid = threadIdx.x;
     // one kd decision at inner node nd (kdtree.cpp:258-275): T.node = the child to
     // descend into (child + k), the far child pushed when both are crossed
@@ -790,9 +794,17 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 template <bool SHADOW>
 __device__ __forceinline__ void leaf_exchange(const DevScene &S, volatile lds_u32 *lx, uint32_t m, uint32_t first,
                                               f3 o, f3 d, float tmax, uint32_t exclude, bool &occluded, bool &found,
-                                              float &bx, float &by, float &bt, uint32_t &tri) {
-    const uint32_t lane = threadIdx.x & 63u;
+                                              float &bx, float &by, float &bt, uint32_t &tri, Pc *pc = nullptr) {
+    const uint32_t lane = lane_id();
     const uint32_t c = (uint32_t)__builtin_popcount(m);
+    if (pc) { // the exchange's shape: rounds, windows (diters), owner lanes and their pairs
+        const uint32_t owners = (uint32_t)__popcll(__ballot(c > 0u));
+        if (wave_leader()) {
+            pc->drounds++;
+            pc->dlanes += owners;
+        }
+        pc->dtests += c;
+    }
     // exclusive prefix P of c over the lanes and the total, bit-sliced (c <= 32)
     uint32_t P = 0, total = 0;
 #pragma unroll
@@ -812,8 +824,7 @@ __device__ __forceinline__ void leaf_exchange(const DevScene &S, volatile lds_u3
     uint32_t carry = 0, carry_q = 0; // the owner of the pair before the window, and its rank + 1
     for (uint32_t base = 0; base < total; base += 64u) {
         // the owner of pair base + lane: the last lane that starts at or before it
-        uint32_t ln = threadIdx.x & 63u; // (re-derived per window: values hoisted out of this loop hold registers)
-        asm volatile("" : "+v"(ln));
+        const uint32_t ln = lane_id(); // (re-derived per window: values hoisted out of this loop hold registers)
         marks[ln] = 0u;
         const uint32_t P0 = pe & 0xffffu, E0 = pe >> 16;
         if (E0 > P0 && P0 >= base && P0 < base + 64u) marks[P0 - base] = ln + 1u;
@@ -830,14 +841,45 @@ __device__ __forceinline__ void leaf_exchange(const DevScene &S, volatile lds_u3
         const bool live = base + ln < total;
         const uint32_t a = owner << 2;
         const uint32_t om = lx[64 + owner], of = lx[128 + owner];
-        const f3 oo = mk(bpermf(a, o.x), bpermf(a, o.y), bpermf(a, o.z));
-        const f3 od = mk(bpermf(a, d.x), bpermf(a, d.y), bpermf(a, d.z));
-        const float ot = bpermf(a, tmax);
         const uint32_t j = nth_bit(om, q);                    // (any value < 32 for a dead lane)
         const uint32_t ref = live ? of + j : 0u;              // (record 0: a dead lane's harmless load)
         const TriRec r = load_rec(S, ref);
+        if (pc) {
+            if (wave_leader()) pc->diters++;
+            pc->tests += live ? 1u : 0u;
+            pc->vb += live ? 16u * REC_STRIDE : 0u;
+        }
+        // tri_test_wave's arithmetic with the owner's ray fetched in stages (the direction, then the origin,
+        // then tmax), each where it is first used: the scheduler keeps them apart (fewer live registers)
         float ux, uy, t;
-        bool acc = tri_test_wave(oo, od, r, ot, ux, uy, t, live);
+        bool acc;
+        {
+            const f3 od = mk(bpermf(a, d.x), bpermf(a, d.y), bpermf(a, d.z));
+            const f3 v0 = ld3(r.a), e1 = ld3(r.b), e2 = ld3(r.c);
+            const f3 p = cross(od, e2);
+            const float aa = dot(e1, p);
+            bool ok = live & !((aa < 1.19209290e-7F) & (aa > -1.19209290e-7F));
+            acc = false;
+            if (__ballot(ok)) {
+                __builtin_amdgcn_sched_barrier(0);
+                const f3 oo = mk(bpermf(a, o.x), bpermf(a, o.y), bpermf(a, o.z));
+                const float f = rcp_rn_wave(aa);
+                const f3 sv = sub(oo, v0);
+                ux = f * dot(sv, p);
+                ok = ok & !((ux < 0.f) | (ux > 1.f));
+                if (__ballot(ok)) {
+                    const f3 qv = cross(sv, e1);
+                    uy = f * dot(od, qv);
+                    ok = ok & !((uy < 0.f) | (uy + ux > 1.f));
+                    if (__ballot(ok)) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        const float ot = bpermf(a, tmax);
+                        t = f * dot(e2, qv);
+                        acc = ok & (t >= 0.f) & (t < ot);
+                    }
+                }
+            }
+        }
         if (SHADOW) {
             acc = acc & (rec_id(r) != bperm(a, exclude));
             const uint64_t h = __ballot(acc);
@@ -861,7 +903,7 @@ __device__ __forceinline__ void leaf_exchange(const DevScene &S, volatile lds_u3
                 const float uxw = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ux), w));
                 const float uyw = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uy), w));
                 const uint32_t idw = __builtin_amdgcn_readlane(rec_id(r), w);
-                const bool take = lane == ow && (!found || (__float_as_uint(tw) & 0x7fffffffu) <
+                const bool take = lane_id() == ow && (!found || (__float_as_uint(tw) & 0x7fffffffu) <
                                                                (__float_as_uint(bt) & 0x7fffffffu));
                 found = found | take;
                 bt = take ? tw : bt;

@@ -323,6 +323,7 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
     extern __shared__ uint2 ring_lds[];
     const DevScene &S = A.S;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t n = SHADOW ? *cnt_shadow(W, g) : *cnt_closest(W, g);
     uint32_t *work = SHADOW ? work_shadow(W, g) : work_closest(W, g);
     const float4 *rays = SHADOW ? W.sray : W.ray[g & 1];
@@ -412,12 +413,31 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
             if (!__any(state != ST_DONE)) break;
             continue;
         }
+        // the query's result: the answer stored, the lane free
+        auto answer = [&](uint32_t r) {
+            if (PC) pc.vb += SHADOW ? (W.vis_mark ? (r == ST_OCCLUDED ? 0u : 1u) : 4u) : 16u;
+            if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
+            // w: the hit's leaf + 1, the queue sort's key region
+            else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
+                                                       __float_as_uint(d.y), T.node + 1u)
+                                          : make_uint4(0u, 0u, 0u, 0u);
+            state = ST_NEED_WORK;
+        };
+        if (!C::LX) {
+            if (state == busy_st) {
+                const uint32_t r = trav_round<C>(A.lc_debug, A.lc_min, S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T,
+                                                 c, csx, csy, A.cull, A.cull_node, FULL ? &dg : nullptr,
+                                                 PC ? &pc : nullptr, A.desc_quorum);
+                if (r != busy_st) answer(r);
+            }
+            continue;
+        }
         LeafX lx = {0u, 0u};
         uint32_t r = busy_st;
         if (state == busy_st)
             r = trav_round<C>(A.lc_debug, A.lc_min,
                 S, ring_lds, W.gstack, W.gstride, gid, o, d, SHADOW, exclude, T, c, csx, csy, A.cull,
-                A.cull_node, FULL ? &dg : nullptr, PC ? &pc : nullptr, A.desc_quorum, C::LX ? &lx : nullptr);
+                A.cull_node, FULL ? &dg : nullptr, PC ? &pc : nullptr, A.desc_quorum, &lx);
         // LX: the deferred leaves' tests by the whole wave (traverse.hpp leaf_exchange), then each deferred
         // lane ends its round as trav_round does after a leaf
         if (C::LX && __ballot(r == ST_LEAFX)) {
@@ -426,8 +446,8 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
             float bx = 0.f, by = 0.f, bt = 0.f;
             uint32_t tri = 0u;
             const bool deferred = r == ST_LEAFX;
-            leaf_exchange<SHADOW>(S, (volatile lds_u32 *)lx_lds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], deferred ? lx.mask : 0u,
-                                  lx.first, o, d, T.tmax, exclude, occl, fnd, bx, by, bt, tri);
+            leaf_exchange<SHADOW>(S, (volatile lds_u32 *)lx_lds[wave], deferred ? lx.mask : 0u,
+                                  lx.first, o, d, T.tmax, exclude, occl, fnd, bx, by, bt, tri, PC ? &pc : nullptr);
             if (deferred) {
                 if (occl) {
                     r = ST_OCCLUDED;
@@ -443,15 +463,7 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
                 }
             }
         }
-        if (state == busy_st && r != busy_st) { // the query's result: the answer stored, the lane free
-            if (PC) pc.vb += SHADOW ? (W.vis_mark ? (r == ST_OCCLUDED ? 0u : 1u) : 4u) : 16u;
-            if (SHADOW) shadow_store(W, g, idx, r == ST_OCCLUDED);
-            // w: the hit's leaf + 1, the queue sort's key region
-            else W.hit[g & 1][idx] = r == ST_HIT ? make_uint4(__float_as_uint(d.z), __float_as_uint(d.x),
-                                                       __float_as_uint(d.y), T.node + 1u)
-                                          : make_uint4(0u, 0u, 0u, 0u);
-            state = ST_NEED_WORK;
-        }
+        if (state == busy_st && r != busy_st) answer(r);
     }
     if (SHADOW) c.shadow = issued; // queries, box-culled ones included
     else c.closest = issued;
@@ -468,7 +480,7 @@ __global__ void __launch_bounds__(256, C::MINW) wf_trace(RenderArgs A, WfArgs W,
             unsigned long long x = v[i];
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
-            if ((threadIdx.x & 63) == 0 && x) atomicAdd(&base[i], x);
+            if (lane == 0 && x) atomicAdd(&base[i], x);
         }
         diag_flush(A.counters, dg);
     }
@@ -1302,7 +1314,6 @@ struct WfVariant {
     // the shadow trace of a queue wf_shade appended in chunks (its dead entries skipped); null: the build's
     // wf_shade appends per iteration
     void (*shadow_dead)(RenderArgs, WfArgs, uint32_t) = nullptr;
-    int shadow_waves = 0; // waves per SIMD of the shadow trace's grid (0: waves_per_simd)
 };
 
 // The trace configurations of the builds (traverse.hpp TraceDefaults), by what they restate.
@@ -1332,8 +1343,8 @@ struct ShadowFatLc5FdDead : ShadowFatLc5Fd { static constexpr bool DEAD = true; 
 struct ClosestFatLc5Lx : ClosestFatLc5 { static constexpr bool LX = true; };
 struct ShadowFatLc5FdLx : ShadowFatLc5Fd { static constexpr bool LX = true; };
 struct ShadowFatLc5FdDeadLx : ShadowFatLc5FdDead { static constexpr bool LX = true; };
-struct ShadowFatLc5FdLx7 : ShadowFatLc5FdLx { static constexpr int MINW = 7; };
-struct ShadowFatLc5FdDeadLx7 : ShadowFatLc5FdDeadLx { static constexpr int MINW = 7; };
+struct ClosestFatLc5LxPerf : ClosestFatLc5Lx { static constexpr bool PC = true; };
+struct ShadowFatLc5LxPerf : ClosestFatLc5LxPerf { static constexpr bool SHADOW = true; };
 struct ClosestFatLc5Perf : ClosestFatLc5 { static constexpr bool PC = true; };
 struct ShadowFatLc5Perf : ClosestFatLc5Perf { static constexpr bool SHADOW = true; };
 // the performed-work counting instances (RenderArgs::perf_counters; measurement only)
@@ -1388,12 +1399,14 @@ static const WfBuild kWf[] = {
     //     (leafcull.hpp LC_RECC: boxes on the scene's 16-bit grid, octahedral axes, half constants)
     {49, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5Fd>, 8, 8, 2, 1, 5,
           wf_trace<tc::ShadowFatLc5FdDead>}},
-    // 53 / 54: 49 whose shadow trace (53) or shadow and secondary closest traces (54) test a divergent
-    //     leaf round's masked references with the whole wave (the leaf exchange)
+    // 53 / 54 (54: the default, round 6): 49 whose shadow trace (53) or shadow and secondary closest traces
+    //     (54) test a divergent leaf round's masked references with the whole wave (the leaf exchange,
+    //     traverse.hpp leaf_exchange): sponza 2315 -> 2348 (53) / 2362 (54) Mray/s, shadow
+    //     trace 39.2 -> 38.3 ms, closest 68.9 -> 67.2 ms per launch beside it.  Measured and removed: the
+    //     shadow exchange at 7 waves per SIMD (no spills then; 2305 Mray/s) and the lane index recomputed
+    //     per use instead of held in a register (no spills at 8 waves; 2300 / 2330 Mray/s)
     {53, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5FdLx>, 8, 8, 2, 1, 5,
           wf_trace<tc::ShadowFatLc5FdDeadLx>}},
-    {55, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5>, wf_trace<tc::ShadowFatLc5FdLx7>, 8, 8, 2, 1, 5,
-          wf_trace<tc::ShadowFatLc5FdDeadLx7>, 7}},
     {54, {wf_trace_packet<8, 2, false, true>, wf_trace<tc::ClosestFatLc5Lx>, wf_trace<tc::ShadowFatLc5FdLx>, 8, 8, 2, 1, 5,
           wf_trace<tc::ShadowFatLc5FdDeadLx>}},
 };
@@ -1421,13 +1434,21 @@ static const WfVariant kWfPerf42 = {wf_trace_packet<8, 2, true, true>, wf_trace<
 // ... and build 49 (the compressed leaf cull records: the same work, half the mask bytes)
 static const WfVariant kWfPerf49 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc5Perf>,
                                     wf_trace<tc::ShadowFatLc5Perf>, 8, 8, 2, 1, 5};
+// ... and the leaf-exchange builds 53 / 54
+static const WfVariant kWfPerf53 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc5Perf>,
+                                    wf_trace<tc::ShadowFatLc5LxPerf>, 8, 8, 2, 1, 5};
+static const WfVariant kWfPerf54 = {wf_trace_packet<8, 2, true, true>, wf_trace<tc::ClosestFatLc5LxPerf>,
+                                    wf_trace<tc::ShadowFatLc5LxPerf>, 8, 8, 2, 1, 5};
 // (43 / 44 count through 40 / 42's instances: their shadow trace's short division does the same work)
 bool wf_perf_available(int variant) {
-    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 || variant == 49;
+    return variant == 18 || variant == 26 || variant == 40 || variant == 42 || variant == 43 || variant == 44 ||
+           variant == 49 || variant == 53 || variant == 54;
 }
 static const WfVariant &perf_variant(int variant) {
     return variant == 18 ? kWfPerf18
            : variant == 49 ? kWfPerf49
+           : variant == 53 ? kWfPerf53
+           : variant == 54 ? kWfPerf54
            : (variant == 40 || variant == 43) ? kWfPerf40
            : (variant == 42 || variant == 44) ? kWfPerf42
                                               : kWfPerf26;
@@ -1664,8 +1685,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
                                            : wf_build_or_ref(A.variant);
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
-    const uint32_t cblocks = blocks;
-    const uint32_t sblocks = v.shadow_waves ? blocks / (uint32_t)v.waves_per_simd * (uint32_t)v.shadow_waves : blocks;
+    const uint32_t cblocks = blocks, sblocks = blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
     const size_t lds =
@@ -1772,8 +1792,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
                                            : wf_build_or_ref(A.variant);
     uint32_t blk, blocks, tblk, tblocks;
     wf_trace_geometry(A.full_counters ? -1 : A.variant, num_cus, blk, blocks);
-    const uint32_t cblocks = blocks;
-    const uint32_t sblocks = v.shadow_waves ? blocks / (uint32_t)v.waves_per_simd * (uint32_t)v.shadow_waves : blocks;
+    const uint32_t cblocks = blocks, sblocks = blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     for (int i = 0; i < nl; i++)
         if (L[i].W.gstride < blk * blocks || L[i].W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
