@@ -284,6 +284,58 @@ def test_wavefront_trace_builds_bitexact(ca, sponza, variant):
     assert {k: gc[k] for k in ORACLE_KEYS} == oc
 
 
+def _doubled_cornell(scenes, directory):
+    """cornell_box_lit with every wall / block face given twice, the copy in another material: every ray
+    that hits a face hits two triangles at exactly the same t, and only the reference's tie rule (the
+    first in leaf order, src/kdtree.cpp:235-246) gives the oracle's colour."""
+    src = scenes.ensure("cornell_box_lit")
+    swap = {"white": "red", "red": "white", "green": "white"}
+    out, cur = [], None
+    for ln in src.read_text().splitlines():
+        if ln.startswith("mtllib"):
+            out.append("mtllib doubled.mtl")
+            continue
+        out.append(ln)
+        if ln.startswith("usemtl"):
+            cur = ln.split()[1]
+        elif ln.startswith("f ") and cur in swap:  # (the light stays single)
+            out += ["usemtl " + swap[cur], ln, "usemtl " + cur]
+    obj = directory / "doubled.obj"
+    obj.write_text("\n".join(out) + "\n")
+    (directory / "doubled.mtl").write_text(src.with_suffix(".mtl").read_text())
+    return obj
+
+
+@pytest.mark.parametrize("variant", [49, 53, 54])
+def test_leaf_exchange_ties_and_windows_bitexact(ca, po, scenes, tmp_path, variant):
+    """The leaf exchange (builds 53 / 54, traverse.hpp leaf_exchange) against the per-lane leaf loop's
+    answers: a box whose faces are all doubled (equal t, different materials: the closest reduction must
+    keep the first in mask order) with leaves of up to 24 references (kdtree-leaf-size 24), so a round's
+    pairs fill several 64-pair windows and owners carry over from one window to the next.  Counting and
+    lean builds, forced queue sorting, bit for bit against the oracle; the performed-work build of 54
+    must have run multi-window exchange rounds in both traces."""
+    rtc = scenes.config_rtc("cornell_box")
+    pair = Pair(ca, po, rtc, "input", str(_doubled_cornell(scenes, tmp_path)), "kdtree-leaf-size", "24")
+    pair.dev.set_option("kernel", 2)
+    pair.dev.set_option("variant", variant)
+    pair.dev.set_option("wf_sort", 1)
+    pair.dev.set_option("wf_sort_min", 0)
+    g, gc, o, oc = _render_both(ca, pair, 64, 48, 16)
+    assert_bitwise(g, o, "doubled box, leaf size 24, build %d" % variant)
+    assert {k: gc[k] for k in ORACLE_KEYS} == oc
+    if variant == 54:
+        pair.dev.set_option("counters", 0)
+        pair.dev.set_option("perf_counters", 1)
+        cam = pair.camera(ca, 64, 48)
+        g2 = pair.dev.render(cam, ca.render_params(64, 48, 16, 6, 0xC41A05C0, layer=1), None)
+        perf = pair.dev.perf()
+        assert_bitwise(g2, o, "doubled box, performed-work build 54")
+        for kind in ("closest", "shadow"):
+            pk = perf[kind]
+            assert pk["drounds"] > 0 and pk["diters"] > pk["drounds"], (kind, pk)  # multi-window rounds
+            assert 0 < pk["dtests"] <= pk["tests"], (kind, pk)  # every pair tested once (+ uniform leaves)
+
+
 # cameras per scene for the cull test: the config's own, one close to a surface looking along it
 # (edge-on triangles), one wide-angle from inside the geometry (triangles behind / beside the eye)
 CULL_CAMS = {
