@@ -1688,6 +1688,7 @@ int launch_wavefront_chunk(const RenderArgs &A, const WfArgs &W0, int num_cus, h
     const uint32_t cblocks = blocks, sblocks = blocks;
     wf_tail_geometry(num_cus, tblk, tblocks);
     if (W.gstride < blk * blocks || W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
+    if (blk != 256) return (int)hipErrorInvalidConfiguration; // (wf_trace's per-wave LDS of the leaf exchange)
     const size_t lds =
         (size_t)v.ring * blk * sizeof(uint2);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8; // grid-stride phases
@@ -1796,6 +1797,7 @@ int run_wavefront_lanes(const RenderArgs &A, WfLane *L, int nl, int num_cus, hip
     wf_tail_geometry(num_cus, tblk, tblocks);
     for (int i = 0; i < nl; i++)
         if (L[i].W.gstride < blk * blocks || L[i].W.gstride < tblk * tblocks) return (int)hipErrorInvalidValue;
+    if (blk != 256) return (int)hipErrorInvalidConfiguration; // (wf_trace's per-wave LDS of the leaf exchange)
     const size_t lds =
         (size_t)v.ring * blk * sizeof(uint2);
     const uint32_t sgrid = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8;
