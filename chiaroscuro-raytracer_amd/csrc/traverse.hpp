@@ -764,13 +764,14 @@ __device__ __forceinline__ uint32_t trav_round(int lc_debug, uint32_t lc_min, co
 // Here the whole wave (every lane, busy or idle) tests the round's (lane, reference) pairs 64 at a time:
 // pair i belongs to the lane whose exclusive prefix of mask popcounts is the largest one <= i, and is that
 // lane's (i - prefix)-th mask bit.  The answers are the per-lane loop's:
-//   shadow: occluded == some masked reference other than the excluded one accepts for [0, tmax] -- an OR,
+//   shadow: occluded == some masked reference other than the excluded one accepts (0 <= t < tmax) -- an OR,
 //           whatever the order (kdtree.cpp:309-320);
 //   closest: the loop keeps a hit when t < the current tmax, so it ends with the smallest t over the
 //           accepting references and, among equal t (+0 == -0), the first in mask order
 //           (kdtree.cpp:235-246); the pairs are reduced in ascending (window, lane) = mask order with a
 //           strict <, which selects the same reference, and its own ux, uy, t are taken.
-// Every lane of the wave must be active.  marks: 64 words of LDS owned by the wave.
+// Every lane of the wave must be active.  lx: 192 words of LDS owned by the wave (the window's start marks,
+// every lane's mask and first record).
 
 // the position of the q-th (from 0) set bit of m (q < popcount(m))
 __device__ __forceinline__ uint32_t nth_bit(uint32_t m, uint32_t q) {
