@@ -650,7 +650,7 @@ def run_rank(args, world, backend):
     # performed-work pass (untimed): the default trace build's kernels with counters of what they
     # actually execute and load (cr_get_perf), the same layer
     perf = None
-    if wavefront and args.variant in (-1, 18, 26, 40, 42, 43, 44, 49, 53, 54) and hasattr(dev, "perf") and not args.no_perf_pass:
+    if wavefront and args.variant in (-1, 18, 26, 40, 42, 43, 44, 49, 53, 54, 59) and hasattr(dev, "perf") and not args.no_perf_pass:
         dev.set_option("perf_counters", 1)
         if world == 1:
             dev.render_device(cam, pc, scratch.data_ptr(), stream)

@@ -161,7 +161,8 @@ void fill_args(cr_ctx *c, cr::RenderArgs &A, const cr_camera *cam, const cr_rend
     // loads instead of six): 2179 -> 2252 Mray/s at the driver's command, shadow 41.7 -> 40.0 ms;
     // 54 = 49 with the leaf exchange in the shadow and secondary closest traces (round 6: a divergent leaf
     // round's masked tests spread over the whole wave): 2315 -> 2362 Mray/s, shadow 39.2 -> 38.3 ms
-    A.variant = c->variant >= 0 ? c->variant : (c->n_tris >= LEAF_CULL_MIN_TRIS ? 54 : 44);
+    // 59 = 54 with the exchange's prefix by a DPP scan: 2348 -> 2395 Mray/s, shadow 38.4 -> 37.6 ms
+    A.variant = c->variant >= 0 ? c->variant : (c->n_tris >= LEAF_CULL_MIN_TRIS ? 59 : 44);
     A.eye_on_split = 0;
     for (int a = 0; a < 3; a++)
         if (std::binary_search(c->splits[a].begin(), c->splits[a].end(), cam->eye[a])) A.eye_on_split = 1;
@@ -212,7 +213,7 @@ int run_render(cr_ctx *c, const cr_camera *cam, const cr_render_params *p, float
                                          " does not exist (DESIGN.md §3 lists the measured builds that were removed)");
     if (c->perf_counters && (c->kernel != 2 || c->full_counters || !cr::wf_perf_available(A.variant)))
         return fail(c, CR_E_INVALID, "perf_counters: the wavefront kernel's trace builds 18, 26, 40, 42, 43, 44, "
-                                     "49 and 53-57 only, without the counting build");
+                                     "49, 53, 54 and 59 only, without the counting build");
     c->last_build = c->kernel == 2 ? (c->full_counters ? -1 : A.variant) : -2;
     HIPCHK(hipMemsetAsync(c->d_counters, 0, cr::CTR_SLOTS * sizeof(unsigned long long), st));
     {

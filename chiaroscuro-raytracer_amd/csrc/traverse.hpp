@@ -341,6 +341,7 @@ struct TraceDefaults {
     static constexpr bool PC = false;     // performed-work counters (measurement only)
     static constexpr bool DEAD = false;   // shadow queues with dead entries (wf_shade's chunked appends) skipped
     static constexpr bool LX = false;     // a divergent leaf's masked tests spread over the wave (leaf_exchange)
+    static constexpr bool LXD = false;    // LX builds: the exchange's prefix by a DPP scan
 };
 
 // A lane's deferred leaf (LX builds): the references of the leaf whose first record is `first` that its
@@ -792,7 +793,20 @@ __device__ __forceinline__ uint32_t bperm(uint32_t addr, uint32_t v) {
 __device__ __forceinline__ float bpermf(uint32_t addr, float v) { return __uint_as_float(bperm(addr, __float_as_uint(v))); }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-template <bool SHADOW>
+// Inclusive prefix sum of x over the 64 lanes of a converged wave: row scans by DPP row shifts (out-of-row
+// sources read 0), then rows 1 / 3 add lane 15 of the row below and rows 2 / 3 add lane 31.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true); // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true); // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true); // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true); // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false); // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return x;
+}
+
+// DPP: the prefix by wave_incl_scan instead of the six bit-sliced ballots
+template <bool SHADOW, bool DPP = false>
 __device__ __forceinline__ void leaf_exchange(const DevScene &S, volatile lds_u32 *lx, uint32_t m, uint32_t first,
                                               f3 o, f3 d, float tmax, uint32_t exclude, bool &occluded, bool &found,
                                               float &bx, float &by, float &bt, uint32_t &tri, Pc *pc = nullptr) {
@@ -808,11 +822,17 @@ __device__ __forceinline__ void leaf_exchange(const DevScene &S, volatile lds_u3
     }
     // exclusive prefix P of c over the lanes and the total, bit-sliced (c <= 32)
     uint32_t P = 0, total = 0;
+    if (DPP) {
+        const uint32_t inc = wave_incl_scan(c);
+        P = inc - c;
+        total = __builtin_amdgcn_readlane(inc, 63);
+    } else {
 #pragma unroll
-    for (int b = 0; b < 6; b++) {
-        const uint64_t bal = __ballot((c >> b) & 1u);
-        P += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u)) << b;
-        total += (uint32_t)__popcll(bal) << b;
+        for (int b = 0; b < 6; b++) {
+            const uint64_t bal = __ballot((c >> b) & 1u);
+            P += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u)) << b;
+            total += (uint32_t)__popcll(bal) << b;
+        }
     }
     // this lane's pairs: [P, E) (packed: one register through the exchange)
     const uint32_t pe = P | ((P + c) << 16);

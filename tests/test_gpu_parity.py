@@ -21,8 +21,8 @@ ORACLE_KEYS = ("closest", "shadow", "inner", "leaf", "tritest", "hit", "texhit",
 # trace's fallback), round 2's default 18, 26 (leaf cull records), 40 / 42 (26 / 18 with the exact
 # short division in the camera packet), 43 / 44 (40 / 42 with it in the shadow trace) and the default 49
 # (43 with the compressed leaf cull records); 53 / 54 (49 with the leaf exchange in the shadow trace, and
-# in the shadow and secondary closest traces: the default 54)
-TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44, 49, 53, 54]
+# in the shadow and secondary closest traces); the default 59 (54 with the exchange's prefix by a DPP scan)
+TRACE_BUILDS = [0, 15, 18, 26, 40, 42, 43, 44, 49, 53, 54, 59]
 VIS_DEFAULT = 1  # ctx.hpp wf_vis_dw
 SKIP_DEFAULT = 1  # ctx.hpp wf_nee_skip
 QUORUM_DEFAULT = -1  # ctx.hpp desc_quorum (8, but 0 for 1024 <= triangles < 65536)
@@ -204,7 +204,7 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, resolve
                     p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=layer)
                     g = pair.dev.render(cam, p, None)
                     gc = pair.dev.counters()
-                    assert pair.dev.last_trace_build() in (54, 44)
+                    assert pair.dev.last_trace_build() in (59, 44)
                     o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
                     assert_bitwise(g, o, "cam_fuse %d ctl_ray %d wf_paths %d layer %d" % (fuse, ctl, paths, layer))
                     assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
@@ -225,7 +225,7 @@ def test_wavefront_camera_fused_bitexact(ca, sponza, nanobox, fuse, ctl, resolve
 def test_wavefront_desc_quorum_bitexact(ca, sponza, nanobox, quorum):
     """desc_quorum q: a wave's descent round stops at a node fetch once at most q / 64 of its lanes still
     descend; those lanes keep their node and interval and descend on next round (64: after every fetch).
-    The lean builds 54 / 44, sorted queues, several layers: the same bits and query counters."""
+    The lean builds 59 / 44, sorted queues, several layers: the same bits and query counters."""
     for pair, (x, y, s) in ((sponza, (96, 54, 3)), (nanobox, (64, 48, 4))):
         pair.dev.set_option("kernel", 2)
         pair.dev.set_option("desc_quorum", quorum)
@@ -239,7 +239,7 @@ def test_wavefront_desc_quorum_bitexact(ca, sponza, nanobox, quorum):
                 p = ca.render_params(x, y, s, 6, 0xC41A05C0, layer=layer)
                 g = pair.dev.render(cam, p, None)
                 gc = pair.dev.counters()
-                assert pair.dev.last_trace_build() in (54, 44)
+                assert pair.dev.last_trace_build() in (59, 44)
                 o, oc = pair.oracle.render(cam.as_array(), x, y, s, 6, 0xC41A05C0, layer=layer, pixels=o)
                 assert_bitwise(g, o, "desc_quorum %d layer %d" % (quorum, layer))
                 assert {k: gc[k] for k in keys} == {k: oc[k] for k in keys}
@@ -306,7 +306,7 @@ def _doubled_cornell(scenes, directory):
     return obj
 
 
-@pytest.mark.parametrize("variant", [49, 53, 54])
+@pytest.mark.parametrize("variant", [49, 53, 54, 59])
 def test_leaf_exchange_ties_and_windows_bitexact(ca, po, scenes, tmp_path, variant):
     """The leaf exchange (builds 53 / 54, traverse.hpp leaf_exchange) against the per-lane leaf loop's
     answers: a box whose faces are all doubled (equal t, different materials: the closest reduction must
@@ -905,7 +905,7 @@ def test_triangle_less_scene_culling_builds(ca, po, scenes, tmp_path, variant):
     assert pair.dev.counters()["closest"] == oc["closest"] == 24 * 16 * 2
 
 
-@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44, 49, 53, 54])
+@pytest.mark.parametrize("variant", [18, 26, 40, 42, 43, 44, 49, 53, 54, 59])
 @pytest.mark.parametrize("tail_min", [0, 3000])
 def test_perf_counters_build(ca, sponza, nanobox, tail_min, variant):
     """The performed-work builds (option perf_counters: builds 18 / 26 / 40 / 42 / 43 / 44 / 49 / 53 / 54 with
@@ -972,7 +972,7 @@ def test_perf_counters_default_build_only(ca, cornell):
 
 
 def test_default_build_by_scene_size(ca, sponza, nanobox):
-    """The default trace build culls leaves (54) on the 261k-triangle sponza stand-in and not (44)
+    """The default trace build culls leaves (59) on the 261k-triangle sponza stand-in and not (44)
     on the 20k-triangle nanobox stand-in (cabi.cpp LEAF_CULL_MIN_TRIS): seen through the
     performed-work counts of the default build."""
     masks = {}
@@ -994,7 +994,7 @@ def test_default_build_by_scene_size(ca, sponza, nanobox):
         builds.append(pair.dev.last_trace_build())
         masks[name] = perf["shadow"]["masks"] + perf["closest"]["masks"] + perf["tail"]["masks"]
         # cr_last_trace_build names it: perf and lean renders the scene-size default, counting -1
-        want = 54 if name == "sponza" else 44
+        want = 59 if name == "sponza" else 44
         assert builds == [want, want, -1], (name, builds)
     assert masks["sponza"] > 0 and masks["nanobox"] == 0, masks
 
