@@ -195,3 +195,35 @@ def test_shadow_or_equals_the_per_lane_loop():
                 seq = True
                 break
         assert any(a and i != exclude for i, a in zip(ids, acc)) == seq
+
+
+def dpp_incl_scan(x):
+    """traverse.hpp wave_incl_scan as the DPP modifiers define it: row_shr:n reads lane - n of the same
+    row of 16 (0 outside it: bound_ctrl), row_bcast:15 gives rows 1 and 3 (row_mask 0xa) lane 15 of the
+    row below, row_bcast:31 gives rows 2 and 3 (row_mask 0xc) lane 31; masked-off rows add 0 (old = 0)."""
+    x = list(x)
+    for n in (1, 2, 4, 8):
+        src = [x[lane - n] if (lane % 16) >= n else 0 for lane in range(64)]
+        x = [a + b for a, b in zip(x, src)]
+    src = [x[16 * (lane // 16) - 1] if (lane // 16) in (1, 3) else 0 for lane in range(64)]
+    x = [a + b for a, b in zip(x, src)]
+    src = [x[31] if (lane // 16) in (2, 3) else 0 for lane in range(64)]
+    return [a + b for a, b in zip(x, src)]
+
+
+def test_dpp_prefix_equals_the_ballot_prefix():
+    """Build 59's prefix (the inclusive DPP scan minus the lane's own count) against the bit-sliced
+    ballot prefix of builds 53 / 54 and a plain running sum."""
+    rng = random.Random(11)
+    for _ in range(3000):
+        c = [rng.choice([0, 0, 1, 2, 5, 16, 32, rng.randint(0, 32)]) for _ in range(64)]
+        inc = dpp_incl_scan(c)
+        P_dpp = [i - ci for i, ci in zip(inc, c)]
+        P_bal = [0] * 64
+        for b in range(6):
+            bal = ballot([(ci >> b) & 1 for ci in c])
+            for lane in range(64):
+                P_bal[lane] += mbcnt(bal, lane) << b
+        run = [sum(c[:lane]) for lane in range(64)]
+        assert P_dpp == P_bal == run
+        assert inc[63] == sum(c)
