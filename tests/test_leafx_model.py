@@ -1,4 +1,4 @@
-"""CPU model check of the leaf exchange (trace builds 53 / 54, csrc/traverse.hpp leaf_exchange).
+"""CPU model check of the leaf exchange (trace builds 53 / 54 / 59, csrc/traverse.hpp leaf_exchange).
 
 The exchange hands a wave's (lane, reference) pairs of one divergent leaf round to the 64 lanes, 64 at a
 time.  This restates its index arithmetic operation for operation -- the bit-sliced exclusive prefix of
